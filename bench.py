@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident N-client FedAvg fp32 reduction (aggregated GB/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5|c4] [--variant V]
+                    [--sweep] [--no-cpu-baseline]
+
+One "step" = one aggregation round over one batch already resident in HBM:
+the fa_fedavg_f32 fold of [N_clients x P] -> [P] (stall-aware for c5, bf16 for
+c4), plus, at world size > 1, the RCCL all-gather of every rank's output
+bucket over xGMI (the one real exchange step of the path: SURVEY 8e).
+
+Default workload = BASELINE config 3: 1024 clients x 10,000,000 fp32 params on
+ONE GPU.  With --gpus N (torch.distributed.run, one process per GPU) every rank
+owns its own 10M-param bucket of a 10M*N-param model (weak scaling) and the
+global model is reassembled by all_gather_into_tensor.
+
+Inputs: integer-exact synthetic generator (fedlesscan_amd/synth.py), generated
+directly in HBM by fa_synth_*; random-init, no dataset.  Rank 0 at N=1 also
+times the CPU oracle on a bounded column sample of the same workload and
+checks the GPU output on that sample bit-for-bit.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from fedlesscan_amd import _lib, synth  # noqa: E402
+from fedlesscan_amd.engine import Factors  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (clients, params per rank, dtype, scored, seed, card_hi, description)
+    "c2": (100, 1_000_000, "f32", False, 2, 600, "100 clients x 1M fp32 FedAvg, 1 MI355X (BASELINE config 2)"),
+    "c3": (1024, 10_000_000, "f32", False, 3, 600,
+           "1024 clients x 10M fp32 FedAvg, device-resident (BASELINE config 3, headline)"),
+    "c4": (256, 12_500_000, "bf16", False, 4, 600,
+           "256 clients x 100M bf16, one 12.5M-param bucket per GPU (BASELINE config 4 shard)"),
+    "c5": (512, 25_000_000, "f32", True, 5, 2000,
+           "512 clients x 25M fp32 FedLesScan stall-aware, tolerance 2, R=10 (BASELINE config 5)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cols", type=int, default=1 << 20, help="columns in the CPU baseline sample")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device("cuda", torch.cuda.current_device())
+
+
+class Workload:
+    def __init__(self, cfg, rank, dev):
+        self.N, self.P, self.dtype, self.scored, self.seed, card_hi, self.desc = cfg
+        self.rank, self.dev = rank, dev
+        L = _lib.load()
+        st = torch.cuda.current_stream(dev).cuda_stream
+        tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
+        self.X = torch.empty((self.N, self.P), dtype=tdt, device=dev)
+        col0 = rank * self.P  # this rank's parameter bucket of the global model
+        gen = L.fa_synth_f32 if self.dtype == "f32" else L.fa_synth_bf16
+        _lib.check(gen(self.X.data_ptr(), self.N, self.P, self.P, self.seed, 0, col0, st), "synth")
+        self.col0 = col0
+        self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
+        self.scores = ([(r + 1) / 11 for r in synth.round_ids(self.seed, self.N, 10, 2)]
+                       if self.scored else None)
+        f = Factors(self.weights, self.scores, np.dtype(np.float32))
+        self.a, self.s = f.to(dev)
+        self.div = float(f.div)
+        self.out = torch.empty(self.P, dtype=torch.float32, device=dev)
+        elt = 4 if self.dtype == "f32" else 2
+        # algorithmic bytes per launch: every input element once + the fp32 output once
+        self.bytes = self.N * self.P * elt + self.P * 4
+        torch.cuda.synchronize()
+
+    def launch(self, variant=0):
+        L = _lib.load()
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        s = None if self.s is None else self.s.data_ptr()
+        if self.dtype == "f32":
+            rc = L.fa_fedavg_f32_variant(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s,
+                                         self.div, self.out.data_ptr(), st, variant)
+        else:
+            rc = L.fa_fedavg_bf16(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s, self.div,
+                                  self.out.data_ptr(), None, st)
+        if rc:
+            _lib.check(rc, "fold")
+
+
+def cpu_baseline(wl: Workload, ncols: int):
+    """Oracle on host cores over a bounded column sample of the same workload."""
+    from oracle import fedavg_oracle as O  # checker / CPU baseline only
+    from oracle import oracle_lib as OL
+    ncols = min(ncols, wl.P)
+    t0 = time.time()
+    Xh = OL.synth_f32(wl.seed, wl.N, ncols, col0=wl.col0) if wl.dtype == "f32" else \
+        synth.bf16_bits_to_f32(OL.synth_bf16(wl.seed, wl.N, ncols, col0=wl.col0))
+    gen_s = time.time() - t0
+    sample_bytes = wl.N * ncols * (4 if wl.dtype == "f32" else 2) + ncols * 4
+    # (i) literal numpy restatement of fed_avg_aggregator.py:24-42 (1 core: numpy ufuncs are single-threaded)
+    params = [[Xh[i]] for i in range(wl.N)]
+    t0 = time.perf_counter()
+    if wl.scored:
+        ref = O.stall_aware_literal([{"round_id": r} for r in synth.round_ids(wl.seed, wl.N, 10, 2)], 10,
+                                    params, wl.weights)[0]
+    else:
+        ref = O.fedavg_literal(params, wl.weights)[0]
+    t_np = time.perf_counter() - t0
+    del params
+    # (ii) bit-identical C restatement, OpenMP over all host cores
+    threads = OL.max_threads()
+    a = np.array(wl.weights, np.float32)
+    s = None if wl.scores is None else np.array(wl.scores, np.float32)
+    t_omp = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ref_omp = OL.fedavg_f32(Xh, a, np.float32(wl.div), s=s, nthreads=threads)
+        t_omp.append(time.perf_counter() - t0)
+    gpu = wl.out[:ncols].cpu().numpy()
+    exact = bool(np.array_equal(gpu.view(np.uint32), ref.view(np.uint32)) and
+                 np.array_equal(ref_omp.view(np.uint32), ref.view(np.uint32)))
+    return {
+        "value": round(sample_bytes / t_np / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+        "sample": f"{wl.N} clients x first {ncols} params of the same workload; numpy literal restatement "
+                  f"of fed_avg_aggregator.py:24-42 (1 core, numpy ufuncs single-threaded), {t_np:.2f} s",
+        "omp": {"value": round(sample_bytes / min(t_omp) / 1e9, 3), "unit": "GB/s", "cores": threads,
+                "kind": "port", "impl": "oracle/fedavg_ref.c (bit-identical, OpenMP)"},
+        "host_cpus_visible": len(os.sched_getaffinity(0)),
+        "sample_bit_exact_vs_gpu": exact,
+        "gen_s": round(gen_s, 2),
+    }
+
+
+def read_traffic(config: str):
+    """PMC HBM bytes per launch measured by the committed rocprofv3 pass (profiles/)."""
+    p = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, REPO)
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    if args.gpus != world and world > 1:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+    cfg = CONFIGS[args.config]
+    wl = Workload(cfg, rank, dev)
+    L = _lib.load()
+    gathered = torch.empty(world * wl.P, dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    if args.sweep and rank == 0:
+        nvar = L.fa_num_variants() if wl.dtype == "f32" else 1
+        res = {v: [] for v in range(nvar)}
+        for _ in range(2):
+            for v in range(nvar):
+                wl.launch(v)
+        for _ in range(max(args.steps, 5)):
+            for v in range(nvar):  # interleaved rounds in one process
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                wl.launch(v)
+                e1.record(stream)
+                e1.synchronize()
+                res[v].append(e0.elapsed_time(e1))
+        for v, ts in res.items():
+            ts = sorted(ts)
+            log(f"variant {v} {L.fa_variant_name(v).decode():10s} median {ts[len(ts)//2]:.3f} ms  "
+                f"min {ts[0]:.3f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
+
+    def step(events=None):
+        if events is not None:
+            events[0].record(stream)
+        wl.launch(args.variant)
+        if events is not None:
+            events[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, wl.out)
+
+    for _ in range(args.warmup):
+        step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    kern_avg = float(np.mean(kern_ms))
+    if world > 1:
+        t = torch.tensor([kern_avg], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        kern_avg = float(t.item())
+
+    total_bytes = world * wl.bytes * args.steps
+    value = total_bytes / elapsed / 1e9
+    achieved = wl.bytes / (kern_avg * 1e-3) / 1e9
+    traffic, traffic_src = read_traffic(args.config)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(wl, args.cpu_cols)
+        except Exception as e:  # the baseline must never hide the GPU result
+            cpu = {"error": repr(e)}
+    if rank == 0:
+        line = {
+            "metric": "aggregated GB/s (device-resident) — N-client FedAvg fp32 reduction",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if wl.dtype == "f32" else "bf16-in/f32-acc",
+            "data": "synthetic (integer-exact splitmix64 generator, generated in HBM)",
+            "config": {
+                "workload": cfg[6],
+                "clients": wl.N,
+                "params_per_gpu": wl.P,
+                "params_total": wl.P * world,
+                "layout": "row-stacked [clients][params] fp32 in HBM",
+                "parallelism": f"param-bucket x{world}" + (" + RCCL all_gather" if world > 1 else ""),
+                "variant": L.fa_variant_name(args.variant).decode() if wl.dtype == "f32" else "bf16_v8u8",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel_ms_avg": round(kern_avg, 4),
+                "bytes_per_launch": wl.bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+"""FedAvg strategies on the MI355X engine.
+
+Drop-in for fedless/aggregator/fed_avg_aggregator.py:
+  FedAvgAggregator._aggregate                  :24-42   -> engine.aggregate_layers (HIP fold)
+  FedAvgAggregator.select_aggregation_candidates :44-55
+  FedAvgAggregator.aggregate                   :57-92
+  StreamFedAvgAggregator.chunks / .aggregate   :95-153
+
+Same constructor signatures, argument meaning, return types and exceptions.
+`select_aggregation_candidates` takes a result store with the ClientResultDao
+query methods (fedlesscan_amd.store.InMemoryClientResultStore) where the
+reference takes a pymongo client.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Iterable, Iterator, List, Optional, Tuple
+
+import numpy as np
+
+from .. import engine
+from ..common.models import ClientResult, Parameters, TestMetrics
+from ..common.serialization import deserialize_parameters
+from .exceptions import InsufficientClientResults, UnknownCardinalityError
+from .parameter_aggregator import ParameterAggregator
+
+logger = logging.getLogger(__name__)
+
+# tf.data.UNKNOWN_CARDINALITY / tf.data.INFINITE_CARDINALITY
+UNKNOWN_CARDINALITY = -2
+INFINITE_CARDINALITY = -1
+
+
+def resolve_cardinality(cardinality, default_cardinality):
+    """fed_avg_aggregator.py:71-82.  Note the reference's `if not default`:
+    a default of 0 / 0.0 counts as "no default" (SURVEY App. C.8)."""
+    if cardinality in (UNKNOWN_CARDINALITY, INFINITE_CARDINALITY):
+        if not default_cardinality:
+            raise UnknownCardinalityError("Cardinality for client result invalid. ")
+        return default_cardinality
+    return cardinality
+
+
+def decode_result(result: ClientResult, default_cardinality):
+    """Deserialize one ClientResult and release its blob (`del client_result.parameters`)."""
+    params = deserialize_parameters(result.parameters)
+    result.parameters = None
+    return params, resolve_cardinality(result.cardinality, default_cardinality), result.test_metrics
+
+
+def decode_results(results: Iterable[ClientResult], default_cardinality):
+    params, cards, metrics = [], [], []
+    for r in results:
+        p, c, m = decode_result(r, default_cardinality)
+        params.append(p)
+        cards.append(c)
+        if m:
+            metrics.append(m)
+    return params, cards, metrics
+
+
+def chunked(items: Iterable, n: int) -> Iterator[list]:
+    """Full chunks of n, then the remainder (fed_avg_aggregator.py:99-109)."""
+    buf: list = []
+    for el in items:
+        buf.append(el)
+        if len(buf) == n:
+            yield buf
+            buf = []
+    if buf:
+        yield buf
+
+
+class FedAvgAggregator(ParameterAggregator):
+    """Cardinality-weighted FedAvg; the fold runs in libfedavg_hip.so."""
+
+    def __init__(self, device=None):
+        self.device = device
+
+    def _aggregate(self, parameters: List[List[np.ndarray]], weights: List[float]) -> List[np.ndarray]:
+        return engine.aggregate_layers(parameters, weights, None, device=self.device)
+
+    def select_aggregation_candidates(self, store, session_id, round_id):
+        dicts, candidates = store.load_results_for_round(session_id=session_id, round_id=round_id)
+        if not dicts:
+            raise InsufficientClientResults(
+                f"Found no client results for session {session_id} and round {round_id}")
+        return dicts, candidates
+
+    def aggregate(self, client_results: Iterator[ClientResult], client_feats: Optional[List[dict]] = None,
+                  default_cardinality: Optional[float] = None) -> Tuple[Parameters, Optional[List[TestMetrics]]]:
+        params, cards, metrics = decode_results(client_results, default_cardinality)
+        return self._aggregate(params, cards), (metrics or None)
+
+
+class StreamFedAvgAggregator(FedAvgAggregator):
+    """Online FedAvg over chunks: g <- FedAvg([g, *chunk], [W, *n_chunk]).
+
+    Reproduces the reference's running re-weighting exactly (it is not
+    bit-equal to batch FedAvg)."""
+
+    def __init__(self, chunk_size: int = 25, device=None):
+        super().__init__(device)
+        self.chunk_size = chunk_size
+
+    def chunks(self, iterator: Iterator, n) -> Iterator[List]:
+        return chunked(iterator, n)
+
+    def aggregate(self, client_results: Iterator[ClientResult], client_feats: Optional[List[dict]] = None,
+                  default_cardinality: Optional[float] = None) -> Tuple[Parameters, Optional[List[TestMetrics]]]:
+        g, w_seen, metrics = None, 0, []
+        for chunk in self.chunks(client_results, self.chunk_size):
+            params, cards, m = decode_results(chunk, default_cardinality)
+            metrics.extend(m)
+            if g is None:
+                g = self._aggregate(params, cards)
+            else:
+                g = self._aggregate([g, *params], [w_seen, *cards])
+            w_seen += sum(cards)
+        return g, (metrics or None)

@@ -1,0 +1,618 @@
+// libfedavg_hip.so — MI355X (gfx950, CDNA4) FedAvg / FedLesScan aggregation.
+//
+// Hot path replaced (reference, all numpy on one CPU core):
+//   fedless/aggregator/fed_avg_aggregator.py:24-42        FedAvgAggregator._aggregate
+//   fedless/aggregator/stall_aware_aggregation.py:42-67   StallAwareAggregator._aggregate
+//
+// The op is a bandwidth-bound weighted column reduction over a row-stacked
+// [N clients][ldx] matrix: 2-3 FLOP per 4-byte element, far below any MFMA
+// ridge, so it runs on the VALU and the design goal is HBM read bandwidth.
+//
+// Bit-exactness contract: every output column is owned by
+// ONE lane, which folds clients 0..N-1 strictly in order with a separate
+// multiply and add (no FMA: this TU is compiled with fp-contract off) and
+// finishes with an IEEE divide.  No split-N, tree or atomic reassociation.
+//
+// Parallelism comes from the columns: lane = 4 consecutive fp32 columns
+// (one 16-byte global_load_dwordx4 per client row), a 64-lane wave reads
+// 1 KiB contiguous per row, a 256-thread block 4 KiB per row.  Memory-level
+// parallelism comes from unrolling U independent client-row loads ahead of
+// the in-order adds (the loads are independent, only the adds are ordered).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "fedavg_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+constexpr int kBlock = 256;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const f32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+__device__ __forceinline__ f32x4 scale4(f32x4 x, float a) { return x * a; }
+__device__ __forceinline__ f32x4 add4(f32x4 x, f32x4 y) { return x + y; }
+__device__ __forceinline__ f32x4 div4(f32x4 x, float d) { return x / d; }
+
+// t_i = fl(fl(x*a) * s): two roundings, left-to-right like `layer * n * s`.
+template <bool SCORED>
+__device__ __forceinline__ f32x4 term4(f32x4 x, float a, float s) {
+    f32x4 t = scale4(x, a);
+    if constexpr (SCORED) t = scale4(t, s);
+    return t;
+}
+template <bool SCORED>
+__device__ __forceinline__ float term1(float x, float a, float s) {
+    float t = x * a;
+    if constexpr (SCORED) t = t * s;
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// fp32 fold over a stacked matrix, 16 B per lane per client row.
+//   X4   : [N][ldq] f32x4 (ldq = ldx/4), 16-byte aligned rows
+//   nq   : full f32x4 quads per row (P/4); a trailing P%4 tail is folded by
+//          the lane q == nq with scalar loads (one wave diverges, once).
+// Template: U = client rows loaded ahead of the ordered adds; NT = non-temporal
+// (read-once) loads; SCORED = stall-aware second multiply; ACC = continue a
+// fold from acc_in; FIN = divide at the end.
+// ---------------------------------------------------------------------------
+template <int U, bool NT, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* __restrict__ acc_in, float divisor, float* __restrict__ out) {
+    const int64_t nq = P >> 2;
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q < nq) {
+        const int64_t ldq = ldx >> 2;
+        const f32x4* __restrict__ p = reinterpret_cast<const f32x4*>(X) + q;
+        f32x4 acc;
+        int64_t i = 0;
+        if constexpr (ACC) {
+            acc = reinterpret_cast<const f32x4*>(acc_in)[q];
+        } else {
+            acc = term4<SCORED>(ld4<NT>(p), a[0], SCORED ? s[0] : 1.0f);
+            i = 1;
+        }
+        for (; i + U <= N; i += U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld4<NT>(p + (i + u) * ldq);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
+        }
+        for (; i < N; ++i)
+            acc = add4(acc, term4<SCORED>(ld4<NT>(p + i * ldq), a[i], SCORED ? s[i] : 1.0f));
+        if constexpr (FIN) acc = div4(acc, divisor);
+        reinterpret_cast<f32x4*>(out)[q] = acc;
+    } else if (q == nq && (P & 3)) {
+        // column tail: at most 3 columns, scalar loads, same order
+        for (int64_t c = nq * 4; c < P; ++c) {
+            float acc;
+            int64_t i = 0;
+            if constexpr (ACC) {
+                acc = acc_in[c];
+            } else {
+                acc = term1<SCORED>(X[c], a[0], SCORED ? s[0] : 1.0f);
+                i = 1;
+            }
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + c], a[i], SCORED ? s[i] : 1.0f);
+            if constexpr (FIN) acc = acc / divisor;
+            out[c] = acc;
+        }
+    }
+}
+
+// One column per lane, any alignment / stride (fallback for unaligned input).
+template <bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* __restrict__ acc_in, float divisor, float* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    float acc;
+    int64_t i = 0;
+    if constexpr (ACC) {
+        acc = acc_in[c];
+    } else {
+        acc = term1<SCORED>(X[c], a[0], SCORED ? s[0] : 1.0f);
+        i = 1;
+    }
+#pragma unroll 8
+    for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + c], a[i], SCORED ? s[i] : 1.0f);
+    if constexpr (FIN) acc = acc / divisor;
+    out[c] = acc;
+}
+
+// List-of-rows form: xi[i] = device pointer to client i's P floats.  The row
+// alignment test is wave-uniform (every lane reads the same pointer).
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f32_ptrs(
+    const float* const* __restrict__ xi, int64_t N, int64_t P,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t c0 = q * 4;
+    if (c0 >= P) return;
+    const int w = (P - c0) >= 4 ? 4 : (int)(P - c0);
+    float acc[4];
+    for (int64_t i = 0; i < N; ++i) {
+        const float* row = xi[i];
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (w == 4 && aligned16(row)) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
+            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+        } else {
+            for (int k = 0; k < w; ++k) x[k] = row[c0 + k];
+        }
+        const float ai = a[i];
+        const float si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float t = term1<SCORED>(x[k], ai, si);
+            acc[k] = (i == 0) ? t : acc[k] + t;
+        }
+    }
+    if (w == 4 && aligned16(out)) {
+        reinterpret_cast<f32x4*>(out + c0)[0] =
+            f32x4{acc[0] / divisor, acc[1] / divisor, acc[2] / divisor, acc[3] / divisor};
+    } else {
+        for (int k = 0; k < w; ++k) out[c0 + k] = acc[k] / divisor;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bf16: 8 columns per lane (one 16-byte load per row), exact upcast, f32 fold.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f != f) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <int U, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb) {
+    const int64_t no = P >> 3;  // full octets
+    const int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (o < no) {
+        const int64_t ldo = ldx >> 3;
+        const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(X) + o;
+        float acc[8];
+        {
+            u32x4 v = __builtin_nontemporal_load(p);
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc[2 * k] = term1<SCORED>(bf2f(w[k] & 0xFFFFu), a0, s0);
+                acc[2 * k + 1] = term1<SCORED>(bf2f(w[k] >> 16), a0, s0);
+            }
+        }
+        int64_t i = 1;
+        for (; i + U <= N; i += U) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldo);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    acc[2 * k] = acc[2 * k] + term1<SCORED>(bf2f(w[k] & 0xFFFFu), ai, si);
+                    acc[2 * k + 1] = acc[2 * k + 1] + term1<SCORED>(bf2f(w[k] >> 16), ai, si);
+                }
+            }
+        }
+        for (; i < N; ++i) {
+            u32x4 v = __builtin_nontemporal_load(p + i * ldo);
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc[2 * k] = acc[2 * k] + term1<SCORED>(bf2f(w[k] & 0xFFFFu), ai, si);
+                acc[2 * k + 1] = acc[2 * k + 1] + term1<SCORED>(bf2f(w[k] >> 16), ai, si);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = acc[k] / divisor;
+        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * o;
+        o4[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+        o4[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+        if (outb) {
+            u32x4 b;
+            b.x = (uint32_t)f2bf_rne(acc[0]) | ((uint32_t)f2bf_rne(acc[1]) << 16);
+            b.y = (uint32_t)f2bf_rne(acc[2]) | ((uint32_t)f2bf_rne(acc[3]) << 16);
+            b.z = (uint32_t)f2bf_rne(acc[4]) | ((uint32_t)f2bf_rne(acc[5]) << 16);
+            b.w = (uint32_t)f2bf_rne(acc[6]) | ((uint32_t)f2bf_rne(acc[7]) << 16);
+            reinterpret_cast<u32x4*>(outb)[o] = b;
+        }
+    } else if (o == no && (P & 7)) {
+        for (int64_t c = no * 8; c < P; ++c) {
+            float acc = term1<SCORED>(bf2f(X[c]), a[0], SCORED ? s[0] : 1.0f);
+            for (int64_t i = 1; i < N; ++i)
+                acc = acc + term1<SCORED>(bf2f(X[i * ldx + c]), a[i], SCORED ? s[i] : 1.0f);
+            acc = acc / divisor;
+            out[c] = acc;
+            if (outb) outb[c] = f2bf_rne(acc);
+        }
+    }
+}
+
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_scalar(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    float acc = term1<SCORED>(bf2f(X[c]), a[0], SCORED ? s[0] : 1.0f);
+    for (int64_t i = 1; i < N; ++i)
+        acc = acc + term1<SCORED>(bf2f(X[i * ldx + c]), a[i], SCORED ? s[i] : 1.0f);
+    acc = acc / divisor;
+    out[c] = acc;
+    if (outb) outb[c] = f2bf_rne(acc);
+}
+
+// ---------------------------------------------------------------------------
+// float64 and integer folds: one column per lane, coalesced 8-byte loads.
+// ---------------------------------------------------------------------------
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f64(
+    const double* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const double* __restrict__ a, const double* __restrict__ s, double divisor,
+    double* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    double acc = X[c] * a[0];
+    if constexpr (SCORED) acc = acc * s[0];
+#pragma unroll 8
+    for (int64_t i = 1; i < N; ++i) {
+        double t = X[i * ldx + c] * a[i];
+        if constexpr (SCORED) t = t * s[i];
+        acc = acc + t;
+    }
+    out[c] = acc / divisor;
+}
+
+// numpy integer semantics: product and fold in the input dtype with
+// two's-complement wrap (computed unsigned to avoid C++ UB), then
+// true_divide -> float64(acc) / float64(total).
+template <typename T, typename UT>
+__global__ __launch_bounds__(kBlock) void k_fedavg_int(
+    const T* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const int64_t* __restrict__ a, double divisor, double* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    UT acc = 0;
+    for (int64_t i = 0; i < N; ++i) {
+        UT t = (UT)X[i * ldx + c] * (UT)(T)a[i];
+        acc = (i == 0) ? t : (UT)(acc + t);
+    }
+    out[c] = (double)(T)acc / divisor;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic generator (bit-identical to fedlesscan_amd/synth.py)
+// ---------------------------------------------------------------------------
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float synth_value(uint64_t key, int64_t col) {
+    uint64_t h = mix64(key + (uint64_t)(col + 1) * kGolden);
+    int64_t v = (int64_t)(h & 0x1FFFFF) + (int64_t)((h >> 21) & 0x1FFFFF) +
+                (int64_t)((h >> 42) & 0x1FFFFF) - 3 * (1 << 20);
+    return (float)v * 0x1p-24f;
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(kBlock) void k_synth(OutT* __restrict__ X, int64_t nrows, int64_t ncols,
+                                                   int64_t ldx, uint64_t seed, int64_t row0, int64_t col0) {
+    const int64_t total = nrows * ncols;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = e / ncols;
+        const int64_t c = e - r * ncols;
+        const uint64_t key = mix64((seed * kGolden) ^ mix64((uint64_t)(row0 + r) + 1));
+        const float v = synth_value(key, col0 + c);
+        if constexpr (sizeof(OutT) == 4) X[r * ldx + c] = v;
+        else X[r * ldx + c] = f2bf_rne(v);
+    }
+}
+
+// contiguous streaming read (calibration ceiling for the fold)
+__global__ __launch_bounds__(kBlock) void k_read_sweep(const f32x4* __restrict__ X, int64_t nq,
+                                                        float* __restrict__ sink) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq;
+         q += (int64_t)gridDim.x * kBlock) {
+        f32x4 v = __builtin_nontemporal_load(X + q);
+        acc = add4(acc, v);
+    }
+    float t = acc.x + acc.y + acc.z + acc.w;
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    __shared__ float red[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) sink[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+inline dim3 grid_for(int64_t lanes) { return dim3((unsigned)((lanes + kBlock - 1) / kBlock)); }
+
+int check_common(int64_t N, int64_t P, int64_t ldx, const void* X, const void* a, const void* out) {
+    if (N < 0 || P < 0) return fail(FA_ERR_ARG, "negative size (N=%lld, P=%lld)", (long long)N, (long long)P);
+    if (N == 0) return fail(FA_ERR_NO_CLIENTS, "no client results to aggregate (N == 0)");
+    if (ldx < P) return fail(FA_ERR_SHAPE, "row pitch ldx=%lld < P=%lld", (long long)ldx, (long long)P);
+    if (P > 0 && (!X || !a || !out)) return fail(FA_ERR_ARG, "null X/a/out pointer");
+    if ((P + 4 * (int64_t)kBlock) / (4 * (int64_t)kBlock) > (int64_t)0x7FFFFFFF)
+        return fail(FA_ERR_ARG, "P too large for one launch");
+    return FA_OK;
+}
+
+struct F32Variant {
+    const char* name;
+    int unroll;
+    bool nt;
+};
+// variant 0 is the shipped default (chosen from the on-device sweep)
+constexpr F32Variant kVariants[] = {
+    {"v4u16nt", 16, true}, {"v4u8nt", 8, true}, {"v4u16", 16, false},
+    {"v4u8", 8, false},    {"v4u4nt", 4, true}, {"v4u32nt", 32, true},
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int U, bool NT, bool SC, bool ACC, bool FIN>
+void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+               const float* s, const float* acc_in, float d, float* out) {
+    hipLaunchKernelGGL((k_fold_f32_v4<U, NT, SC, ACC, FIN>), grid_for((P >> 2) + 1), dim3(kBlock), 0,
+                       st, X, N, P, ldx, a, s, acc_in, d, out);
+}
+
+template <int U, bool NT>
+void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+#define FA_V4(SC, ACC, FIN) launch_v4<U, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out)
+    if (sc) {
+        if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
+        else     { if (fin) FA_V4(true, false, true); else FA_V4(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_V4(false, true, true); else FA_V4(false, true, false); }
+        else     { if (fin) FA_V4(false, false, true); else FA_V4(false, false, false); }
+    }
+#undef FA_V4
+}
+
+template <bool SC, bool ACC, bool FIN>
+void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                   const float* s, const float* acc_in, float d, float* out) {
+    hipLaunchKernelGGL((k_fold_f32_scalar<SC, ACC, FIN>), grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx,
+                       a, s, acc_in, d, out);
+}
+
+int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+             const float* acc_in, float divisor, int finalize, float* out, void* stream, int variant) {
+    // With acc_in, N == 0 is a valid "finalize only" call.
+    if (!(acc_in && N == 0)) {
+        int rc = check_common(N, P, ldx, X, a, out);
+        if (rc) return rc;
+    } else if (P > 0 && !out) {
+        return fail(FA_ERR_ARG, "null out pointer");
+    }
+    if (variant < 0 || variant >= kNumVariants) return fail(FA_ERR_ARG, "unknown variant %d", variant);
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    const bool sc = s != nullptr, acc = acc_in != nullptr, fin = finalize != 0;
+    const bool vec = (N == 0 || aligned16(X)) && (ldx % 4 == 0) && aligned16(out) &&
+                     (!acc || aligned16(acc_in));
+    if (!vec) {
+#define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
+        if (sc) {
+            if (acc) { if (fin) FA_SC(true, true, true); else FA_SC(true, true, false); }
+            else     { if (fin) FA_SC(true, false, true); else FA_SC(true, false, false); }
+        } else {
+            if (acc) { if (fin) FA_SC(false, true, true); else FA_SC(false, true, false); }
+            else     { if (fin) FA_SC(false, false, true); else FA_SC(false, false, false); }
+        }
+#undef FA_SC
+        return check_launch("k_fold_f32_scalar");
+    }
+    const F32Variant& v = kVariants[variant];
+#define FA_VF(U, NT) launch_v4_flags<U, NT>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+    if (v.nt) {
+        switch (v.unroll) {
+            case 4: FA_VF(4, true); break;
+            case 8: FA_VF(8, true); break;
+            case 16: FA_VF(16, true); break;
+            default: FA_VF(32, true); break;
+        }
+    } else {
+        switch (v.unroll) {
+            case 8: FA_VF(8, false); break;
+            default: FA_VF(16, false); break;
+        }
+    }
+#undef FA_VF
+    return check_launch("k_fold_f32_v4");
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int fa_abi_version(void) { return FA_ABI_VERSION; }
+const char* fa_last_error(void) { return g_err; }
+int fa_num_variants(void) { return kNumVariants; }
+const char* fa_variant_name(int variant) {
+    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant].name : "";
+}
+
+int fa_fedavg_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                  float divisor, float* out, void* stream) {
+    return fold_f32(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream, 0);
+}
+
+int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                          const float* s, float divisor, float* out, void* stream, int variant) {
+    return fold_f32(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream, variant);
+}
+
+int fa_fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                const float* acc_in, float divisor, int finalize, float* out, void* stream) {
+    return fold_f32(X, N, P, ldx, a, s, acc_in, divisor, finalize, out, stream, 0);
+}
+
+int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                       float divisor, float* out, void* stream) {
+    int rc = check_common(N, P, P, xi, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    if (s)
+        hipLaunchKernelGGL(k_fedavg_f32_ptrs<true>, grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P, a,
+                           s, divisor, out);
+    else
+        hipLaunchKernelGGL(k_fedavg_f32_ptrs<false>, grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P,
+                           a, s, divisor, out);
+    return check_launch("k_fedavg_f32_ptrs");
+}
+
+int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                   float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out_f32);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && (!out_bf16 || aligned16(out_bf16));
+    if (vec) {
+        if (s)
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<8, true>), grid_for((P >> 3) + 1), dim3(kBlock), 0, st, X, N,
+                               P, ldx, a, s, divisor, out_f32, out_bf16);
+        else
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<8, false>), grid_for((P >> 3) + 1), dim3(kBlock), 0, st, X,
+                               N, P, ldx, a, s, divisor, out_f32, out_bf16);
+        return check_launch("k_fedavg_bf16_v8");
+    }
+    if (s)
+        hipLaunchKernelGGL(k_fedavg_bf16_scalar<true>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
+                           divisor, out_f32, out_bf16);
+    else
+        hipLaunchKernelGGL(k_fedavg_bf16_scalar<false>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
+                           divisor, out_f32, out_bf16);
+    return check_launch("k_fedavg_bf16_scalar");
+}
+
+int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const double* a, const double* s,
+                  double divisor, double* out, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    if (s)
+        hipLaunchKernelGGL(k_fedavg_f64<true>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s, divisor,
+                           out);
+    else
+        hipLaunchKernelGGL(k_fedavg_f64<false>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s, divisor,
+                           out);
+    return check_launch("k_fedavg_f64");
+}
+
+int fa_fedavg_i32(const int32_t* X, int64_t N, int64_t P, int64_t ldx, const int64_t* a, double divisor,
+                  double* out, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipLaunchKernelGGL((k_fedavg_int<int32_t, uint32_t>), grid_for(P), dim3(kBlock), 0, (hipStream_t)stream,
+                       X, N, P, ldx, a, divisor, out);
+    return check_launch("k_fedavg_int<int32>");
+}
+
+int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx, const int64_t* a, double divisor,
+                  double* out, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipLaunchKernelGGL((k_fedavg_int<int64_t, uint64_t>), grid_for(P), dim3(kBlock), 0, (hipStream_t)stream,
+                       X, N, P, ldx, a, divisor, out);
+    return check_launch("k_fedavg_int<int64>");
+}
+
+int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed, int64_t row0,
+                 int64_t col0, void* stream) {
+    if (nrows < 0 || ncols < 0 || ldx < ncols) return fail(FA_ERR_ARG, "bad synth shape");
+    if (nrows == 0 || ncols == 0) { g_err[0] = 0; return FA_OK; }
+    if (!X) return fail(FA_ERR_ARG, "null X");
+    hipLaunchKernelGGL(k_synth<float>, dim3(8192), dim3(kBlock), 0, (hipStream_t)stream, X, nrows, ncols, ldx,
+                       seed, row0, col0);
+    return check_launch("k_synth<f32>");
+}
+
+int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed, int64_t row0,
+                  int64_t col0, void* stream) {
+    if (nrows < 0 || ncols < 0 || ldx < ncols) return fail(FA_ERR_ARG, "bad synth shape");
+    if (nrows == 0 || ncols == 0) { g_err[0] = 0; return FA_OK; }
+    if (!X) return fail(FA_ERR_ARG, "null X");
+    hipLaunchKernelGGL(k_synth<uint16_t>, dim3(8192), dim3(kBlock), 0, (hipStream_t)stream, X, nrows, ncols,
+                       ldx, seed, row0, col0);
+    return check_launch("k_synth<bf16>");
+}
+
+int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream) {
+    if (n < 0 || !X || !sink || sink_len <= 0 || !aligned16(X) || (n & 3))
+        return fail(FA_ERR_ARG, "read sweep needs 16-B aligned X, n %% 4 == 0, sink_len > 0");
+    int64_t grid = sink_len < 65535 ? sink_len : 65535;
+    hipLaunchKernelGGL(k_read_sweep, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<const f32x4*>(X), n >> 2, sink);
+    return check_launch("k_read_sweep");
+}
+
+}  // extern "C"

@@ -1,0 +1,259 @@
+"""Device-side aggregation engine: numpy-exact scalar factors + HIP folds.
+
+Layering
+  engine.fold_stacked(X, weights, scores)   X: CUDA tensor [N, P] (row pitch = X.stride(0))
+  engine.fold_rows(rows, weights, scores)   N separately allocated CUDA rows (pointer list)
+  engine.aggregate_layers(params, weights)  host or device per-client layer lists -> per-layer outputs
+
+The scalar factors are formed on the host exactly as numpy forms them in the
+reference (fed_avg_aggregator.py:31-41, stall_aware_aggregation.py:52-66):
+Python-scalar weights are *weak* (rounded once to the array dtype), the total
+is a Python ``sum`` (exact for ints), scores are Python floats from a double
+division.  The kernels then fold in client order with separate roundings.
+
+There is no CPU fallback anywhere in this module: every output element is
+computed by libfedavg_hip.so on the GPU, or the call raises.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .aggregator.exceptions import InvalidParameterShapeError
+
+_TORCH_TO_NP = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                torch.int64: np.int64, torch.float16: np.float16}
+_NP_TO_TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+                np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64}
+ROW_ALIGN = 64  # elements; row pitch multiple of 256 B for fp32
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("fedlesscan_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _np_dtype_of(x) -> np.dtype:
+    if isinstance(x, torch.Tensor):
+        if x.dtype == torch.bfloat16:
+            return np.dtype("V2")  # marker; handled separately
+        return np.dtype(_TORCH_TO_NP[x.dtype])
+    return np.asarray(x).dtype
+
+
+def result_dtype(in_dtype: np.dtype, weights: Sequence, scores: Optional[Sequence] = None,
+                 total=None) -> np.dtype:
+    """dtype numpy gives `reduce(add, [x * n_i (* s_i)]) / sum(n)` (NEP 50 weak Python scalars)."""
+    if total is None:
+        total = sum(weights)
+    dt = np.result_type(in_dtype, *weights, *(scores or ()), total)
+    if dt.kind in "iu" or dt.kind == "b":
+        dt = np.result_type(dt, np.float64)  # true_divide of integers
+    return dt
+
+
+class Factors:
+    """a_i, s_i and the divisor as numpy would round them for compute dtype `dt`."""
+
+    def __init__(self, weights: Sequence, scores: Optional[Sequence], dt: np.dtype, int_weights=False,
+                 total=None):
+        self.total = sum(weights) if total is None else total
+        if int_weights:
+            self.a = np.array([int(w) for w in weights], dtype=np.int64)
+            self.div = float(self.total)
+        else:
+            t = dt.type
+            self.a = np.array([t(w) for w in weights], dtype=dt)
+            self.div = t(self.total)
+        self.s = None if scores is None else np.array([dt.type(x) for x in scores], dtype=dt)
+
+    def to(self, device):
+        a = torch.from_numpy(self.a).to(device, non_blocking=False)
+        s = None if self.s is None else torch.from_numpy(self.s).to(device, non_blocking=False)
+        return a, s
+
+
+def _check_matrix(X: torch.Tensor) -> tuple[int, int, int]:
+    if not X.is_cuda:
+        raise ValueError("X must be a CUDA (HIP) tensor")
+    if X.dim() != 2 or X.stride(1) != 1:
+        raise InvalidParameterShapeError(f"X must be 2-D with unit column stride, got {tuple(X.shape)} "
+                                         f"strides {X.stride()}")
+    N, P = X.shape
+    return N, P, X.stride(0) if N > 1 else max(P, 1)
+
+
+def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] = None, *,
+                 out: Optional[torch.Tensor] = None, want_bf16: bool = False, total=None):
+    """FedAvg (scores None) / stall-aware fold over the rows of X, in row order.
+
+    `total` overrides the divisor sum (used when zip() truncated the rows but
+    the reference still divides by the sum of every weight).  Returns `out`
+    ([P] tensor in the result dtype); with bf16 input and want_bf16=True
+    returns (out_f32, out_bf16).
+    """
+    N, P, ldx = _check_matrix(X)
+    if len(weights) != N or (scores is not None and len(scores) != N):
+        raise InvalidParameterShapeError(f"{N} rows but {len(weights)} weights"
+                                         + ("" if scores is None else f" / {len(scores)} scores"))
+    dev = X.device
+    st = stream_ptr(dev)
+    if X.dtype == torch.bfloat16:
+        f = Factors(weights, scores, np.dtype(np.float32), total=total)
+        a, s = f.to(dev)
+        out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
+        outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
+        _lib.call("fa_fedavg_bf16", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                  out.data_ptr(), _ptr(outb), st)
+        return (out, outb) if want_bf16 else out
+    in_dt = np.dtype(_TORCH_TO_NP.get(X.dtype, np.void))
+    if in_dt == np.void:
+        raise InvalidParameterShapeError(f"unsupported dtype {X.dtype}")
+    dt = result_dtype(in_dt, weights, scores, total)
+    int_path = in_dt.kind == "i" and scores is None and all(isinstance(w, int) for w in weights)
+    if int_path:
+        f = Factors(weights, None, dt, int_weights=True, total=total)
+        a, _ = f.to(dev)
+        out = out if out is not None else torch.empty(P, dtype=torch.float64, device=dev)
+        name = "fa_fedavg_i32" if in_dt == np.int32 else "fa_fedavg_i64"
+        _lib.call(name, X.data_ptr(), N, P, ldx, a.data_ptr(), f.div, out.data_ptr(), st)
+        return out
+    if dt not in (np.float32, np.float64):
+        raise InvalidParameterShapeError(f"unsupported result dtype {dt} (input {in_dt})")
+    if in_dt != dt:
+        # numpy promotes the operand before multiplying; same on the device.
+        X = X.to(_NP_TO_TORCH[dt])
+        ldx = X.stride(0) if N > 1 else max(P, 1)
+    f = Factors(weights, scores, dt, total=total)
+    a, s = f.to(dev)
+    out = out if out is not None else torch.empty(P, dtype=_NP_TO_TORCH[dt], device=dev)
+    if dt == np.float32:
+        _lib.call("fa_fedavg_f32", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                  out.data_ptr(), st)
+    else:
+        _lib.call("fa_fedavg_f64", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                  out.data_ptr(), st)
+    return out
+
+
+def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[Sequence] = None, *,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Same fold over separately allocated 1-D CUDA rows (no stacking copy for fp32)."""
+    N = len(rows)
+    if N == 0:
+        _lib.check(_lib.FA_ERR_NO_CLIENTS, "fold_rows")
+    P = rows[0].numel()
+    dev = rows[0].device
+    for r in rows:
+        if r.numel() != P or r.dtype != rows[0].dtype or not r.is_contiguous() or r.device != dev:
+            raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
+    if rows[0].dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores) != np.float32:
+        return fold_stacked(torch.stack([r.reshape(-1) for r in rows]), weights, scores, out=out)
+    f = Factors(weights, scores, np.dtype(np.float32))
+    a, s = f.to(dev)
+    ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).to(dev)
+    out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
+    _lib.call("fa_fedavg_f32_ptrs", ptrs.data_ptr(), N, P, a.data_ptr(), _ptr(s), float(f.div),
+              out.data_ptr(), stream_ptr(dev))
+    # `ptrs` may be freed on return: the caching allocator reuses it only in
+    # stream order, i.e. after this kernel has read it.
+    return out
+
+
+# ---------------------------------------------------------------------------
+# per-layer (reference-shaped) aggregation
+# ---------------------------------------------------------------------------
+def _layer_meta(parameters, n_eff):
+    L = min(len(p) for p in parameters[:n_eff])
+    shapes, dtypes = [], []
+    for li in range(L):
+        ref = parameters[0][li]
+        shp = tuple(ref.shape)
+        dt = ref.dtype
+        for ci in range(1, n_eff):
+            x = parameters[ci][li]
+            if tuple(x.shape) != shp:
+                raise InvalidParameterShapeError(
+                    f"layer {li}: client {ci} has shape {tuple(x.shape)}, client 0 has {shp}")
+            if x.dtype != dt:
+                raise InvalidParameterShapeError(f"layer {li}: client {ci} dtype {x.dtype} != {dt}")
+        shapes.append(shp)
+        dtypes.append(dt)
+    return L, shapes, dtypes
+
+
+def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: Optional[Sequence] = None,
+                     device: Optional[torch.device] = None) -> List:
+    """Reference-shaped FedAvg / stall-aware aggregation.
+
+    parameters: N clients x L layers (numpy arrays, or CUDA tensors).  Returns
+    L outputs (numpy in -> numpy out, tensors in -> CUDA tensors out).  zip()
+    truncation over clients/weights/scores and over layers is kept
+    (fed_avg_aggregator.py:32-41); the divisor is the sum of ALL weights.
+    """
+    n_eff = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
+    if n_eff == 0:
+        return []
+    total_weights = list(weights)
+    L, shapes, dtypes = _layer_meta(parameters, n_eff)
+    if L == 0:
+        return []
+    on_device = isinstance(parameters[0][0], torch.Tensor)
+    dev = device or (parameters[0][0].device if on_device else default_device())
+    w = list(weights[:n_eff])
+    sc = None if scores is None else list(scores[:n_eff])
+    groups: dict = {}
+    for li, dt in enumerate(dtypes):
+        groups.setdefault(str(dt), []).append(li)
+    outs: list = [None] * L
+    for _, lis in groups.items():
+        sizes = [int(np.prod(shapes[li])) if len(shapes[li]) else 1 for li in lis]
+        P = sum(sizes)
+        X = _stack_group(parameters, n_eff, lis, sizes, P, dev, on_device)
+        res = fold_stacked(X, w, sc, total=sum(total_weights))
+        flat = res if on_device else res.cpu().numpy()
+        off = 0
+        for li, n in zip(lis, sizes):
+            outs[li] = flat[off:off + n].reshape(shapes[li])
+            off += n
+    return outs
+
+
+def _stack_group(parameters, n, lis, sizes, P, dev, on_device) -> torch.Tensor:
+    ldx = ((P + ROW_ALIGN - 1) // ROW_ALIGN) * ROW_ALIGN
+    if on_device:
+        ref = parameters[0][lis[0]]
+        X = torch.empty((n, ldx), dtype=ref.dtype, device=dev)
+        for i in range(n):
+            off = 0
+            for li, sz in zip(lis, sizes):
+                X[i, off:off + sz].copy_(parameters[i][li].reshape(-1))
+                off += sz
+        return X[:, :P]
+    np_dt = np.asarray(parameters[0][lis[0]]).dtype
+    tdt = _NP_TO_TORCH.get(np_dt)
+    if tdt is None:
+        raise InvalidParameterShapeError(f"unsupported parameter dtype {np_dt}")
+    stage = torch.empty((n, ldx), dtype=tdt, pin_memory=True)
+    sv = stage.numpy()
+    for i in range(n):
+        off = 0
+        for li, sz in zip(lis, sizes):
+            sv[i, off:off + sz] = np.asarray(parameters[i][li]).reshape(-1)
+            off += sz
+    X = torch.empty((n, ldx), dtype=tdt, device=dev)
+    X.copy_(stage, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()  # stage may be freed after return
+    return X[:, :P]

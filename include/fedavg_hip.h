@@ -1,0 +1,119 @@
+/*
+ * fedavg_hip.h — C-ABI of libfedavg_hip.so, the MI355X (gfx950) FedAvg /
+ * FedLesScan parameter-aggregation engine.
+ *
+ * The reference has no native code; its hot path is the numpy fold in
+ *   fedless/aggregator/fed_avg_aggregator.py:24-42   FedAvgAggregator._aggregate
+ *   fedless/aggregator/stall_aware_aggregation.py:42-67  StallAwareAggregator._aggregate
+ * The Python drop-in classes (fedlesscan_amd/aggregator/) bind these entry
+ * points with ctypes; INTEGRATION.md shows the binding a maintainer would add
+ * to the reference itself.
+ *
+ * Conventions
+ *  - Every data pointer is DEVICE memory (hipMalloc / torch CUDA tensors)
+ *    unless marked [host].  The caller owns all buffers; the library never
+ *    allocates or frees in a compute call.
+ *  - X is row-major [N][ldx]: row i = client i's flattened parameters, in the
+ *    order the reference iterates client_results.  ldx >= P (elements).
+ *  - a[i] = fl(n_i), the client's cardinality rounded to the compute type the
+ *    way numpy rounds a Python scalar; s[i] = fl((r_i+1)/(R+1)) for the
+ *    stall-aware variant, NULL for FedAvg; divisor = fl(sum_i n_i) with the
+ *    sum taken exactly (Python int).  These are [device] arrays of N.
+ *  - stream is a hipStream_t (NULL = legacy default stream).  All work is
+ *    enqueued on it; no call synchronises.  Calls are stateless and reentrant.
+ *  - Result, bit for bit:  acc = t_0; acc = acc + t_i (i = 1..N-1, in order);
+ *    out = acc / divisor, where t_i = (x_i * a_i) [* s_i] with separate
+ *    roundings (no FMA) and an IEEE divide.
+ *  - Return FA_OK (0) or an FA_ERR_* code; fa_last_error() describes the last
+ *    failure on the calling thread.
+ */
+#ifndef FEDAVG_HIP_H
+#define FEDAVG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_ABI_VERSION 1
+
+enum fa_status {
+    FA_OK = 0,
+    FA_ERR_ARG = 1,        /* bad size/pointer/stride -> ValueError                          */
+    FA_ERR_NO_CLIENTS = 2, /* N == 0 -> InsufficientClientResults (fed_avg_aggregator.py:51-54) */
+    FA_ERR_SHAPE = 3,      /* -> InvalidParameterShapeError (exceptions.py:13)                  */
+    FA_ERR_HIP = 4,        /* launch / runtime failure -> AggregationError (exceptions.py:1)    */
+};
+
+int fa_abi_version(void);
+/* [host] message for the last failing call on this thread ("" if none). */
+const char* fa_last_error(void);
+
+/* ---- FedAvg / stall-aware fold over a stacked [N][ldx] matrix --------------
+ * replaces FedAvgAggregator._aggregate      (fed_avg_aggregator.py:24-42)  when s == NULL
+ * replaces StallAwareAggregator._aggregate  (stall_aware_aggregation.py:42-67) when s != NULL */
+int fa_fedavg_f32(const float* X, int64_t N, int64_t P, int64_t ldx,
+                  const float* a, const float* s, float divisor,
+                  float* out, void* stream);
+
+/* Same fold over N separately allocated client rows: xi is a [device] array of
+ * N [device] pointers, each to P floats (the list-of-arrays form the reference
+ * passes: fed_avg_aggregator.py:32-35). */
+int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P,
+                       const float* a, const float* s, float divisor,
+                       float* out, void* stream);
+
+/* Chunked fold, the building block of streaming ingest
+ * (StreamFedAvgAggregator.aggregate, fed_avg_aggregator.py:111-153):
+ *   acc_in == NULL : acc = t_0 + ... (as fa_fedavg_f32)
+ *   acc_in != NULL : acc = acc_in[p] + t_0 + t_1 + ...  (continues a fold in order)
+ *   finalize != 0  : out = acc / divisor, else out = acc (partial, unrounded by /)
+ * acc_in may alias out.  Folding rows in chunks this way is bit-identical to
+ * one fa_fedavg_f32 over all rows. */
+int fa_fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx,
+                const float* a, const float* s, const float* acc_in,
+                float divisor, int finalize, float* out, void* stream);
+
+/* bf16 updates (BASELINE config 4; no reference path: defined as exact upcast
+ * to f32 + the f32 fold).  out_f32 [P] required; out_bf16 [P] optional (RNE). */
+int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                   const float* a, const float* s, float divisor,
+                   float* out_f32, uint16_t* out_bf16, void* stream);
+
+/* float64 updates (the reference unit-test fixture is float64,
+ * test/test_aggregation.py:23-38). */
+int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx,
+                  const double* a, const double* s, double divisor,
+                  double* out, void* stream);
+
+/* Integer updates: numpy keeps `layer * n` and the np.add fold in the integer
+ * dtype (wrapping) and true-divides into float64 (fed_avg_aggregator.py:33,39).
+ * a = integer cardinalities [device, int64]; out float64. */
+int fa_fedavg_i32(const int32_t* X, int64_t N, int64_t P, int64_t ldx,
+                  const int64_t* a, double divisor, double* out, void* stream);
+int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx,
+                  const int64_t* a, double divisor, double* out, void* stream);
+
+/* ---- support: synthetic workloads and calibration (not reference API) ----- */
+/* Deterministic generator, bit-identical to fedlesscan_amd/synth.py. */
+int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
+                 int64_t row0, int64_t col0, void* stream);
+int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
+                  int64_t row0, int64_t col0, void* stream);
+/* Contiguous read-only sweep of n floats (16 B/lane) -> one partial per block
+ * in sink[grid]: the streaming-read ceiling the fold is compared with. */
+int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
+/* Tuning entry: fa_fedavg_f32 with an explicit kernel variant;
+ * variant 0 = the default.  Returns FA_ERR_ARG for an unknown variant. */
+int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
+                          const float* a, const float* s, float divisor,
+                          float* out, void* stream, int variant);
+int fa_num_variants(void);
+/* [host] short name of a variant, e.g. "v4u8". */
+const char* fa_variant_name(int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDAVG_HIP_H */

@@ -1,0 +1,339 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the pinned oracle / golden
+vectors.  Contract: bit-exact for fp32/fp64/int outputs (NaN positions only,
+payload not pinned); bf16 is defined as exact upcast + the fp32 fold, so it is
+bit-exact against that definition too."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from fedlesscan_amd import _lib
+    return _lib
+
+
+def _bits_equal(a, b):
+    return G.same_bits(np.asarray(a), np.asarray(b))
+
+
+# ---------------------------------------------------------------------------
+# golden vectors through the drop-in strategy classes
+# ---------------------------------------------------------------------------
+def _npz_results(params, cards, b64=False):
+    from fedlesscan_amd.common.models import (BinaryStringFormat, ClientResult, NpzWeightsSerializerConfig,
+                                              SerializedParameters, WeightsSerializerConfig)
+    from fedlesscan_amd.common.serialization import Base64StringConverter, NpzWeightsSerializer
+    out = []
+    for i, (p, c) in enumerate(zip(params, cards)):
+        blob = NpzWeightsSerializer().serialize(p)
+        fmt = BinaryStringFormat.NONE
+        if b64 and i % 2 == 0:
+            blob, fmt = Base64StringConverter.to_str(blob), BinaryStringFormat.BASE64
+        out.append(ClientResult(parameters=SerializedParameters(
+            blob=blob, serializer=WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig()),
+            string_format=fmt), cardinality=c))
+    return out
+
+
+GOLDEN_LITERAL = [(c, p) for c, m in G.manifest().items() if not m.get("sampled")
+                  for p in m["outputs"] if p in ("fedavg", "_aggregate", "stall")]
+
+
+@pytest.mark.parametrize("case,prefix", GOLDEN_LITERAL)
+def test_strategy_classes_match_golden(dev, case, prefix):
+    from fedlesscan_amd import FedAvgAggregator, StallAwareAggregator
+    from fedlesscan_amd.common.models import AggregationHyperParams
+    m = G.manifest()[case]
+    params = G.parameters(case)
+    if prefix == "stall":
+        out = StallAwareAggregator(m["current_round"], AggregationHyperParams(tolerance=2))._aggregate(
+            G.feats(case), params, m["weights"])
+    else:
+        out = FedAvgAggregator()._aggregate(params, m["weights"])
+    exp = G.expected(case, prefix)
+    assert len(out) == len(exp)
+    for a, b in zip(out, exp):
+        assert a.shape == b.shape and a.dtype == b.dtype, (case, prefix, a.dtype, b.dtype)
+        assert _bits_equal(a, b), (case, prefix)
+
+
+def test_reference_fixture_aggregate_paths(dev):
+    from fedlesscan_amd import FedAvgAggregator, StreamFedAvgAggregator, UnknownCardinalityError
+    params = G.parameters("ref_fixture")
+    res, _ = FedAvgAggregator().aggregate(_npz_results(params, [1, 2, 0], b64=True), None)
+    assert all(_bits_equal(a, b) for a, b in zip(res, G.expected("ref_fixture", "aggregate_intcards")))
+    bad = _npz_results(params, [-1, 2, 0], b64=True)
+    with pytest.raises(UnknownCardinalityError):
+        FedAvgAggregator().aggregate(bad, None)
+    res, _ = FedAvgAggregator().aggregate(_npz_results(params, [-1, 2, 0], b64=True), None,
+                                          default_cardinality=1.0)
+    assert all(_bits_equal(a, b) for a, b in zip(res, G.expected("ref_fixture", "aggregate_default_card")))
+    for cs in (1, 2, 10, 50):
+        res, _ = StreamFedAvgAggregator(chunk_size=cs).aggregate(_npz_results(params, [1, 2, 0], True), None)
+        assert all(_bits_equal(a, b) for a, b in zip(res, G.expected("ref_fixture", f"stream_c{cs}"))), cs
+
+
+def test_n60_aggregate_and_stream_paths(dev):
+    from fedlesscan_amd import (FedAvgAggregator, StallAwareAggregator, StreamFedAvgAggregator,
+                                StreamStallAwareAggregator)
+    from fedlesscan_amd.common.models import AggregationHyperParams
+    case = "f32_n60"
+    m = G.manifest()[case]
+    params, w, feats, R = G.parameters(case), m["weights"], G.feats(case), m["current_round"]
+    hp = AggregationHyperParams(tolerance=2)
+    got = {
+        "aggregate": FedAvgAggregator().aggregate(_npz_results(params, w), feats)[0],
+        "aggregate_stall": StallAwareAggregator(R, hp).aggregate(_npz_results(params, w), feats)[0],
+        "stream_c25": StreamFedAvgAggregator(25).aggregate(_npz_results(params, w), feats)[0],
+        "stream_stall_c25": StreamStallAwareAggregator(R, hp, 25).aggregate(_npz_results(params, w), feats)[0],
+    }
+    for prefix, out in got.items():
+        assert all(_bits_equal(a, b) for a, b in zip(out, G.expected(case, prefix))), prefix
+
+
+def test_mnist_c1_sampled(dev):
+    from fedlesscan_amd import FedAvgAggregator
+    import hashlib
+    case = "mnist_c1"
+    m = G.manifest()[case]
+    out = FedAvgAggregator()._aggregate(G.parameters(case), m["weights"])
+    flat = np.concatenate([o.ravel() for o in out])
+    assert hashlib.sha256(flat.tobytes()).hexdigest() == m["outputs"]["fedavg"]["flat_sha256"]
+
+
+# ---------------------------------------------------------------------------
+# kernels directly vs the C oracle: shapes, strides, alignment, variants
+# ---------------------------------------------------------------------------
+from oracle import oracle_lib as OL  # noqa: E402  (checker)
+from fedlesscan_amd import synth  # noqa: E402
+
+
+SHAPES = [(1, 1), (1, 4), (2, 3), (3, 5), (7, 1023), (16, 1024), (17, 1025), (33, 4099), (100, 65536),
+          (129, 10007), (1000, 333)]
+
+
+@pytest.mark.parametrize("N,P", SHAPES)
+@pytest.mark.parametrize("scored", [False, True])
+def test_fold_f32_shapes(dev, N, P, scored):
+    from fedlesscan_amd import engine
+    X = synth.clients_f32(1000 + N, N, 0, P)
+    w = synth.cardinalities(1000 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(7, N, 10, 2)] if scored else None
+    a = np.array(w, np.float32)
+    s = None if sc is None else np.array(sc, np.float32)
+    exp = OL.fedavg_f32(X, a, np.float32(sum(w)), s=s)
+    got = engine.fold_stacked(torch.from_numpy(X).to(dev), w, sc).cpu().numpy()
+    assert _bits_equal(got, exp)
+
+
+@pytest.mark.parametrize("offset", [0, 1, 2, 3])
+@pytest.mark.parametrize("pad", [0, 1, 5, 64])
+def test_fold_f32_pitch_and_misalignment(dev, offset, pad):
+    """Row pitch ldx > P and base offsets that break 16-B alignment (scalar path)."""
+    from fedlesscan_amd import engine
+    N, P = 9, 1030
+    X = synth.clients_f32(5, N, 0, P)
+    w = synth.cardinalities(5, N)
+    big = torch.zeros((N, P + pad + offset), dtype=torch.float32, device=dev)
+    big[:, offset:offset + P] = torch.from_numpy(X).to(dev)
+    view = big[:, offset:offset + P]
+    got = engine.fold_stacked(view, w).cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    assert _bits_equal(got, exp)
+
+
+def test_all_variants_bit_identical(dev, lib):
+    L = lib.load()
+    N, P = 77, 50003
+    X = torch.from_numpy(synth.clients_f32(8, N, 0, P)).to(dev)
+    w = synth.cardinalities(8, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor([(r + 1) / 11 for r in synth.round_ids(8, N, 10, 2)], dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = []
+    for v in range(L.fa_num_variants()):
+        for sp in (None, s):
+            o = torch.empty(P, dtype=torch.float32, device=dev)
+            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+                                              None if sp is None else sp.data_ptr(),
+                                              float(np.float32(sum(w))), o.data_ptr(), st, v), "variant")
+            outs.append((v, sp is None, o.cpu().numpy()))
+    base = {True: None, False: None}
+    for v, plain, o in outs:
+        if base[plain] is None:
+            base[plain] = o
+        assert _bits_equal(o, base[plain]), (v, plain)
+    exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
+    assert _bits_equal(base[True], exp)
+
+
+def test_chunked_fold_equals_batch(dev, lib):
+    """fa_fold_f32 over row chunks (acc carried, divide at the end) == one batch fold."""
+    L = lib.load()
+    N, P = 50, 12345
+    X = torch.from_numpy(synth.clients_f32(31, N, 0, P)).to(dev)
+    w = synth.cardinalities(31, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    div = float(np.float32(sum(w)))
+    acc = torch.empty(P, dtype=torch.float32, device=dev)
+    bounds = [0, 1, 7, 20, 21, 49, 50]
+    for k, (r0, r1) in enumerate(zip(bounds[:-1], bounds[1:])):
+        last = r1 == N
+        lib.check(L.fa_fold_f32(X[r0].data_ptr(), r1 - r0, P, P, a[r0:].data_ptr(), None,
+                                None if k == 0 else acc.data_ptr(), div, int(last), acc.data_ptr(), st), "fold")
+    exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
+    assert _bits_equal(acc.cpu().numpy(), exp)
+
+
+def test_ptr_rows_equal_stacked(dev):
+    from fedlesscan_amd import engine
+    N, P = 23, 7001
+    X = synth.clients_f32(41, N, 0, P)
+    w = synth.cardinalities(41, N)
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]
+    # one misaligned row exercises the per-row scalar path
+    holder = torch.zeros(P + 1, dtype=torch.float32, device=dev)
+    holder[1:] = rows[3]
+    rows[3] = holder[1:]
+    sc = [(r + 1) / 11 for r in synth.round_ids(41, N, 10, 2)]
+    for scores in (None, sc):
+        got = engine.fold_rows(rows, w, scores).cpu().numpy()
+        exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                            s=None if scores is None else np.array(scores, np.float32))
+        assert _bits_equal(got, exp)
+
+
+@pytest.mark.parametrize("N,P", [(1, 8), (5, 9), (64, 8 * 1000 + 3), (256, 65536)])
+@pytest.mark.parametrize("scored", [False, True])
+def test_bf16_matches_definition(dev, N, P, scored):
+    from fedlesscan_amd import engine
+    Xb = synth.clients_bf16(60 + N, N, 0, P)
+    w = synth.cardinalities(60 + N, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(60, N, 10, 2)] if scored else None
+    exp, expb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)),
+                               s=None if sc is None else np.array(sc, np.float32))
+    Xd = torch.from_numpy(Xb.view(np.int16)).to(dev).view(torch.bfloat16)
+    out, outb = engine.fold_stacked(Xd, w, sc, want_bf16=True)
+    assert _bits_equal(out.cpu().numpy(), exp)
+    assert np.array_equal(outb.view(torch.int16).cpu().numpy().view(np.uint16), expb)
+
+
+def test_f64_and_int_paths(dev):
+    from fedlesscan_amd import engine
+    X = np.stack([p[0] for p in G.parameters("f64_n40")])
+    m = G.manifest()["f64_n40"]
+    got = engine.fold_stacked(torch.from_numpy(X).to(dev), m["weights"]).cpu().numpy()
+    assert _bits_equal(got, G.expected("f64_n40", "fedavg")[0])
+    for case in ("int64_inputs", "int32_inputs"):
+        m = G.manifest()[case]
+        params = G.parameters(case)
+        from fedlesscan_amd import FedAvgAggregator
+        out = FedAvgAggregator()._aggregate(params, m["weights"])
+        exp = G.expected(case, "fedavg")
+        assert all(a.dtype == b.dtype and _bits_equal(a, b) for a, b in zip(out, exp)), case
+
+
+def test_gpu_synth_matches_host(dev, lib):
+    L = lib.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    X = torch.empty((5, 3000), dtype=torch.float32, device=dev)
+    lib.check(L.fa_synth_f32(X.data_ptr(), 5, 2999, 3000, 77, 10, 123, st), "synth")
+    exp = synth.clients_f32(77, 5, 123, 2999, row0=10)
+    assert np.array_equal(X[:, :2999].cpu().numpy().view(np.uint32), exp.view(np.uint32))
+    B = torch.empty((3, 1000), dtype=torch.int16, device=dev)
+    lib.check(L.fa_synth_bf16(B.data_ptr(), 3, 1000, 1000, 78, 0, 5, st), "synth_bf16")
+    assert np.array_equal(B.cpu().numpy().view(np.uint16), synth.clients_bf16(78, 3, 5, 1000))
+
+
+def test_error_mapping(dev, lib):
+    from fedlesscan_amd import FedAvgAggregator, InsufficientClientResults, InvalidParameterShapeError
+    L = lib.load()
+    X = torch.zeros((2, 8), device=dev)
+    a = torch.ones(2, device=dev)
+    with pytest.raises(InsufficientClientResults):
+        lib.check(L.fa_fedavg_f32(X.data_ptr(), 0, 8, 8, a.data_ptr(), None, 1.0, X.data_ptr(), None), "x")
+    with pytest.raises(InvalidParameterShapeError):
+        lib.check(L.fa_fedavg_f32(X.data_ptr(), 2, 8, 4, a.data_ptr(), None, 1.0, X.data_ptr(), None), "x")
+    with pytest.raises(ValueError):
+        lib.check(L.fa_fedavg_f32(None, 2, 8, 8, a.data_ptr(), None, 1.0, X.data_ptr(), None), "x")
+    with pytest.raises(InvalidParameterShapeError):
+        FedAvgAggregator()._aggregate([[np.zeros(3, np.float32)], [np.zeros(4, np.float32)]], [1, 1])
+    assert FedAvgAggregator()._aggregate([], []) == []
+
+
+# ---------------------------------------------------------------------------
+# BASELINE full sizes: exact on a column sample regenerated on the host
+# ---------------------------------------------------------------------------
+def _full_size_check(dev, lib, N, P, seed, dtype, scored, card_hi=600, ncheck=4096):
+    from fedlesscan_amd import engine
+    L = lib.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    X = torch.empty((N, P), dtype=tdt, device=dev)
+    fn = L.fa_synth_f32 if dtype == "f32" else L.fa_synth_bf16
+    lib.check(fn(X.data_ptr(), N, P, P, seed, 0, 0, st), "synth")
+    w = synth.cardinalities(seed, N, 1, card_hi)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
+    out = engine.fold_stacked(X, w, sc)
+    torch.cuda.synchronize()
+    del X
+    torch.cuda.empty_cache()
+    rng = np.random.default_rng(seed)
+    # a contiguous block at each end + random 4-column groups across the row
+    cols = np.unique(np.concatenate([np.arange(0, 1024), np.arange(P - 1024, P),
+                                     (rng.integers(0, P // 4, ncheck) * 4)[:, None] + np.arange(4)[None, :]
+                                     ]).ravel())
+    got = out.cpu().numpy()[cols]
+    a = np.array(w, np.float32)
+    s = None if sc is None else np.array(sc, np.float32)
+    # regenerate exactly those columns on the host (contiguous runs)
+    runs = np.split(cols, np.where(np.diff(cols) != 1)[0] + 1)
+    exp = []
+    for r in runs:
+        if dtype == "f32":
+            Xh = OL.synth_f32(seed, N, len(r), col0=int(r[0]))
+            exp.append(OL.fedavg_f32(Xh, a, np.float32(sum(w)), s=s))
+        else:
+            Xh = OL.synth_bf16(seed, N, len(r), col0=int(r[0]))
+            exp.append(OL.fedavg_bf16(Xh, a, np.float32(sum(w)), s=s)[0])
+    exp = np.concatenate(exp)
+    assert _bits_equal(got, exp)
+    assert np.isfinite(got).all()
+
+
+def test_config2_full_100x1M(dev, lib):
+    from fedlesscan_amd import engine
+    N, P, seed = 100, 1_000_000, 2
+    X = OL.synth_f32(seed, N, P)
+    w = synth.cardinalities(seed, N)
+    got = engine.fold_stacked(torch.from_numpy(X).to(dev), w).cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    assert _bits_equal(got, exp)
+
+
+def test_config3_full_size_1024x10M(dev, lib):
+    _full_size_check(dev, lib, 1024, 10_000_000, 3, "f32", scored=False)
+
+
+def test_config5_full_size_stall_512x25M(dev, lib):
+    _full_size_check(dev, lib, 512, 25_000_000, 5, "f32", scored=True, card_hi=2000)
+
+
+def test_config4_shard_size_bf16_256x12_5M(dev, lib):
+    # one of 8 parameter buckets of config 4 (256 x 100M bf16 over 8 GPUs)
+    _full_size_check(dev, lib, 256, 12_500_000, 4, "bf16", scored=False)

@@ -1,0 +1,265 @@
+"""CPU-side tests: the C-ABI library loads and exports its header, host-side
+factor rounding, store/selection semantics, serialization, and the handler's
+bookkeeping.  No GPU compute here (the GPU parity tests are in
+test_gpu_parity.py)."""
+import ctypes
+import io
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+from fedlesscan_amd import _lib, engine
+from fedlesscan_amd.aggregator.fed_avg_aggregator import chunked, resolve_cardinality
+from fedlesscan_amd.common.models import (AggregationHyperParams, AggregationStrategy, AggregatorFunctionParams,
+                                          BinaryStringFormat, ClientResult, NpzWeightsSerializerConfig,
+                                          SerializedParameters, TestMetrics, WeightsSerializerConfig)
+from fedlesscan_amd.common.serialization import (Base64StringConverter, NpzWeightsSerializer, SerializationError,
+                                                 WeightsSerializerBuilder, deserialize_parameters)
+from fedlesscan_amd.store import InMemoryClientResultStore, InMemoryParameterStore
+from oracle import fedavg_oracle as O
+
+
+# ---------------------------------------------------------------------------
+# the C-ABI library
+# ---------------------------------------------------------------------------
+def test_library_exports_every_header_symbol():
+    L = _lib.load()
+    declared = _lib.header_functions()
+    assert len(declared) >= 14
+    missing = [f for f in declared if not hasattr(L, f)]
+    assert not missing, missing
+    assert set(declared) == set(_lib._PROTOS), "ctypes prototypes out of sync with the header"
+    assert L.fa_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_variant_table():
+    L = _lib.load()
+    n = L.fa_num_variants()
+    assert n >= 1
+    names = [L.fa_variant_name(i).decode() for i in range(n)]
+    assert all(names) and len(set(names)) == n
+    assert L.fa_variant_name(n) == b""
+
+
+def test_library_argument_errors_need_no_gpu():
+    L = _lib.load()
+    # validation happens before any HIP call
+    assert L.fa_fedavg_f32(None, 0, 10, 10, None, None, 1.0, None, None) == _lib.FA_ERR_NO_CLIENTS
+    assert "N == 0" in _lib.last_error()
+    assert L.fa_fedavg_f32(ctypes.c_void_p(16), 2, 10, 5, ctypes.c_void_p(16), None, 1.0,
+                           ctypes.c_void_p(16), None) == _lib.FA_ERR_SHAPE
+    assert L.fa_fedavg_f32(None, 2, 10, 10, None, None, 1.0, None, None) == _lib.FA_ERR_ARG
+    assert L.fa_fedavg_f32(None, -1, 10, 10, None, None, 1.0, None, None) == _lib.FA_ERR_ARG
+    with pytest.raises(Exception) as ei:
+        _lib.check(_lib.FA_ERR_NO_CLIENTS, "x")
+    assert type(ei.value).__name__ == "InsufficientClientResults"
+
+
+def test_product_package_does_not_import_oracle():
+    import pathlib
+    pkg = pathlib.Path(_lib.PKG)
+    for f in pkg.rglob("*.py"):
+        text = f.read_text()
+        assert "import oracle" not in text and "from oracle" not in text, f
+
+
+# ---------------------------------------------------------------------------
+# numpy-exact host factors
+# ---------------------------------------------------------------------------
+def test_result_dtype_matches_numpy():
+    cases = [(np.float32, [1, 2, 3], None), (np.float32, [1.5, 2], None), (np.float32, [1, 2], [0.5, 1.0]),
+             (np.float64, [3, 4], None), (np.int64, [1, 2], None), (np.int32, [1, 2], None),
+             (np.int64, [1.5, 2], None), (np.float32, [np.int64(3), 2], None)]
+    for dt, w, s in cases:
+        xs = [np.ones(3, dtype=dt) for _ in w]
+        ref = (O.fedavg_literal([[x] for x in xs], w) if s is None else
+               O.stall_aware_literal([{"round_id": 0}] * len(w), 0, [[x] for x in xs], w))
+        assert engine.result_dtype(np.dtype(dt), w, s) == ref[0].dtype, (dt, w, s)
+
+
+def test_factors_round_like_numpy():
+    w = [3, 16777217, 2.5, 0.1]
+    f = engine.Factors(w, [1 / 3, 2 / 3, 0.7, 1.0], np.dtype(np.float32))
+    for x, aw in zip(w, f.a):
+        assert aw == (np.ones(1, np.float32) * x)[0]
+    assert f.div == (np.ones(1, np.float32) / np.float32(1) * 0 + np.float32(sum(w)))[0]
+    assert f.s[0] == (np.ones(1, np.float32) * (1 / 3))[0]
+
+
+def test_cardinality_resolution_quirks():
+    from fedlesscan_amd import UnknownCardinalityError
+    assert resolve_cardinality(5, None) == 5
+    assert resolve_cardinality(-1, 2.0) == 2.0
+    with pytest.raises(UnknownCardinalityError):
+        resolve_cardinality(-2, None)
+    with pytest.raises(UnknownCardinalityError):  # `if not default_cardinality`: 0.0 counts as absent
+        resolve_cardinality(-1, 0.0)
+
+
+def test_chunking_matches_reference_semantics():
+    assert [len(c) for c in chunked(range(7), 3)] == [3, 3, 1]
+    assert [len(c) for c in chunked(range(6), 3)] == [3, 3]
+    assert list(chunked([], 3)) == []
+
+
+# ---------------------------------------------------------------------------
+# serialization (mirrors reference test/test_serialize.py:198-299)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("compressed", [True, False])
+def test_npz_roundtrip_and_types(compressed):
+    s = NpzWeightsSerializer(compressed=compressed)
+    w = [np.random.randn(10, 15).astype(np.float32), np.random.randint(0, 32, (8, 5)),
+         np.random.randint(0, 1, (5, 6)).astype(np.int8)]
+    r = s.deserialize(s.serialize(w))
+    assert all(np.array_equal(a, b) and a.dtype == b.dtype for a, b in zip(w, r))
+    assert s.deserialize(s.serialize([])) == []
+
+
+def test_npz_errors_wrap():
+    with pytest.raises(SerializationError):
+        NpzWeightsSerializer().deserialize(b"")
+    with pytest.raises(SerializationError):
+        NpzWeightsSerializer().deserialize(b"not a zip at all")
+
+
+def test_deserialize_parameters_formats():
+    w = [np.random.rand(10, 10, 15), np.random.rand(99, 4, 3)]
+    blob = NpzWeightsSerializer(compressed=True).serialize(w)
+    sp = SerializedParameters(blob=Base64StringConverter.to_str(blob),
+                              serializer=WeightsSerializerConfig(type="npz",
+                                                                 params=NpzWeightsSerializerConfig(compressed=True)),
+                              string_format=BinaryStringFormat.BASE64)
+    assert all(np.array_equal(a, b) for a, b in zip(deserialize_parameters(sp), w))
+    sp = SerializedParameters(blob=NpzWeightsSerializer().serialize(w),
+                              serializer=WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig()))
+    assert all(np.array_equal(a, b) for a, b in zip(deserialize_parameters(sp), w))
+    with pytest.raises(NotImplementedError):
+        WeightsSerializerBuilder.from_config(WeightsSerializerConfig.model_construct(type="h5", params=None))
+
+
+# ---------------------------------------------------------------------------
+# store: selection order, tolerance window, counts (client_daos.py:150-235)
+# ---------------------------------------------------------------------------
+def _cr(v, card=10):
+    blob = NpzWeightsSerializer().serialize([np.full(4, v, np.float32)])
+    return ClientResult(parameters=SerializedParameters(
+        blob=blob, serializer=WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())),
+        cardinality=card)
+
+
+def test_store_selection_semantics():
+    st = InMemoryClientResultStore()
+    for r in (7, 8, 9, 10):
+        for c in ("a", "b"):
+            st.save("s", r, c, _cr(r))
+    st.save("other", 10, "a", _cr(0))
+    st.save("s", 8, "a", _cr(88))  # upsert keeps its position
+    d, it = st.load_results_for_round("s", 10)
+    assert [x["client_id"] for x in d] == ["a", "b"]
+    d, it = st.load_results_for_session("s", 10, tolerance=2)
+    assert [(x["round_id"], x["client_id"]) for x in d] == [(8, "a"), (8, "b"), (9, "a"), (9, "b"),
+                                                             (10, "a"), (10, "b")]
+    first = next(it)
+    assert deserialize_parameters(first.parameters)[0][0] == 88
+    assert st.count_results_for_round("s", 10) == 2
+    assert st.count_results_for_session("s") == 8  # whole session, not the window
+    st.delete_results_for_round("s", 10)
+    assert st.count_results_for_session("s") == 6
+    st.delete_results_for_session("s")
+    assert st.count_results_for_session("s") == 0 and st.count_results_for_session("other") == 1
+
+
+def test_store_returns_fresh_objects():
+    st = InMemoryClientResultStore()
+    st.save("s", 1, "a", _cr(1))
+    _, it = st.load_results_for_round("s", 1)
+    r = next(it)
+    r.parameters = None
+    _, it = st.load_results_for_round("s", 1)
+    assert next(it).parameters is not None
+
+
+# ---------------------------------------------------------------------------
+# handler bookkeeping (aggregation.py:45-167) with the fold supplied by the
+# oracle (these tests check selection / counts / persistence, not numerics)
+# ---------------------------------------------------------------------------
+@pytest.fixture
+def oracle_fold(monkeypatch):
+    def fake(parameters, weights, scores=None, device=None):
+        n = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
+        if scores is None:
+            return O.fedavg_literal(parameters[:n], list(weights))
+        return _stall(parameters[:n], list(weights), list(scores))
+    monkeypatch.setattr(engine, "aggregate_layers", fake)
+
+
+def _stall(params, weights, scores):
+    """stall-aware fold with explicit scores (the oracle derives them from round ids)."""
+    from functools import reduce
+    total = sum(weights)
+    prods = [[np.multiply(np.multiply(l, n), s) for l in p] for p, n, s in zip(params, weights, scores)]
+    return [reduce(np.add, ls) / total for ls in zip(*prods)]
+
+
+def test_handler_per_round(oracle_fold):
+    from fedlesscan_amd.handler import MockAggregator
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    for i in range(10):
+        st.save("sess", 3, f"c{i}", _cr(float(i), card=6000))
+    st.save("sess", 2, "old", _cr(100.0))
+    res = MockAggregator(AggregatorFunctionParams(session_id="sess", round_id=3), st, ps).run_aggregator()
+    assert res.new_round_id == 4 and res.num_clients == 10
+    out = NpzWeightsSerializer().deserialize(ps.load("sess", 4).blob)
+    assert out[0][0] == np.float32(4.5)
+    assert st.count_results_for_round("sess", 3) == 0 and st.count_results_for_session("sess") == 1
+
+
+def test_handler_per_session_tolerance(oracle_fold):
+    from fedlesscan_amd.handler import default_aggregation_handler
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    st.save("s", 7, "stale", _cr(1000.0))  # outside R - tol
+    st.save("s", 8, "a", _cr(1.0))
+    st.save("s", 10, "b", _cr(2.0))
+    hp = AggregationHyperParams(tolerance=2)
+    cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
+    res = default_aggregation_handler("s", 10, st, ps, cfg, None, True, AggregationStrategy.PER_SESSION, hp)
+    assert res.new_round_id == 11
+    assert res.num_clients == 3  # count_results_for_session counts every session result
+    out = NpzWeightsSerializer().deserialize(ps.load_latest("s").blob)[0]
+    exp = (np.float32(1.0) * 10 * (9 / 11) + np.float32(2.0) * 10 * (11 / 11)) / 20
+    assert out[0] == pytest.approx(exp, rel=1e-6)
+    assert st.count_results_for_session("s") == 0
+
+
+def test_handler_no_results_raises(oracle_fold):
+    from fedlesscan_amd import InsufficientClientResults
+    from fedlesscan_amd.handler import default_aggregation_handler
+    cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
+    with pytest.raises(InsufficientClientResults):
+        default_aggregation_handler("s", 1, InMemoryClientResultStore(), InMemoryParameterStore(), cfg)
+
+
+def test_handler_online_uses_stream_variant(oracle_fold):
+    from fedlesscan_amd.handler import default_aggregation_handler
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    for i in range(30):
+        st.save("s", 1, f"c{i}", _cr(float(i), card=i + 1))
+    cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
+    res = default_aggregation_handler("s", 1, st, ps, cfg, None, False, AggregationStrategy.PER_ROUND,
+                                      AggregationHyperParams(aggregate_online=True))
+    assert res.num_clients == 30 and st.count_results_for_round("s", 1) == 30
+    out = NpzWeightsSerializer().deserialize(ps.load("s", 2).blob)[0]
+    params = [[np.full(4, float(i), np.float32)] for i in range(30)]
+    results = [{"blob": NpzWeightsSerializer().serialize(p), "cardinality": i + 1} for i, p in enumerate(params)]
+    exp = O.aggregate_stream_fedavg(results, 25)[0][0]
+    assert np.array_equal(out, exp)
+
+
+def test_test_metrics_are_collected(oracle_fold):
+    from fedlesscan_amd import FedAvgAggregator
+    crs = [_cr(1.0), _cr(2.0)]
+    crs[0].test_metrics = TestMetrics(cardinality=5, metrics={"loss": 1.0})
+    _, metrics = FedAvgAggregator().aggregate(crs, None)
+    assert len(metrics) == 1 and metrics[0].cardinality == 5
+    assert crs[0].parameters is None  # blob released after decode, as the reference does
