@@ -64,7 +64,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-cols", type=int, default=1 << 20, help="columns in the CPU baseline sample")
+    ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -118,7 +119,7 @@ class Workload:
             _lib.check(rc, "fold")
 
 
-def cpu_baseline(wl: Workload, ncols: int):
+def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
     """Oracle on host cores over a bounded column sample of the same workload."""
     from oracle import fedavg_oracle as O  # checker / CPU baseline only
     from oracle import oracle_lib as OL
@@ -130,13 +131,16 @@ def cpu_baseline(wl: Workload, ncols: int):
     sample_bytes = wl.N * ncols * (4 if wl.dtype == "f32" else 2) + ncols * 4
     # (i) literal numpy restatement of fed_avg_aggregator.py:24-42 (1 core: numpy ufuncs are single-threaded)
     params = [[Xh[i]] for i in range(wl.N)]
-    t0 = time.perf_counter()
-    if wl.scored:
-        ref = O.stall_aware_literal([{"round_id": r} for r in synth.round_ids(wl.seed, wl.N, 10, 2)], 10,
-                                    params, wl.weights)[0]
-    else:
-        ref = O.fedavg_literal(params, wl.weights)[0]
-    t_np = time.perf_counter() - t0
+    t_np_all = []
+    for _ in range(max(1, reps)):
+        t0 = time.perf_counter()
+        if wl.scored:
+            ref = O.stall_aware_literal([{"round_id": r} for r in synth.round_ids(wl.seed, wl.N, 10, 2)], 10,
+                                        params, wl.weights)[0]
+        else:
+            ref = O.fedavg_literal(params, wl.weights)[0]
+        t_np_all.append(time.perf_counter() - t0)
+    t_np = sorted(t_np_all)[len(t_np_all) // 2]
     del params
     # (ii) bit-identical C restatement, OpenMP over all host cores
     threads = OL.max_threads()
@@ -153,7 +157,8 @@ def cpu_baseline(wl: Workload, ncols: int):
     return {
         "value": round(sample_bytes / t_np / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
         "sample": f"{wl.N} clients x first {ncols} params of the same workload; numpy literal restatement "
-                  f"of fed_avg_aggregator.py:24-42 (1 core, numpy ufuncs single-threaded), {t_np:.2f} s",
+                  f"of fed_avg_aggregator.py:24-42 (1 core, numpy ufuncs single-threaded), median of {len(t_np_all)} runs {t_np:.2f} s "
+                  f"(total {sum(t_np_all):.1f} s)",
         "omp": {"value": round(sample_bytes / min(t_omp) / 1e9, 3), "unit": "GB/s", "cores": threads,
                 "kind": "port", "impl": "oracle/fedavg_ref.c (bit-identical, OpenMP)"},
         "host_cpus_visible": len(os.sched_getaffinity(0)),
@@ -236,6 +241,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg = float(t.item())
 
+    # streaming-read ceiling over the same HBM bytes (contiguous, no fold)
+    ceiling = None
+    if wl.dtype == "f32":
+        nfl = wl.N * wl.P
+        sink = torch.empty(8192, dtype=torch.float32, device=dev)
+        ts = []
+        for k in range(max(3, min(args.steps, 10)) + 2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            _lib.check(L.fa_read_sweep_f32(wl.X.data_ptr(), nfl - nfl % 4, sink.data_ptr(), 8192,
+                                           stream.cuda_stream), "read_sweep")
+            e1.record(stream)
+            e1.synchronize()
+            if k >= 2:
+                ts.append(e0.elapsed_time(e1))
+        ceiling = (nfl - nfl % 4) * 4 / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9
+
     total_bytes = world * wl.bytes * args.steps
     value = total_bytes / elapsed / 1e9
     achieved = wl.bytes / (kern_avg * 1e-3) / 1e9
@@ -243,7 +265,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(wl, args.cpu_cols)
+            cpu = cpu_baseline(wl, args.cpu_cols, args.cpu_reps)
         except Exception as e:  # the baseline must never hide the GPU result
             cpu = {"error": repr(e)}
     if rank == 0:
@@ -278,6 +300,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "kernel_ms_avg": round(kern_avg, 4),
+                "read_sweep_ceiling": None if ceiling is None else round(ceiling, 1),
+                "frac_of_read_ceiling": None if ceiling is None else round(achieved / ceiling, 4),
                 "bytes_per_launch": wl.bytes,
             },
             "cpu_baseline": cpu,

@@ -83,57 +83,88 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 
 // ---------------------------------------------------------------------------
 // fp32 fold over a stacked matrix, 16 B per lane per client row.
-//   X4   : [N][ldq] f32x4 (ldq = ldx/4), 16-byte aligned rows
-//   nq   : full f32x4 quads per row (P/4); a trailing P%4 tail is folded by
-//          the lane q == nq with scalar loads (one wave diverges, once).
-// Template: U = client rows loaded ahead of the ordered adds; NT = non-temporal
-// (read-once) loads; SCORED = stall-aware second multiply; ACC = continue a
-// fold from acc_in; FIN = divide at the end.
+//   X viewed as [N][ldq] f32x4 (ldq = ldx/4), 16-byte aligned rows.
+//   A lane owns C quads spaced kBlock apart (a block covers C*kBlock quads =
+//   C*4 KiB of every client row); nq = P/4 full quads, and the trailing P%4
+//   columns are folded by the lane whose first quad index == nq.
+// Template: U = client rows loaded ahead of the ordered adds; C = quads per
+// lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
+// multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
 // ---------------------------------------------------------------------------
-template <int U, bool NT, bool SCORED, bool ACC, bool FIN>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
+__device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
+                                           const float* __restrict__ a, const float* __restrict__ s,
+                                           const f32x4* __restrict__ acc_in, float divisor,
+                                           f32x4* __restrict__ out) {
+    f32x4 acc[C];
+    int64_t i = 0;
+    if constexpr (ACC) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = acc_in[c * kBlock];
+    } else {
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(ld4<NT>(p + c * kBlock), a0, s0);
+        i = 1;
+    }
+    for (; i + U <= N; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = ld4<NT>(p + (i + u) * ldq + c * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(v[u][c], ai, si));
+        }
+    }
+    for (; i < N; ++i) {
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * kBlock), ai, si));
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) out[c * kBlock] = FIN ? div4(acc[c], divisor) : acc[c];
+}
+
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
     const float* __restrict__ acc_in, float divisor, float* __restrict__ out) {
     const int64_t nq = P >> 2;
-    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (q < nq) {
-        const int64_t ldq = ldx >> 2;
-        const f32x4* __restrict__ p = reinterpret_cast<const f32x4*>(X) + q;
-        f32x4 acc;
-        int64_t i = 0;
-        if constexpr (ACC) {
-            acc = reinterpret_cast<const f32x4*>(acc_in)[q];
-        } else {
-            acc = term4<SCORED>(ld4<NT>(p), a[0], SCORED ? s[0] : 1.0f);
-            i = 1;
-        }
-        for (; i + U <= N; i += U) {
-            f32x4 v[U];
+    const int64_t ldq = ldx >> 2;
+    const int64_t q0 = (int64_t)blockIdx.x * (kBlock * C) + threadIdx.x;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    if (q0 + (int64_t)(C - 1) * kBlock < nq) {
+        // every quad of this lane is in range (all blocks but the last)
+        fold_quads<U, C, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+        return;
+    }
 #pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = ld4<NT>(p + (i + u) * ldq);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
-        }
-        for (; i < N; ++i)
-            acc = add4(acc, term4<SCORED>(ld4<NT>(p + i * ldq), a[i], SCORED ? s[i] : 1.0f));
-        if constexpr (FIN) acc = div4(acc, divisor);
-        reinterpret_cast<f32x4*>(out)[q] = acc;
-    } else if (q == nq && (P & 3)) {
+    for (int c = 0; c < C; ++c) {
+        const int64_t q = q0 + (int64_t)c * kBlock;
+        if (q < nq)
+            fold_quads<U, 1, NT, SCORED, ACC, FIN>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
+    }
+    if (q0 == nq && (P & 3)) {
         // column tail: at most 3 columns, scalar loads, same order
-        for (int64_t c = nq * 4; c < P; ++c) {
+        for (int64_t col = nq * 4; col < P; ++col) {
             float acc;
             int64_t i = 0;
             if constexpr (ACC) {
-                acc = acc_in[c];
+                acc = acc_in[col];
             } else {
-                acc = term1<SCORED>(X[c], a[0], SCORED ? s[0] : 1.0f);
+                acc = term1<SCORED>(X[col], a[0], SCORED ? s[0] : 1.0f);
                 i = 1;
             }
-            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + c], a[i], SCORED ? s[i] : 1.0f);
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
             if constexpr (FIN) acc = acc / divisor;
-            out[c] = acc;
+            out[col] = acc;
         }
     }
 }
@@ -364,15 +395,21 @@ __global__ __launch_bounds__(kBlock) void k_synth(OutT* __restrict__ X, int64_t 
     }
 }
 
-// contiguous streaming read (calibration ceiling for the fold)
+// contiguous streaming read (calibration ceiling for the fold): grid-stride,
+// 8 independent 16-byte non-temporal loads in flight per lane.
 __global__ __launch_bounds__(kBlock) void k_read_sweep(const f32x4* __restrict__ X, int64_t nq,
                                                         float* __restrict__ sink) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq;
-         q += (int64_t)gridDim.x * kBlock) {
-        f32x4 v = __builtin_nontemporal_load(X + q);
-        acc = add4(acc, v);
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; q + 7 * stride < nq; q += 8 * stride) {
+        f32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(X + q + k * stride);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = add4(acc, v[k]);
     }
+    for (; q < nq; q += stride) acc = add4(acc, __builtin_nontemporal_load(X + q));
     float t = acc.x + acc.y + acc.z + acc.w;
     for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
     __shared__ float red[kBlock / 64];
@@ -398,27 +435,30 @@ int check_common(int64_t N, int64_t P, int64_t ldx, const void* X, const void* a
 
 struct F32Variant {
     const char* name;
-    int unroll;
-    bool nt;
+    int unroll;  // client rows loaded ahead of the ordered adds
+    int quads;   // 16-byte quads per lane (block covers quads * 4 KiB per row)
+    bool nt;     // non-temporal loads
 };
 // variant 0 is the shipped default (chosen from the on-device sweep)
 constexpr F32Variant kVariants[] = {
-    {"v4u16nt", 16, true}, {"v4u8nt", 8, true}, {"v4u16", 16, false},
-    {"v4u8", 8, false},    {"v4u4nt", 4, true}, {"v4u32nt", 32, true},
+    {"u4c4nt", 4, 4, true}, {"u8c1nt", 8, 1, true}, {"u16c1", 16, 1, false}, {"u4c1nt", 4, 1, true},
+    {"u8c2nt", 8, 2, true}, {"u16c1nt", 16, 1, true}, {"u16c2nt", 16, 2, true}, {"u2c8nt", 2, 8, true},
+    {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int U, bool NT, bool SC, bool ACC, bool FIN>
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
-    hipLaunchKernelGGL((k_fold_f32_v4<U, NT, SC, ACC, FIN>), grid_for((P >> 2) + 1), dim3(kBlock), 0,
+    const int64_t lanes = ((P >> 2) + 1 + C - 1) / C;  // +1: the column-tail lane
+    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN>), grid_for(lanes), dim3(kBlock), 0,
                        st, X, N, P, ldx, a, s, acc_in, d, out);
 }
 
-template <int U, bool NT>
+template <int U, int C, bool NT>
 void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
-#define FA_V4(SC, ACC, FIN) launch_v4<U, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out)
+#define FA_V4(SC, ACC, FIN) launch_v4<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out)
     if (sc) {
         if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
         else     { if (fin) FA_V4(true, false, true); else FA_V4(true, false, false); }
@@ -463,20 +503,18 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #undef FA_SC
         return check_launch("k_fold_f32_scalar");
     }
-    const F32Variant& v = kVariants[variant];
-#define FA_VF(U, NT) launch_v4_flags<U, NT>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
-    if (v.nt) {
-        switch (v.unroll) {
-            case 4: FA_VF(4, true); break;
-            case 8: FA_VF(8, true); break;
-            case 16: FA_VF(16, true); break;
-            default: FA_VF(32, true); break;
-        }
-    } else {
-        switch (v.unroll) {
-            case 8: FA_VF(8, false); break;
-            default: FA_VF(16, false); break;
-        }
+#define FA_VF(U, C, NT) launch_v4_flags<U, C, NT>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+    switch (variant) {  // must match kVariants[]
+        case 0: FA_VF(4, 4, true); break;
+        case 1: FA_VF(8, 1, true); break;
+        case 2: FA_VF(16, 1, false); break;
+        case 3: FA_VF(4, 1, true); break;
+        case 4: FA_VF(8, 2, true); break;
+        case 5: FA_VF(16, 1, true); break;
+        case 6: FA_VF(16, 2, true); break;
+        case 7: FA_VF(2, 8, true); break;
+        case 8: FA_VF(4, 2, true); break;
+        default: FA_VF(2, 4, true); break;
     }
 #undef FA_VF
     return check_launch("k_fold_f32_v4");

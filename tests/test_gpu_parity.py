@@ -295,9 +295,8 @@ def _full_size_check(dev, lib, N, P, seed, dtype, scored, card_hi=600, ncheck=40
     torch.cuda.empty_cache()
     rng = np.random.default_rng(seed)
     # a contiguous block at each end + random 4-column groups across the row
-    cols = np.unique(np.concatenate([np.arange(0, 1024), np.arange(P - 1024, P),
-                                     (rng.integers(0, P // 4, ncheck) * 4)[:, None] + np.arange(4)[None, :]
-                                     ]).ravel())
+    quads = (rng.integers(0, P // 4, ncheck) * 4)[:, None] + np.arange(4)[None, :]
+    cols = np.unique(np.concatenate([np.arange(0, 1024), np.arange(P - 1024, P), quads.ravel()]))
     got = out.cpu().numpy()[cols]
     a = np.array(w, np.float32)
     s = None if sc is None else np.array(sc, np.float32)
