@@ -36,17 +36,21 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
+from fedlesscan_amd.sharding import ShardedAggregator, bucket_bounds  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 CONFIGS = {
-    # name: (clients, params per rank, dtype, scored, seed, card_hi, description)
-    "c2": (100, 1_000_000, "f32", False, 2, 600, "100 clients x 1M fp32 FedAvg, 1 MI355X (BASELINE config 2)"),
-    "c3": (1024, 10_000_000, "f32", False, 3, 600,
-           "1024 clients x 10M fp32 FedAvg, device-resident (BASELINE config 3, headline)"),
-    "c4": (256, 12_500_000, "bf16", False, 4, 600,
-           "256 clients x 100M bf16, one 12.5M-param bucket per GPU (BASELINE config 4 shard)"),
-    "c5": (512, 25_000_000, "f32", True, 5, 2000,
+    # name: (clients, params, dtype, scored, seed, card_hi, scaling, description)
+    #   scaling "weak":   `params` per GPU, the model grows with the GPU count
+    #   scaling "strong": `params` in total, split into per-GPU buckets
+    "c2": (100, 1_000_000, "f32", False, 2, 600, "weak",
+           "100 clients x 1M fp32 FedAvg, 1 MI355X (BASELINE config 2)"),
+    "c3": (1024, 10_000_000, "f32", False, 3, 600, "weak",
+           "1024 clients x 10M fp32 FedAvg per GPU, device-resident (BASELINE config 3, headline)"),
+    "c4": (256, 100_000_000, "bf16", False, 4, 600, "strong",
+           "256 clients x 100M bf16, parameter buckets over the GPUs + RCCL gather (BASELINE config 4)"),
+    "c5": (512, 25_000_000, "f32", True, 5, 2000, "weak",
            "512 clients x 25M fp32 FedLesScan stall-aware, tolerance 2, R=10 (BASELINE config 5)"),
 }
 
@@ -74,25 +78,33 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("FEDAVG_BENCH_BACKEND") == "gloo":
+            # rehearsal on a box with fewer GPUs than ranks: ranks share devices,
+            # the gather goes through gloo (host memory); never a headline number
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", torch.cuda.current_device())
 
 
 class Workload:
-    def __init__(self, cfg, rank, dev):
-        self.N, self.P, self.dtype, self.scored, self.seed, card_hi, self.desc = cfg
+    def __init__(self, cfg, rank, world, dev):
+        self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
+        self.P_total = P * world if self.scaling == "weak" else P
+        lo, hi = bucket_bounds(self.P_total, world)[rank]  # this rank's parameter bucket
+        self.P = hi - lo
         self.rank, self.dev = rank, dev
         L = _lib.load()
         st = torch.cuda.current_stream(dev).cuda_stream
         tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
         self.X = torch.empty((self.N, self.P), dtype=tdt, device=dev)
-        col0 = rank * self.P  # this rank's parameter bucket of the global model
         gen = L.fa_synth_f32 if self.dtype == "f32" else L.fa_synth_bf16
-        _lib.check(gen(self.X.data_ptr(), self.N, self.P, self.P, self.seed, 0, col0, st), "synth")
-        self.col0 = col0
+        _lib.check(gen(self.X.data_ptr(), self.N, self.P, self.P, self.seed, 0, lo, st), "synth")
+        self.col0 = lo
         self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
         self.scores = ([(r + 1) / 11 for r in synth.round_ids(self.seed, self.N, 10, 2)]
                        if self.scored else None)
@@ -113,8 +125,8 @@ class Workload:
             rc = L.fa_fedavg_f32_variant(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s,
                                          self.div, self.out.data_ptr(), st, variant)
         else:
-            rc = L.fa_fedavg_bf16(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s, self.div,
-                                  self.out.data_ptr(), None, st)
+            rc = L.fa_fedavg_bf16_variant(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s,
+                                          self.div, self.out.data_ptr(), None, st, variant)
         if rc:
             _lib.check(rc, "fold")
 
@@ -183,13 +195,17 @@ def main():
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
     cfg = CONFIGS[args.config]
-    wl = Workload(cfg, rank, dev)
+    wl = Workload(cfg, rank, world, dev)
     L = _lib.load()
-    gathered = torch.empty(world * wl.P, dtype=torch.float32, device=dev) if world > 1 else None
+    sharded = ShardedAggregator() if world > 1 else None
+    from fedlesscan_amd.sharding import chunk_size
+    gathered = (torch.empty(chunk_size(wl.P_total, world) * world, dtype=torch.float32, device=dev)
+                if world > 1 else None)
     stream = torch.cuda.current_stream(dev)
 
     if args.sweep and rank == 0:
-        nvar = L.fa_num_variants() if wl.dtype == "f32" else 1
+        nvar = L.fa_num_variants() if wl.dtype == "f32" else L.fa_num_bf16_variants()
+        vname = L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name
         res = {v: [] for v in range(nvar)}
         for _ in range(2):
             for v in range(nvar):
@@ -204,7 +220,7 @@ def main():
                 res[v].append(e0.elapsed_time(e1))
         for v, ts in res.items():
             ts = sorted(ts)
-            log(f"variant {v} {L.fa_variant_name(v).decode():10s} median {ts[len(ts)//2]:.3f} ms  "
+            log(f"variant {v} {vname(v).decode():10s} median {ts[len(ts)//2]:.3f} ms  "
                 f"min {ts[0]:.3f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
 
     def step(events=None):
@@ -213,8 +229,8 @@ def main():
         wl.launch(args.variant)
         if events is not None:
             events[1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, wl.out)
+        if world > 1:  # reassemble the global model: RCCL all-gather over xGMI
+            sharded.gather(wl.out, wl.P_total, out=gathered)
 
     for _ in range(args.warmup):
         step()
@@ -234,6 +250,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    gather_ok = None
+    if world > 1:  # my bucket inside the reassembled model must be my fold output, bit for bit
+        lo = wl.col0
+        ok = torch.equal(gathered[lo:lo + wl.P].view(torch.int32), wl.out.view(torch.int32))
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        gather_ok = bool(t.item())
     kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
     kern_avg = float(np.mean(kern_ms))
     if world > 1:
@@ -258,7 +281,10 @@ def main():
                 ts.append(e0.elapsed_time(e1))
         ceiling = (nfl - nfl % 4) * 4 / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9
 
-    total_bytes = world * wl.bytes * args.steps
+    tb = torch.tensor([float(wl.bytes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tb)  # units all ranks processed
+    total_bytes = float(tb.item()) * args.steps
     value = total_bytes / elapsed / 1e9
     achieved = wl.bytes / (kern_avg * 1e-3) / 1e9
     traffic, traffic_src = read_traffic(args.config)
@@ -278,7 +304,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl.scaling,
             "vs_baseline": None,
             "dtype": "f32" if wl.dtype == "f32" else "bf16-in/f32-acc",
             "data": "synthetic (integer-exact splitmix64 generator, generated in HBM)",
@@ -286,10 +312,11 @@ def main():
                 "workload": cfg[6],
                 "clients": wl.N,
                 "params_per_gpu": wl.P,
-                "params_total": wl.P * world,
+                "params_total": wl.P_total,
                 "layout": "row-stacked [clients][params] fp32 in HBM",
                 "parallelism": f"param-bucket x{world}" + (" + RCCL all_gather" if world > 1 else ""),
-                "variant": L.fa_variant_name(args.variant).decode() if wl.dtype == "f32" else "bf16_v8u8",
+                "variant": (L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name)(
+                    args.variant).decode(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -305,6 +332,7 @@ def main():
                 "bytes_per_launch": wl.bytes,
             },
             "cpu_baseline": cpu,
+            "gather_check": gather_ok,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

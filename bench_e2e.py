@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""End-to-end aggregation rate from host-resident serialized client blobs.
+
+    python bench_e2e.py [--clients N] [--params P] [--reps R]
+
+What the reference's aggregator function actually does per round
+(aggregation.py:87-97, fed_avg_aggregator.py:57-92): N ClientResult objects
+holding NPZ blobs -> decode -> weighted fold -> parameters.  Timed here:
+
+  gpu_e2e   FedAvgAggregator.aggregate(ClientResults) of this package: zero-copy
+            NPZ views -> pinned chunks -> H2D (copy stream) -> in-order chunked
+            HIP fold -> D2H of the result, returned as numpy layers
+  cpu_ref   the oracle's restatement of the same call (np.load decode + numpy
+            fold on one core), i.e. the reference's own cost on this host
+  h2d       pinned host->device copy bandwidth of the same bytes (PCIe bound)
+
+Rates are input bytes (N * P * 4) per second.  Results are compared bit for bit.
+Writes one JSON line (rank 0, one GPU).  Not the headline metric: DESIGN.md.
+"""
+from __future__ import annotations
+
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from fedlesscan_amd import FedAvgAggregator, synth  # noqa: E402
+from fedlesscan_amd.common.models import (ClientResult, NpzWeightsSerializerConfig,  # noqa: E402
+                                          SerializedParameters, WeightsSerializerConfig)
+
+MNIST_LIKE = [(5, 5, 1, 32), (32,), (5, 5, 32, 64), (64,), (1024, 512), (512,), (512, 10), (10,)]
+
+
+def make_blobs(N, P, seed):
+    from oracle import oracle_lib as OL  # fast host generator (test/bench infrastructure)
+    blobs = []
+    for i in range(N):
+        row = OL.synth_f32(seed, 1, P, row0=i)[0]
+        # split the row into a few layers like a Keras get_weights() list
+        cuts = [0, P // 64, P // 8, P // 2, P]
+        layers = [row[cuts[k]:cuts[k + 1]].reshape(-1, 1) if k % 2 else row[cuts[k]:cuts[k + 1]]
+                  for k in range(4)]
+        f = io.BytesIO()
+        np.savez(f, *layers)
+        blobs.append(f.getvalue())
+    return blobs
+
+
+def results(blobs, cards):
+    cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
+    return [ClientResult(parameters=SerializedParameters(blob=b, serializer=cfg), cardinality=c)
+            for b, c in zip(blobs, cards)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=100)
+    ap.add_argument("--params", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+    from oracle import fedavg_oracle as O  # checker + CPU reference timing only
+    N, P = a.clients, a.params
+    t0 = time.time()
+    blobs = make_blobs(N, P, a.seed)
+    cards = synth.cardinalities(a.seed, N)
+    gen_s = time.time() - t0
+    in_bytes = N * P * 4
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+
+    # warm up the pipeline (pinned allocations, library load)
+    FedAvgAggregator().aggregate(results(blobs[: min(N, 4)], cards[: min(N, 4)]), None)
+    torch.cuda.synchronize()
+    ts, out = [], None
+    for _ in range(a.reps):
+        crs = results(blobs, cards)
+        t0 = time.perf_counter()
+        out, _ = FedAvgAggregator().aggregate(crs, None)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t_gpu = sorted(ts)[len(ts) // 2]
+
+    # decode-only (zero-copy views) and pinned H2D of the same bytes
+    from fedlesscan_amd.npz import read_layers
+    t0 = time.perf_counter()
+    for b in blobs:
+        read_layers(b)
+    t_decode = time.perf_counter() - t0
+    host = torch.empty(min(in_bytes // 4, 1 << 28), dtype=torch.float32, pin_memory=True)
+    dbuf = torch.empty_like(host, device=dev)
+    dbuf.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dbuf.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_gbs = 3 * host.numel() * 4 / (time.perf_counter() - t0) / 1e9
+
+    res = {
+        "metric": "end-to-end aggregation GB/s from host NPZ blobs (not the headline)",
+        "clients": N, "params": P, "input_bytes": in_bytes, "gen_s": round(gen_s, 1),
+        "gpu_e2e_s": round(t_gpu, 4), "gpu_e2e_gbs": round(in_bytes / t_gpu / 1e9, 2),
+        "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),
+    }
+    if not a.no_cpu:
+        dicts = [{"blob": b, "cardinality": c} for b, c in zip(blobs, cards)]
+        t0 = time.perf_counter()
+        ref, _ = O.aggregate_fedavg(dicts)
+        t_cpu = time.perf_counter() - t0
+        res["cpu_ref_s"] = round(t_cpu, 3)
+        res["cpu_ref_gbs"] = round(in_bytes / t_cpu / 1e9, 3)
+        res["cpu_ref_cores"] = 1
+        res["speedup_vs_cpu_ref"] = round(t_cpu / t_gpu, 1)
+        res["bit_exact"] = all(np.array_equal(x.view(np.uint32), y.view(np.uint32)) and x.shape == y.shape
+                               for x, y in zip(out, ref))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -47,6 +47,9 @@ _PROTOS = {
     "fa_fedavg_f32_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
     "fa_num_variants": (_int, []),
     "fa_variant_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
+    "fa_num_bf16_variants": (_int, []),
+    "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
 }
 
 _lock = threading.Lock()

@@ -43,8 +43,8 @@ def resolve_cardinality(cardinality, default_cardinality):
 
 def decode_result(result: ClientResult, default_cardinality):
     """Deserialize one ClientResult and release its blob (`del client_result.parameters`)."""
-    params = deserialize_parameters(result.parameters)
-    result.parameters = None
+    params = deserialize_parameters(result.parameters, zero_copy=True)
+    result.parameters = None  # the reference's `del client_result.parameters`
     return params, resolve_cardinality(result.cardinality, default_cardinality), result.test_metrics
 
 

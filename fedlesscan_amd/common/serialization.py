@@ -77,7 +77,9 @@ class WeightsSerializerBuilder:
         raise NotImplementedError(f"Serializer of type {config.type} does not exist")
 
 
-def deserialize_parameters(serialized: SerializedParameters) -> List[np.ndarray]:
+def deserialize_parameters(serialized: SerializedParameters, zero_copy: bool = False) -> List[np.ndarray]:
+    """serialization.py:80-93.  zero_copy=True returns read-only views into the
+    blob for uncompressed NPZ (fedlesscan_amd.npz) -- same values, no copy."""
     serializer = WeightsSerializerBuilder.from_config(serialized.serializer)
     if serialized.string_format == BinaryStringFormat.BASE64:
         try:
@@ -88,4 +90,12 @@ def deserialize_parameters(serialized: SerializedParameters) -> List[np.ndarray]
         blob = serialized.blob
     else:
         raise SerializationError(f"Binary string format {serialized.string_format} not known")
+    if zero_copy and not serializer.compressed:
+        from ..npz import read_layers
+        try:
+            return read_layers(blob)
+        except MemoryError:
+            raise
+        except Exception as e:
+            raise SerializationError(e) from e
     return serializer.deserialize(blob)

@@ -94,8 +94,7 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
 __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
                                            const float* __restrict__ a, const float* __restrict__ s,
-                                           const f32x4* __restrict__ acc_in, float divisor,
-                                           f32x4* __restrict__ out) {
+                                           const f32x4* acc_in, float divisor, f32x4* out) {
     f32x4 acc[C];
     int64_t i = 0;
     if constexpr (ACC) {
@@ -133,7 +132,7 @@ template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
-    const float* __restrict__ acc_in, float divisor, float* __restrict__ out) {
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
     const int64_t nq = P >> 2;
     const int64_t ldq = ldx >> 2;
     const int64_t q0 = (int64_t)blockIdx.x * (kBlock * C) + threadIdx.x;
@@ -174,7 +173,7 @@ template <bool SCORED, bool ACC, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
-    const float* __restrict__ acc_in, float divisor, float* __restrict__ out) {
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
     const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (c >= P) return;
     float acc;
@@ -239,74 +238,105 @@ __device__ __forceinline__ uint16_t f2bf_rne(float f) {
     return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 
-template <int U, bool SCORED>
+// A 16-byte load holds 8 bf16 = 4 words; the low half of word k is column 2k,
+// the high half column 2k+1.  Exact upcast = the half moved to the top of an
+// f32, so the 8 columns fold as two f32x4 (even / odd columns).
+__device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) {
+    even = __builtin_bit_cast(f32x4, w << 16);
+    odd = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
+}
+
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
+                                            const float* __restrict__ a, const float* __restrict__ s,
+                                            float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
+                                            int64_t o0) {
+    f32x4 ev[C], od[C];
+    {
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + c * kBlock), e, o);
+            ev[c] = term4<SCORED>(e, a0, s0);
+            od[c] = term4<SCORED>(o, a0, s0);
+        }
+    }
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        u32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                f32x4 e, o;
+                unpack_bf16x8(v[u][c], e, o);
+                ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
+                od[c] = add4(od[c], term4<SCORED>(o, ai, si));
+            }
+        }
+    }
+    for (; i < N; ++i) {
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + i * ldo + c * kBlock), e, o);
+            ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
+            od[c] = add4(od[c], term4<SCORED>(o, ai, si));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
+        const int64_t oc = o0 + (int64_t)c * kBlock;
+        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
+        o4[0] = f32x4{e.x, o.x, e.y, o.y};
+        o4[1] = f32x4{e.z, o.z, e.w, o.w};
+        if (outb) {
+            u32x4 b;
+            b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
+            b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
+            b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
+            b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
+            reinterpret_cast<u32x4*>(outb)[oc] = b;
+        }
+    }
+}
+
+// bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
+// spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
+template <int U, int C, bool SCORED>
 __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
     const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s, float divisor,
     float* __restrict__ out, uint16_t* __restrict__ outb) {
     const int64_t no = P >> 3;  // full octets
-    const int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (o < no) {
-        const int64_t ldo = ldx >> 3;
-        const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(X) + o;
-        float acc[8];
-        {
-            u32x4 v = __builtin_nontemporal_load(p);
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+    const int64_t ldo = ldx >> 3;
+    const int64_t o0 = (int64_t)blockIdx.x * (kBlock * C) + threadIdx.x;
+    const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
+    if (o0 + (int64_t)(C - 1) * kBlock < no) {
+        fold_octets<U, C, SCORED>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+        return;
+    }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                acc[2 * k] = term1<SCORED>(bf2f(w[k] & 0xFFFFu), a0, s0);
-                acc[2 * k + 1] = term1<SCORED>(bf2f(w[k] >> 16), a0, s0);
-            }
-        }
-        int64_t i = 1;
-        for (; i + U <= N; i += U) {
-            u32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldo);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    acc[2 * k] = acc[2 * k] + term1<SCORED>(bf2f(w[k] & 0xFFFFu), ai, si);
-                    acc[2 * k + 1] = acc[2 * k + 1] + term1<SCORED>(bf2f(w[k] >> 16), ai, si);
-                }
-            }
-        }
-        for (; i < N; ++i) {
-            u32x4 v = __builtin_nontemporal_load(p + i * ldo);
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const float ai = a[i], si = SCORED ? s[i] : 1.0f;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                acc[2 * k] = acc[2 * k] + term1<SCORED>(bf2f(w[k] & 0xFFFFu), ai, si);
-                acc[2 * k + 1] = acc[2 * k + 1] + term1<SCORED>(bf2f(w[k] >> 16), ai, si);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = acc[k] / divisor;
-        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * o;
-        o4[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
-        o4[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
-        if (outb) {
-            u32x4 b;
-            b.x = (uint32_t)f2bf_rne(acc[0]) | ((uint32_t)f2bf_rne(acc[1]) << 16);
-            b.y = (uint32_t)f2bf_rne(acc[2]) | ((uint32_t)f2bf_rne(acc[3]) << 16);
-            b.z = (uint32_t)f2bf_rne(acc[4]) | ((uint32_t)f2bf_rne(acc[5]) << 16);
-            b.w = (uint32_t)f2bf_rne(acc[6]) | ((uint32_t)f2bf_rne(acc[7]) << 16);
-            reinterpret_cast<u32x4*>(outb)[o] = b;
-        }
-    } else if (o == no && (P & 7)) {
-        for (int64_t c = no * 8; c < P; ++c) {
-            float acc = term1<SCORED>(bf2f(X[c]), a[0], SCORED ? s[0] : 1.0f);
+    for (int c = 0; c < C; ++c) {
+        const int64_t o = o0 + (int64_t)c * kBlock;
+        if (o < no) fold_octets<U, 1, SCORED>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+    }
+    if (o0 == no && (P & 7)) {
+        for (int64_t col = no * 8; col < P; ++col) {
+            float acc = term1<SCORED>(bf2f(X[col]), a[0], SCORED ? s[0] : 1.0f);
             for (int64_t i = 1; i < N; ++i)
-                acc = acc + term1<SCORED>(bf2f(X[i * ldx + c]), a[i], SCORED ? s[i] : 1.0f);
+                acc = acc + term1<SCORED>(bf2f(X[i * ldx + col]), a[i], SCORED ? s[i] : 1.0f);
             acc = acc / divisor;
-            out[c] = acc;
-            if (outb) outb[c] = f2bf_rne(acc);
+            out[col] = acc;
+            if (outb) outb[col] = f2bf_rne(acc);
         }
     }
 }
@@ -446,6 +476,8 @@ constexpr F32Variant kVariants[] = {
     {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr const char* kBf16Variants[] = {"bf16u4c2", "bf16u8c1", "bf16u4c4", "bf16u2c4", "bf16u8c2"};
+constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
@@ -564,20 +596,34 @@ int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float
     return check_launch("k_fedavg_f32_ptrs");
 }
 
-int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                   float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                           const float* s, float divisor, float* out_f32, uint16_t* out_bf16, void* stream,
+                           int variant) {
     int rc = check_common(N, P, ldx, X, a, out_f32);
     if (rc) return rc;
+    if (variant < 0 || variant >= kNumBf16Variants) return fail(FA_ERR_ARG, "unknown bf16 variant %d", variant);
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
     const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && (!out_bf16 || aligned16(out_bf16));
     if (vec) {
-        if (s)
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<8, true>), grid_for((P >> 3) + 1), dim3(kBlock), 0, st, X, N,
-                               P, ldx, a, s, divisor, out_f32, out_bf16);
-        else
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<8, false>), grid_for((P >> 3) + 1), dim3(kBlock), 0, st, X,
-                               N, P, ldx, a, s, divisor, out_f32, out_bf16);
+#define FA_BF(U, C)                                                                                        \
+    {                                                                                                      \
+        const int64_t lanes = ((P >> 3) + 1 + (C)-1) / (C);                                                \
+        if (s)                                                                                             \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid_for(lanes), dim3(kBlock), 0, st, X, N, \
+                               P, ldx, a, s, divisor, out_f32, out_bf16);                                  \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid_for(lanes), dim3(kBlock), 0, st, X,   \
+                               N, P, ldx, a, s, divisor, out_f32, out_bf16);                               \
+    }
+        switch (variant) {  // must match kBf16Variants[]
+            case 0: FA_BF(4, 2); break;
+            case 1: FA_BF(8, 1); break;
+            case 2: FA_BF(4, 4); break;
+            case 3: FA_BF(2, 4); break;
+            default: FA_BF(8, 2); break;
+        }
+#undef FA_BF
         return check_launch("k_fedavg_bf16_v8");
     }
     if (s)
@@ -587,6 +633,16 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const f
         hipLaunchKernelGGL(k_fedavg_bf16_scalar<false>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
                            divisor, out_f32, out_bf16);
     return check_launch("k_fedavg_bf16_scalar");
+}
+
+int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                   float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+    return fa_fedavg_bf16_variant(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream, 0);
+}
+
+int fa_num_bf16_variants(void) { return kNumBf16Variants; }
+const char* fa_bf16_variant_name(int variant) {
+    return (variant >= 0 && variant < kNumBf16Variants) ? kBf16Variants[variant] : "";
 }
 
 int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const double* a, const double* s,

@@ -221,14 +221,31 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
     for _, lis in groups.items():
         sizes = [int(np.prod(shapes[li])) if len(shapes[li]) else 1 for li in lis]
         P = sum(sizes)
-        X = _stack_group(parameters, n_eff, lis, sizes, P, dev, on_device)
-        res = fold_stacked(X, w, sc, total=sum(total_weights))
+        if (not on_device and P > 0 and dtypes[lis[0]] == np.float32
+                and result_dtype(np.dtype(np.float32), total_weights, sc) == np.float32):
+            # host fp32 rows: pipelined pinned-chunk H2D + in-order chunked fold (bit-identical)
+            res = _stream_group(parameters, n_eff, lis, P, w, sc, sum(total_weights), dev)
+        else:
+            X = _stack_group(parameters, n_eff, lis, sizes, P, dev, on_device)
+            res = fold_stacked(X, w, sc, total=sum(total_weights))
         flat = res if on_device else res.cpu().numpy()
         off = 0
         for li, n in zip(lis, sizes):
             outs[li] = flat[off:off + n].reshape(shapes[li])
             off += n
     return outs
+
+
+STREAM_CHUNK_BYTES = 128 << 20  # pinned staging per chunk (two chunks in flight)
+
+
+def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
+    from .ingest import StreamingFold
+    rows = max(1, min(n, STREAM_CHUNK_BYTES // (4 * P)))
+    sf = StreamingFold(P, chunk_rows=rows, device=dev)
+    for i in range(n):
+        sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
+    return sf.finish(total=total)
 
 
 def _stack_group(parameters, n, lis, sizes, P, dev, on_device) -> torch.Tensor:

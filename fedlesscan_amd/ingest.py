@@ -1,0 +1,149 @@
+"""Pipelined host ingest: client rows -> pinned staging -> H2D -> in-order fold.
+
+The reference materialises every decoded client (aggregation.py:87-93) and
+then folds on one CPU core.  Here client rows are packed, in arrival order,
+into pinned host chunks of `chunk_rows` rows; each full chunk is copied to the
+GPU on a dedicated copy stream while the previous chunk is folded on the
+compute stream with fa_fold_f32 (accumulator carried across chunks, divide
+once at the end).  Folding in chunks with a carried accumulator performs the
+same additions in the same order, so the result is bit-identical to one
+fa_fedavg_f32 over all rows (tests/test_gpu_parity.py checks this).
+
+Memory: 2 pinned + 2 device chunks of chunk_rows x P floats and one [P]
+accumulator, independent of the number of clients.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .aggregator.exceptions import InvalidParameterShapeError
+
+
+class StreamingFold:
+    """Accumulate fp32 client rows on the GPU in order; `finish()` divides.
+
+    add(row, weight, score=None): row = flat float32 [P] (or a list of layers
+    that flatten to P), weight = the client's cardinality (Python scalar, rounded
+    to fp32 like numpy), score = stall-aware factor or None.  Either every row
+    has a score or none does.
+    """
+
+    def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
+                 pitch_align: int = 64):
+        if P <= 0:
+            raise InvalidParameterShapeError("StreamingFold needs P > 0")
+        self.P = P
+        self.dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.ldx = ((P + pitch_align - 1) // pitch_align) * pitch_align
+        self.R = max(1, chunk_rows)
+        self.host = [torch.empty((self.R, self.ldx), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        self.hview = [h.numpy() for h in self.host]
+        self.devbuf = [torch.empty((self.R, self.ldx), dtype=torch.float32, device=self.dev) for _ in range(2)]
+        self.acc = torch.empty(P, dtype=torch.float32, device=self.dev)
+        self.copy_stream = torch.cuda.Stream(device=self.dev)
+        self.compute = torch.cuda.current_stream(self.dev)
+        self.h2d_done = [torch.cuda.Event() for _ in range(2)]
+        self.fold_done = [torch.cuda.Event() for _ in range(2)]
+        self.fold_pending = [False, False]
+        self.buf = 0
+        self.fill = 0
+        self.weights: List = []
+        self.scored: Optional[bool] = None
+        self.chunk_a: List = [[], []]
+        self.chunk_s: List = [[], []]
+        self.started = False
+        self.rows = 0
+
+    # -- producer side ------------------------------------------------------
+    def _slot_ready(self, b: int):
+        # the pinned buffer b may be overwritten once its last H2D finished;
+        # its device twin once the fold that read it finished
+        if self.fold_pending[b]:
+            self.fold_done[b].synchronize()
+            self.fold_pending[b] = False
+
+    def add(self, row, weight, score: Optional[float] = None):
+        if self.scored is None:
+            self.scored = score is not None
+        elif self.scored != (score is not None):
+            raise InvalidParameterShapeError("either every row has a score or none does")
+        b = self.buf
+        if self.fill == 0:
+            self._slot_ready(b)
+        dst = self.hview[b][self.fill]
+        if isinstance(row, (list, tuple)):
+            off = 0
+            for layer in row:
+                flat = np.asarray(layer).reshape(-1)
+                if flat.dtype != np.float32:
+                    raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {flat.dtype}")
+                dst[off:off + flat.size] = flat
+                off += flat.size
+            if off != self.P:
+                raise InvalidParameterShapeError(f"row has {off} parameters, expected {self.P}")
+        else:
+            flat = np.asarray(row).reshape(-1)
+            if flat.size != self.P or flat.dtype != np.float32:
+                raise InvalidParameterShapeError(f"row must be float32[{self.P}]")
+            dst[: self.P] = flat
+        self.weights.append(weight)
+        self.chunk_a[b].append(weight)
+        self.chunk_s[b].append(score)
+        self.fill += 1
+        self.rows += 1
+        if self.fill == self.R:
+            self._flush()
+
+    def _flush(self, finalize: bool = False, total=None):
+        b, n = self.buf, self.fill
+        if n:
+            with torch.cuda.stream(self.copy_stream):
+                self.devbuf[b][:n].copy_(self.host[b][:n], non_blocking=True)
+                self.h2d_done[b].record(self.copy_stream)
+            self.compute.wait_event(self.h2d_done[b])
+            a = torch.tensor(np.array([np.float32(w) for w in self.chunk_a[b]], np.float32)).to(
+                self.dev, non_blocking=True)
+            s = None
+            if self.chunk_s[b][0] is not None:
+                s = torch.tensor(np.array([np.float32(x) for x in self.chunk_s[b]], np.float32)).to(
+                    self.dev, non_blocking=True)
+        div = float(np.float32(sum(self.weights) if total is None else total)) if finalize else 0.0
+        L = _lib.load()
+        st = self.compute.cuda_stream
+        if n:
+            _lib.check(L.fa_fold_f32(self.devbuf[b].data_ptr(), n, self.P, self.ldx, a.data_ptr(),
+                                     None if s is None else s.data_ptr(),
+                                     self.acc.data_ptr() if self.started else None, div, int(finalize),
+                                     self.acc.data_ptr(), st), "fa_fold_f32")
+            self.started = True
+            self.fold_done[b].record(self.compute)
+            self.fold_pending[b] = True
+        elif finalize:
+            _lib.check(L.fa_fold_f32(None, 0, self.P, self.ldx, None, None, self.acc.data_ptr(), div, 1,
+                                     self.acc.data_ptr(), st), "fa_fold_f32(finalize)")
+        self.chunk_a[b], self.chunk_s[b] = [], []
+        self.fill = 0
+        self.buf ^= 1
+
+    def finish(self, total=None) -> torch.Tensor:
+        """Fold the last partial chunk and divide by fl32(total or sum(weights))."""
+        if self.rows == 0:
+            _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
+        self._flush(finalize=True, total=total)
+        return self.acc
+
+
+def stream_layers(rows_iter, shapes: Sequence[tuple], weights_iter=None, chunk_rows: int = 16,
+                  device=None):
+    """Convenience: fold an iterator of (layers, weight[, score]) tuples."""
+    P = sum(int(np.prod(s)) if len(s) else 1 for s in shapes)
+    sf = StreamingFold(P, chunk_rows=chunk_rows, device=device)
+    for item in rows_iter:
+        layers, w = item[0], item[1]
+        sc = item[2] if len(item) > 2 else None
+        sf.add(layers, w, sc)
+    return sf.finish()

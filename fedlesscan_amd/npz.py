@@ -1,0 +1,91 @@
+"""Zero-copy NPZ reader for the client-update wire format.
+
+Clients write their weights with NpzWeightsSerializer (serialization.py:280-306,
+`np.savez`, ZIP_STORED unless compress_model is set; client.py:186-199).  An
+uncompressed .npz is a zip whose members arr_0.npy, arr_1.npy, ... hold raw
+.npy payloads, so every layer can be viewed in place inside the blob:
+
+    local file header (30 B + name + extra) -> .npy magic/header -> raw data
+
+`npz_views(blob)` returns numpy views into `blob` (no copy), in member order —
+the same order as `list(np.load(f).values())` — so the ingest pipeline can
+memcpy each layer straight into a pinned staging row.  Compressed members,
+Fortran-ordered or object arrays, and anything unexpected fall back to
+np.load (allow_pickle=False), so results never depend on which path ran.
+"""
+from __future__ import annotations
+
+import ast
+import io
+import struct
+import zipfile
+from typing import List, Optional
+
+import numpy as np
+
+_LOCAL_HDR = struct.Struct("<IHHHHHIIIHH")  # zip local file header (30 bytes)
+_LOCAL_SIG = 0x04034B50
+
+
+def _npy_payload(buf: memoryview, off: int):
+    """Parse a .npy header at `off`; return (dtype, shape, data_offset) or None."""
+    if bytes(buf[off:off + 6]) != b"\x93NUMPY":
+        return None
+    major = buf[off + 6]
+    if major == 1:
+        hlen = struct.unpack_from("<H", buf, off + 8)[0]
+        hstart = off + 10
+    elif major in (2, 3):
+        hlen = struct.unpack_from("<I", buf, off + 8)[0]
+        hstart = off + 12
+    else:
+        return None
+    try:
+        hdr = ast.literal_eval(bytes(buf[hstart:hstart + hlen]).decode("latin1"))
+    except (ValueError, SyntaxError):
+        return None
+    if not isinstance(hdr, dict) or hdr.get("fortran_order"):
+        return None
+    dt = np.dtype(hdr["descr"])
+    if dt.hasobject:
+        return None
+    return dt, tuple(hdr["shape"]), hstart + hlen
+
+
+def npz_views(blob) -> Optional[List[np.ndarray]]:
+    """Layer views into an uncompressed NPZ blob, or None if it needs np.load."""
+    buf = memoryview(blob)
+    try:
+        with zipfile.ZipFile(io.BytesIO(buf)) as zf:
+            infos = zf.infolist()
+    except zipfile.BadZipFile:
+        return None
+    out = []
+    for info in infos:
+        if info.compress_type != zipfile.ZIP_STORED or not info.filename.endswith(".npy"):
+            return None
+        off = info.header_offset
+        fields = _LOCAL_HDR.unpack_from(buf, off)
+        if fields[0] != _LOCAL_SIG:
+            return None
+        name_len, extra_len = fields[9], fields[10]
+        data = off + _LOCAL_HDR.size + name_len + extra_len
+        parsed = _npy_payload(buf, data)
+        if parsed is None:
+            return None
+        dt, shape, start = parsed
+        count = int(np.prod(shape)) if shape else 1
+        if start + count * dt.itemsize > data + info.file_size:
+            return None
+        out.append(np.frombuffer(buf, dtype=dt, count=count, offset=start).reshape(shape))
+    return out
+
+
+def read_layers(blob) -> List[np.ndarray]:
+    """Layers of an NPZ blob: zero-copy views when possible, np.load otherwise."""
+    v = npz_views(blob)
+    if v is not None:
+        return v
+    with io.BytesIO(bytes(blob)) as f:
+        with np.load(f, allow_pickle=False) as z:
+            return [z[k] for k in z.files]

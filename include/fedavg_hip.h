@@ -110,8 +110,14 @@ int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
                           const float* a, const float* s, float divisor,
                           float* out, void* stream, int variant);
 int fa_num_variants(void);
-/* [host] short name of a variant, e.g. "v4u8". */
+/* [host] short name of a variant, e.g. "u4c4nt". */
 const char* fa_variant_name(int variant);
+/* Same for the bf16 fold (variant 0 = fa_fedavg_bf16's default). */
+int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                           const float* a, const float* s, float divisor,
+                           float* out_f32, uint16_t* out_bf16, void* stream, int variant);
+int fa_num_bf16_variants(void);
+const char* fa_bf16_variant_name(int variant);
 
 #ifdef __cplusplus
 }

@@ -233,6 +233,24 @@ def test_bf16_matches_definition(dev, N, P, scored):
     assert np.array_equal(outb.view(torch.int16).cpu().numpy().view(np.uint16), expb)
 
 
+def test_bf16_variants_bit_identical(dev, lib):
+    L = lib.load()
+    N, P = 37, 8 * 3000 + 5
+    Xb = synth.clients_bf16(71, N, 0, P)
+    w = synth.cardinalities(71, N)
+    exp, expb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)))
+    Xd = torch.from_numpy(Xb.view(np.int16)).to(dev)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for v in range(L.fa_num_bf16_variants()):
+        o = torch.empty(P, dtype=torch.float32, device=dev)
+        ob = torch.empty(P, dtype=torch.int16, device=dev)
+        lib.check(L.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
+                                           o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
+        assert _bits_equal(o.cpu().numpy(), exp), v
+        assert np.array_equal(ob.cpu().numpy().view(np.uint16), expb), v
+
+
 def test_f64_and_int_paths(dev):
     from fedlesscan_amd import engine
     X = np.stack([p[0] for p in G.parameters("f64_n40")])

@@ -263,3 +263,35 @@ def test_test_metrics_are_collected(oracle_fold):
     _, metrics = FedAvgAggregator().aggregate(crs, None)
     assert len(metrics) == 1 and metrics[0].cardinality == 5
     assert crs[0].parameters is None  # blob released after decode, as the reference does
+
+
+# ---------------------------------------------------------------------------
+# zero-copy NPZ reader (fedlesscan_amd/npz.py) == np.load
+# ---------------------------------------------------------------------------
+def _savez(layers, compressed=False):
+    f = io.BytesIO()
+    (np.savez_compressed if compressed else np.savez)(f, *layers)
+    return f.getvalue()
+
+
+def test_npz_views_match_np_load():
+    from fedlesscan_amd.npz import npz_views, read_layers
+    layers = [np.arange(12, dtype=np.float32).reshape(3, 4), np.float32(3.5) * np.ones(()),
+              np.zeros((0, 5), np.float32), np.arange(7, dtype=np.int64), np.ones((2, 2, 2), np.float64),
+              np.arange(1000, dtype=np.float32)[::1]]
+    blob = _savez(layers)
+    v = npz_views(blob)
+    assert v is not None and len(v) == len(layers)
+    for a, b in zip(v, layers):
+        assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b)
+    # views alias the blob (no copy)
+    assert all(not x.flags.owndata for x in v)
+    # compressed and Fortran-ordered members fall back to np.load
+    assert npz_views(_savez(layers, compressed=True)) is None
+    assert npz_views(_savez([np.asfortranarray(np.ones((3, 4), np.float32))])) is None
+    for blob2 in (_savez(layers, compressed=True), _savez([np.asfortranarray(np.ones((3, 4), np.float32))])):
+        ref = [np.load(io.BytesIO(blob2))[k] for k in np.load(io.BytesIO(blob2)).files]
+        got = read_layers(blob2)
+        assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+    assert npz_views(b"junk") is None
+    assert npz_views(_savez([])) == []

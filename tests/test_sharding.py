@@ -1,0 +1,81 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): bucket partition, local
+fold of each bucket, all-gather reassembly.  The per-rank fold is the oracle
+here (no GPU in this container); the GPU fold itself is covered by
+test_gpu_parity.py.  Bit-exact against the oracle over the full matrix."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fedlesscan_amd import synth
+from fedlesscan_amd.sharding import ShardedAggregator, bucket_bounds, chunk_size
+
+
+def test_bucket_bounds_cover_and_align():
+    for P in (0, 1, 63, 64, 65, 1000, 10_000_000, 12_345_679):
+        for world in (1, 2, 3, 4, 7, 8):
+            b = bucket_bounds(P, world)
+            assert len(b) == world
+            assert b[0][0] == 0 and b[-1][1] == P
+            for (l0, h0), (l1, h1) in zip(b, b[1:]):
+                assert h0 == l1 and l0 <= h0
+            c = chunk_size(P, world)
+            nonempty = [hi - lo for lo, hi in b if hi > lo]
+            assert all(x == c for x in nonempty[:-1])
+            assert all(lo % 64 == 0 for lo, hi in b if hi > lo)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fold(X, w, s=None, **_):
+    from oracle import fedavg_oracle as O
+    return torch.from_numpy(O.fedavg_stacked(X.numpy(), w, s))
+
+
+def _worker(rank, world, port, N, P, seed, scored, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        agg = ShardedAggregator(fold=_oracle_fold)
+        lo, hi = agg.bounds(P)
+        X = torch.from_numpy(synth.clients_f32(seed, N, lo, hi - lo)) if hi > lo else torch.empty((N, 0))
+        w = synth.cardinalities(seed, N)
+        sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
+        full = agg.aggregate(X, w, sc, P=P)
+        q.put((rank, full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P,scored", [(2, 10007, False), (2, 4096, True), (3, 130, False)])
+def test_sharded_fold_gloo_matches_oracle(world, P, scored):
+    from oracle import fedavg_oracle as O
+    N, seed = 9, 17
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, P, seed, scored, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = synth.clients_f32(seed, N, 0, P)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
+    exp = O.fedavg_stacked(X, w, sc)
+    for r in range(world):
+        out = np.frombuffer(got[r], dtype=np.float32)
+        assert out.shape == exp.shape
+        assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
