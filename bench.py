@@ -309,7 +309,7 @@ def main():
             "dtype": "f32" if wl.dtype == "f32" else "bf16-in/f32-acc",
             "data": "synthetic (integer-exact splitmix64 generator, generated in HBM)",
             "config": {
-                "workload": cfg[6],
+                "workload": wl.desc,
                 "clients": wl.N,
                 "params_per_gpu": wl.P,
                 "params_total": wl.P_total,

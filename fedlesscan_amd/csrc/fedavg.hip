@@ -150,8 +150,10 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
         if (q < nq)
             fold_quads<U, 1, NT, SCORED, ACC, FIN>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
     }
-    if (q0 == nq && (P & 3)) {
-        // column tail: at most 3 columns, scalar loads, same order
+    // column tail: at most 3 columns, folded by the lane that would own quad
+    // index nq under the C-quads-per-lane mapping (scalar loads, same order)
+    const int64_t tb = nq / (kBlock * C), tl = (nq % (kBlock * C)) % kBlock;
+    if ((P & 3) && (int64_t)blockIdx.x == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = nq * 4; col < P; ++col) {
             float acc;
             int64_t i = 0;
@@ -329,7 +331,8 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
         const int64_t o = o0 + (int64_t)c * kBlock;
         if (o < no) fold_octets<U, 1, SCORED>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
-    if (o0 == no && (P & 7)) {
+    const int64_t tb = no / (kBlock * C), tl = (no % (kBlock * C)) % kBlock;
+    if ((P & 7) && (int64_t)blockIdx.x == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = no * 8; col < P; ++col) {
             float acc = term1<SCORED>(bf2f(X[col]), a[0], SCORED ? s[0] : 1.0f);
             for (int64_t i = 1; i < N; ++i)
@@ -482,8 +485,9 @@ constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
-    const int64_t lanes = ((P >> 2) + 1 + C - 1) / C;  // +1: the column-tail lane
-    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN>), grid_for(lanes), dim3(kBlock), 0,
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const dim3 grid((unsigned)((units + per_block - 1) / per_block));  // incl. the column-tail lane
+    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN>), grid, dim3(kBlock), 0,
                        st, X, N, P, ldx, a, s, acc_in, d, out);
 }
 
@@ -608,12 +612,13 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
     if (vec) {
 #define FA_BF(U, C)                                                                                        \
     {                                                                                                      \
-        const int64_t lanes = ((P >> 3) + 1 + (C)-1) / (C);                                                \
+        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);           \
+        const dim3 grid((unsigned)((units + per_block - 1) / per_block));                                  \
         if (s)                                                                                             \
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid_for(lanes), dim3(kBlock), 0, st, X, N, \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid, dim3(kBlock), 0, st, X, N,            \
                                P, ldx, a, s, divisor, out_f32, out_bf16);                                  \
         else                                                                                               \
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid_for(lanes), dim3(kBlock), 0, st, X,   \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X,              \
                                N, P, ldx, a, s, divisor, out_f32, out_bf16);                               \
     }
         switch (variant) {  // must match kBf16Variants[]

@@ -14,6 +14,8 @@ accumulator, independent of the number of clients.
 """
 from __future__ import annotations
 
+import os
+from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -31,6 +33,17 @@ class StreamingFold:
     to fp32 like numpy), score = stall-aware factor or None.  Either every row
     has a score or none does.
     """
+
+    _pool: Optional[ThreadPoolExecutor] = None
+
+    @classmethod
+    def _copy_pool(cls) -> ThreadPoolExecutor:
+        # numpy releases the GIL for plain memcpy-style assignment, so rows of a
+        # chunk are packed into pinned memory by several host threads at once
+        if cls._pool is None:
+            n = int(os.environ.get("FEDAVG_COPY_THREADS", "0")) or min(8, os.cpu_count() or 1)
+            cls._pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="fedavg-pack")
+        return cls._pool
 
     def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
                  pitch_align: int = 64):
@@ -57,6 +70,7 @@ class StreamingFold:
         self.chunk_s: List = [[], []]
         self.started = False
         self.rows = 0
+        self.pending: List = []
 
     # -- producer side ------------------------------------------------------
     def _slot_ready(self, b: int):
@@ -75,21 +89,17 @@ class StreamingFold:
         if self.fill == 0:
             self._slot_ready(b)
         dst = self.hview[b][self.fill]
-        if isinstance(row, (list, tuple)):
-            off = 0
-            for layer in row:
-                flat = np.asarray(layer).reshape(-1)
-                if flat.dtype != np.float32:
-                    raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {flat.dtype}")
-                dst[off:off + flat.size] = flat
-                off += flat.size
-            if off != self.P:
-                raise InvalidParameterShapeError(f"row has {off} parameters, expected {self.P}")
-        else:
-            flat = np.asarray(row).reshape(-1)
-            if flat.size != self.P or flat.dtype != np.float32:
-                raise InvalidParameterShapeError(f"row must be float32[{self.P}]")
-            dst[: self.P] = flat
+        pieces = row if isinstance(row, (list, tuple)) else [row]
+        flats, total = [], 0
+        for layer in pieces:
+            flat = np.asarray(layer).reshape(-1)
+            if flat.dtype != np.float32:
+                raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {flat.dtype}")
+            flats.append(flat)
+            total += flat.size
+        if total != self.P:
+            raise InvalidParameterShapeError(f"row has {total} parameters, expected {self.P}")
+        self.pending.append(self._copy_pool().submit(_pack_row, dst, flats))
         self.weights.append(weight)
         self.chunk_a[b].append(weight)
         self.chunk_s[b].append(score)
@@ -100,6 +110,9 @@ class StreamingFold:
 
     def _flush(self, finalize: bool = False, total=None):
         b, n = self.buf, self.fill
+        for f in self.pending:  # every row of this chunk is packed before its H2D
+            f.result()
+        self.pending = []
         if n:
             with torch.cuda.stream(self.copy_stream):
                 self.devbuf[b][:n].copy_(self.host[b][:n], non_blocking=True)
@@ -135,6 +148,13 @@ class StreamingFold:
             _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
         self._flush(finalize=True, total=total)
         return self.acc
+
+
+def _pack_row(dst: np.ndarray, flats) -> None:
+    off = 0
+    for flat in flats:
+        dst[off:off + flat.size] = flat
+        off += flat.size
 
 
 def stream_layers(rows_iter, shapes: Sequence[tuple], weights_iter=None, chunk_rows: int = 16,

@@ -52,11 +52,41 @@ def _npy_payload(buf: memoryview, off: int):
     return dt, tuple(hdr["shape"]), hstart + hlen
 
 
+class _ViewFile(io.RawIOBase):
+    """Minimal read-only seekable file over a memoryview (zipfile reads only
+    the central directory through it)."""
+
+    def __init__(self, mv: memoryview):
+        self.mv, self.pos = mv.cast("B"), 0
+
+    def readable(self):
+        return True
+
+    def seekable(self):
+        return True
+
+    def tell(self):
+        return self.pos
+
+    def seek(self, off, whence=0):
+        self.pos = off if whence == 0 else (self.pos + off if whence == 1 else len(self.mv) + off)
+        return self.pos
+
+    def readinto(self, b):
+        n = max(0, min(len(b), len(self.mv) - self.pos))
+        b[:n] = self.mv[self.pos:self.pos + n]
+        self.pos += n
+        return n
+
+
 def npz_views(blob) -> Optional[List[np.ndarray]]:
     """Layer views into an uncompressed NPZ blob, or None if it needs np.load."""
     buf = memoryview(blob)
+    # BytesIO shares a bytes object's buffer (no copy); anything else is
+    # wrapped read-only without copying the payload via a file-like view.
+    src = io.BytesIO(blob) if isinstance(blob, bytes) else _ViewFile(buf)
     try:
-        with zipfile.ZipFile(io.BytesIO(buf)) as zf:
+        with zipfile.ZipFile(src) as zf:
             infos = zf.infolist()
     except zipfile.BadZipFile:
         return None

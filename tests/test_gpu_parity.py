@@ -30,6 +30,11 @@ def _bits_equal(a, b):
     return G.same_bits(np.asarray(a), np.asarray(b))
 
 
+def _sentinel(P, dev, dtype=None):
+    """Output buffer pre-filled with NaN so an element the kernel never writes fails the test."""
+    return torch.full((P,), float("nan"), dtype=dtype or torch.float32, device=dev)
+
+
 # ---------------------------------------------------------------------------
 # golden vectors through the drop-in strategy classes
 # ---------------------------------------------------------------------------
@@ -136,7 +141,7 @@ def test_fold_f32_shapes(dev, N, P, scored):
     a = np.array(w, np.float32)
     s = None if sc is None else np.array(sc, np.float32)
     exp = OL.fedavg_f32(X, a, np.float32(sum(w)), s=s)
-    got = engine.fold_stacked(torch.from_numpy(X).to(dev), w, sc).cpu().numpy()
+    got = engine.fold_stacked(torch.from_numpy(X).to(dev), w, sc, out=_sentinel(P, dev)).cpu().numpy()
     assert _bits_equal(got, exp)
 
 
@@ -151,7 +156,7 @@ def test_fold_f32_pitch_and_misalignment(dev, offset, pad):
     big = torch.zeros((N, P + pad + offset), dtype=torch.float32, device=dev)
     big[:, offset:offset + P] = torch.from_numpy(X).to(dev)
     view = big[:, offset:offset + P]
-    got = engine.fold_stacked(view, w).cpu().numpy()
+    got = engine.fold_stacked(view, w, out=_sentinel(P, dev)).cpu().numpy()
     exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
     assert _bits_equal(got, exp)
 
@@ -167,7 +172,7 @@ def test_all_variants_bit_identical(dev, lib):
     outs = []
     for v in range(L.fa_num_variants()):
         for sp in (None, s):
-            o = torch.empty(P, dtype=torch.float32, device=dev)
+            o = _sentinel(P, dev)
             lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
                                               None if sp is None else sp.data_ptr(),
                                               float(np.float32(sum(w))), o.data_ptr(), st, v), "variant")
@@ -190,7 +195,7 @@ def test_chunked_fold_equals_batch(dev, lib):
     a = torch.tensor(w, dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     div = float(np.float32(sum(w)))
-    acc = torch.empty(P, dtype=torch.float32, device=dev)
+    acc = _sentinel(P, dev)
     bounds = [0, 1, 7, 20, 21, 49, 50]
     for k, (r0, r1) in enumerate(zip(bounds[:-1], bounds[1:])):
         last = r1 == N
@@ -228,7 +233,7 @@ def test_bf16_matches_definition(dev, N, P, scored):
     exp, expb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)),
                                s=None if sc is None else np.array(sc, np.float32))
     Xd = torch.from_numpy(Xb.view(np.int16)).to(dev).view(torch.bfloat16)
-    out, outb = engine.fold_stacked(Xd, w, sc, want_bf16=True)
+    out, outb = engine.fold_stacked(Xd, w, sc, want_bf16=True, out=_sentinel(P, dev))
     assert _bits_equal(out.cpu().numpy(), exp)
     assert np.array_equal(outb.view(torch.int16).cpu().numpy().view(np.uint16), expb)
 
@@ -243,8 +248,8 @@ def test_bf16_variants_bit_identical(dev, lib):
     a = torch.tensor(w, dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     for v in range(L.fa_num_bf16_variants()):
-        o = torch.empty(P, dtype=torch.float32, device=dev)
-        ob = torch.empty(P, dtype=torch.int16, device=dev)
+        o = _sentinel(P, dev)
+        ob = torch.full((P,), -1, dtype=torch.int16, device=dev)
         lib.check(L.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
                                            o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
         assert _bits_equal(o.cpu().numpy(), exp), v
@@ -354,3 +359,78 @@ def test_config5_full_size_stall_512x25M(dev, lib):
 def test_config4_shard_size_bf16_256x12_5M(dev, lib):
     # one of 8 parameter buckets of config 4 (256 x 100M bf16 over 8 GPUs)
     _full_size_check(dev, lib, 256, 12_500_000, 4, "bf16", scored=False)
+
+
+@pytest.mark.parametrize("chunk_rows", [1, 3, 7, 64])
+@pytest.mark.parametrize("scored", [False, True])
+def test_streaming_fold_equals_batch(dev, chunk_rows, scored):
+    from fedlesscan_amd.ingest import StreamingFold
+    N, P = 29, 3001
+    X = synth.clients_f32(91, N, 0, P)
+    w = synth.cardinalities(91, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(91, N, 10, 2)] if scored else None
+    sf = StreamingFold(P, chunk_rows=chunk_rows, device=dev)
+    sf.acc.fill_(float("nan"))
+    for i in range(N):
+        # rows arrive as layer lists, like decoded NPZ members
+        sf.add([X[i, :1000].reshape(10, 100), X[i, 1000:]], w[i], None if sc is None else sc[i])
+    got = sf.finish().cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    assert _bits_equal(got, exp)
+
+
+def test_sharded_aggregator_single_rank(dev):
+    from fedlesscan_amd.sharding import ShardedAggregator
+    N, P = 11, 5000
+    X = synth.clients_f32(93, N, 0, P)
+    w = synth.cardinalities(93, N)
+    out = ShardedAggregator().aggregate(torch.from_numpy(X).to(dev), w)
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    assert _bits_equal(out.cpu().numpy(), exp)
+
+
+TAIL_P = [1, 2, 3, 5, 1023, 1025, 1026, 1027, 2049, 4097, 8195, 4 * 1024 * 3 + 1, 4 * 2048 + 2, 40003]
+
+
+@pytest.mark.parametrize("P", TAIL_P)
+def test_every_variant_writes_every_column(dev, lib, P):
+    """Column tails (P % 4 != 0) and partial last blocks for every fp32 variant,
+    folded from scratch and as a continued chunked fold."""
+    L = lib.load()
+    N = 6
+    X = torch.from_numpy(synth.clients_f32(300 + P, N, 0, P)).to(dev)
+    w = synth.cardinalities(300 + P, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
+    for v in range(L.fa_num_variants()):
+        o = _sentinel(P, dev)
+        lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(), None, div, o.data_ptr(), st, v),
+                  "variant")
+        assert _bits_equal(o.cpu().numpy(), exp), (v, P)
+    acc = _sentinel(P, dev)
+    lib.check(L.fa_fold_f32(X.data_ptr(), 2, P, P, a.data_ptr(), None, None, div, 0, acc.data_ptr(), st), "f")
+    lib.check(L.fa_fold_f32(X[2].data_ptr(), N - 2, P, P, a[2:].data_ptr(), None, acc.data_ptr(), div, 1,
+                            acc.data_ptr(), st), "f")
+    assert _bits_equal(acc.cpu().numpy(), exp), P
+
+
+@pytest.mark.parametrize("P", [1, 7, 9, 15, 2049, 2055, 8 * 256 * 2 + 3, 8 * 256 * 4 + 7, 65541])
+def test_every_bf16_variant_writes_every_column(dev, lib, P):
+    L = lib.load()
+    N = 5
+    Xb = synth.clients_bf16(400 + P, N, 0, P)
+    w = synth.cardinalities(400 + P, N)
+    exp, expb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)))
+    Xd = torch.from_numpy(Xb.view(np.int16)).to(dev)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for v in range(L.fa_num_bf16_variants()):
+        o = _sentinel(P, dev)
+        ob = torch.full((P,), -1, dtype=torch.int16, device=dev)
+        lib.check(L.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
+                                           o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
+        assert _bits_equal(o.cpu().numpy(), exp), (v, P)
+        assert np.array_equal(ob.cpu().numpy().view(np.uint16), expb), (v, P)
