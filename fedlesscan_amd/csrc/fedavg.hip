@@ -479,7 +479,7 @@ constexpr F32Variant kVariants[] = {
     {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-constexpr const char* kBf16Variants[] = {"bf16u4c2", "bf16u8c1", "bf16u4c4", "bf16u2c4", "bf16u8c2"};
+constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2"};
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
@@ -621,11 +621,11 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X,              \
                                N, P, ldx, a, s, divisor, out_f32, out_bf16);                               \
     }
-        switch (variant) {  // must match kBf16Variants[]
-            case 0: FA_BF(4, 2); break;
+        switch (variant) {  // must match kBf16Variants[]; 0 = default (on-device sweep)
+            case 0: FA_BF(2, 4); break;
             case 1: FA_BF(8, 1); break;
             case 2: FA_BF(4, 4); break;
-            case 3: FA_BF(2, 4); break;
+            case 3: FA_BF(4, 2); break;
             default: FA_BF(8, 2); break;
         }
 #undef FA_BF
