@@ -36,7 +36,7 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import ShardedAggregator, bucket_bounds  # noqa: E402
+from fedlesscan_amd.sharding import SlotLayout  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=0,
+                    help="exchange rounds per step (fold of round k+1 overlaps the all-gather of round k); "
+                         "default 1 on one GPU, 4 on several")
     return ap.parse_args()
 
 
@@ -92,41 +95,56 @@ def setup_dist(args):
 
 
 class Workload:
-    def __init__(self, cfg, rank, world, dev):
+    """This rank's share of the synthetic round: its parameter slots, all clients.
+
+    The global model is cut by SlotLayout into rounds*world slots; rank r owns
+    slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
+    With rounds=1 that is one contiguous bucket per rank."""
+
+    def __init__(self, cfg, rank, world, dev, rounds):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
-        lo, hi = bucket_bounds(self.P_total, world)[rank]  # this rank's parameter bucket
-        self.P = hi - lo
-        self.rank, self.dev = rank, dev
+        self.layout = SlotLayout(self.P_total, world, rounds)
+        self.slots = self.layout.slots(rank)
+        self.P = sum(hi - lo for lo, hi in self.slots)  # real columns this rank folds
+        self.rank, self.world, self.dev = rank, world, dev
         L = _lib.load()
         st = torch.cuda.current_stream(dev).cuda_stream
         tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
-        self.X = torch.empty((self.N, self.P), dtype=tdt, device=dev)
+        sub, W = self.layout.sub, self.layout.local_width
+        self.X = torch.zeros((self.N, W), dtype=tdt, device=dev)
         gen = L.fa_synth_f32 if self.dtype == "f32" else L.fa_synth_bf16
-        _lib.check(gen(self.X.data_ptr(), self.N, self.P, self.P, self.seed, 0, lo, st), "synth")
-        self.col0 = lo
+        esz = self.X.element_size()
+        for k, (lo, hi) in enumerate(self.slots):
+            if hi > lo:
+                _lib.check(gen(self.X.data_ptr() + k * sub * esz, self.N, hi - lo, W, self.seed, 0, lo, st),
+                           "synth")
+        self.col0 = self.slots[0][0]
         self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
         self.scores = ([(r + 1) / 11 for r in synth.round_ids(self.seed, self.N, 10, 2)]
                        if self.scored else None)
         f = Factors(self.weights, self.scores, np.dtype(np.float32))
         self.a, self.s = f.to(dev)
         self.div = float(f.div)
-        self.out = torch.empty(self.P, dtype=torch.float32, device=dev)
+        self.out = torch.empty(W, dtype=torch.float32, device=dev)  # this rank's slots, side by side
         elt = 4 if self.dtype == "f32" else 2
-        # algorithmic bytes per launch: every input element once + the fp32 output once
+        # algorithmic bytes per step on this rank: every real input element once + the fp32 output once
         self.bytes = self.N * self.P * elt + self.P * 4
         torch.cuda.synchronize()
 
-    def launch(self, variant=0):
+    def launch(self, variant=0, k=0):
+        """Fold round k's slot (all of X when rounds == 1)."""
         L = _lib.load()
         st = torch.cuda.current_stream(self.dev).cuda_stream
         s = None if self.s is None else self.s.data_ptr()
+        sub, W = self.layout.sub, self.layout.local_width
+        x = self.X.data_ptr() + k * sub * self.X.element_size()
+        o = self.out.data_ptr() + k * sub * 4
         if self.dtype == "f32":
-            rc = L.fa_fedavg_f32_variant(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s,
-                                         self.div, self.out.data_ptr(), st, variant)
+            rc = L.fa_fedavg_f32_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st, variant)
         else:
-            rc = L.fa_fedavg_bf16_variant(self.X.data_ptr(), self.N, self.P, self.P, self.a.data_ptr(), s,
-                                          self.div, self.out.data_ptr(), None, st, variant)
+            rc = L.fa_fedavg_bf16_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, None, st,
+                                          variant)
         if rc:
             _lib.check(rc, "fold")
 
@@ -195,12 +213,12 @@ def main():
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
     cfg = CONFIGS[args.config]
-    wl = Workload(cfg, rank, world, dev)
+    rounds = args.rounds or (1 if world == 1 else 4)
+    wl = Workload(cfg, rank, world, dev, rounds)
     L = _lib.load()
-    sharded = ShardedAggregator() if world > 1 else None
-    from fedlesscan_amd.sharding import chunk_size
-    gathered = (torch.empty(chunk_size(wl.P_total, world) * world, dtype=torch.float32, device=dev)
-                if world > 1 else None)
+    lay = wl.layout
+    full = torch.empty(lay.padded_total, dtype=torch.float32, device=dev) if world > 1 else None
+    gloo = world > 1 and dist.get_backend() == "gloo"
     stream = torch.cuda.current_stream(dev)
 
     if args.sweep and rank == 0:
@@ -214,7 +232,8 @@ def main():
             for v in range(nvar):  # interleaved rounds in one process
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                wl.launch(v)
+                for k in range(rounds):
+                    wl.launch(v, k)
                 e1.record(stream)
                 e1.synchronize()
                 res[v].append(e0.elapsed_time(e1))
@@ -223,19 +242,32 @@ def main():
             log(f"variant {v} {vname(v).decode():10s} median {ts[len(ts)//2]:.3f} ms  "
                 f"min {ts[0]:.3f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
 
+    sub = lay.sub
+
     def step(events=None):
-        if events is not None:
-            events[0].record(stream)
-        wl.launch(args.variant)
-        if events is not None:
-            events[1].record(stream)
-        if world > 1:  # reassemble the global model: RCCL all-gather over xGMI
-            sharded.gather(wl.out, wl.P_total, out=gathered)
+        works = []
+        for k in range(rounds):
+            if events is not None:
+                events[k][0].record(stream)
+            wl.launch(args.variant, k)
+            if events is not None:
+                events[k][1].record(stream)
+            if world > 1:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
+                lo, hi = lay.round_range(k)
+                piece = wl.out[k * sub:(k + 1) * sub]
+                if gloo:  # rehearsal only: host-staged
+                    host = torch.empty(hi - lo, dtype=torch.float32)
+                    dist.all_gather_into_tensor(host, piece.cpu())
+                    full[lo:hi].copy_(host)
+                else:
+                    works.append(dist.all_gather_into_tensor(full[lo:hi], piece, async_op=True))
+        for w in works:
+            w.wait()
 
     for _ in range(args.warmup):
         step()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(rounds)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -251,13 +283,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gather_ok = None
-    if world > 1:  # my bucket inside the reassembled model must be my fold output, bit for bit
-        lo = wl.col0
-        ok = torch.equal(gathered[lo:lo + wl.P].view(torch.int32), wl.out.view(torch.int32))
+    if world > 1:  # my slots inside the reassembled model must be my fold output, bit for bit
+        ok = True
+        for k, (lo, hi) in enumerate(wl.slots):
+            if hi > lo:
+                ok &= torch.equal(full[lo:hi].view(torch.int32),
+                                  wl.out[k * sub:k * sub + hi - lo].view(torch.int32))
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
-    kern_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in ev) for ev in evs]
     kern_avg = float(np.mean(kern_ms))
     if world > 1:
         t = torch.tensor([kern_avg], dtype=torch.float64, device=dev)
@@ -314,7 +349,9 @@ def main():
                 "params_per_gpu": wl.P,
                 "params_total": wl.P_total,
                 "layout": "row-stacked [clients][params] fp32 in HBM",
-                "parallelism": f"param-bucket x{world}" + (" + RCCL all_gather" if world > 1 else ""),
+                "parallelism": f"param-bucket x{world}" + (
+                    f" + RCCL all_gather in {rounds} rounds overlapped with the fold" if world > 1 else ""),
+                "rounds": rounds,
                 "variant": (L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name)(
                     args.variant).decode(),
             },

@@ -38,6 +38,39 @@ def chunk_size(P: int, world: int, align: int = ALIGN) -> int:
     return b[0][1] - b[0][0]
 
 
+class SlotLayout:
+    """Round-robin parameter slots for an exchange that overlaps the fold.
+
+    The global vector is cut into rounds*world equal `sub`-element slots
+    (64-element aligned, the last ones partly or wholly past P).  Slot
+    j = k*world + r belongs to rank r, so round k's slots of all ranks form the
+    CONTIGUOUS global range [k*world*sub, (k+1)*world*sub): one
+    all_gather_into_tensor per round writes it in place, while the fold of
+    round k+1 runs.  A rank stores its slots side by side, local width
+    rounds*sub.  rounds=1 is exactly bucket_bounds().
+    """
+
+    def __init__(self, P: int, world: int, rounds: int = 1, align: int = ALIGN):
+        if world < 1 or rounds < 1:
+            raise ValueError("world and rounds must be >= 1")
+        self.P, self.world, self.rounds = P, world, rounds
+        units = -(-P // align)
+        self.sub = align * -(-units // (world * rounds)) if P else 0
+        self.local_width = rounds * self.sub
+        self.padded_total = rounds * world * self.sub
+
+    def slot(self, rank: int, k: int) -> Tuple[int, int]:
+        """Global [lo, hi) of rank's k-th slot (clipped to P; may be empty)."""
+        j = k * self.world + rank
+        return min(self.P, j * self.sub), min(self.P, (j + 1) * self.sub)
+
+    def slots(self, rank: int) -> List[Tuple[int, int]]:
+        return [self.slot(rank, k) for k in range(self.rounds)]
+
+    def round_range(self, k: int) -> Tuple[int, int]:
+        return k * self.world * self.sub, (k + 1) * self.world * self.sub
+
+
 class ShardedAggregator:
     """Fold this rank's parameter bucket, then all-gather the global model.
 
@@ -102,6 +135,39 @@ class ShardedAggregator:
         else:
             local = torch.empty(0, dtype=torch.float32, device=X_local.device)
         return self.gather(local, P)
+
+    def aggregate_slots(self, X_local: torch.Tensor, weights: Sequence, scores: Optional[Sequence],
+                        layout: "SlotLayout", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Fold round by round and all-gather each round asynchronously, so the
+        exchange of round k overlaps the fold of round k+1.
+
+        X_local: [N, layout.local_width], this rank's slots side by side (columns
+        past P may hold anything; their outputs are trimmed).  Returns [P].
+        `fold` must accept out= (engine.fold_stacked does)."""
+        if X_local.shape[1] != layout.local_width:
+            raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
+        sub = layout.sub
+        full = out if out is not None else torch.empty(layout.padded_total, dtype=torch.float32,
+                                                       device=X_local.device)
+        local = torch.empty(layout.local_width, dtype=torch.float32, device=X_local.device)
+        works = []
+        gloo = self.world > 1 and dist.get_backend(self.group) == "gloo"
+        for k in range(layout.rounds):
+            piece = local[k * sub:(k + 1) * sub]
+            if sub:
+                self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece)
+            lo, hi = layout.round_range(k)
+            if self.world == 1:
+                full[lo:hi].copy_(piece)
+            elif gloo and piece.is_cuda:
+                host = torch.empty(hi - lo, dtype=piece.dtype)
+                dist.all_gather_into_tensor(host, piece.cpu(), group=self.group)
+                full[lo:hi].copy_(host)
+            else:
+                works.append(dist.all_gather_into_tensor(full[lo:hi], piece, group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        return full[: layout.P]
 
     def aggregate_layers(self, parameters: Sequence[Sequence], weights: Sequence,
                          scores: Optional[Sequence] = None, device=None) -> List:

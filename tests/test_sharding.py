@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from fedlesscan_amd import synth
-from fedlesscan_amd.sharding import ShardedAggregator, bucket_bounds, chunk_size
+from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, bucket_bounds, chunk_size
 
 
 def test_bucket_bounds_cover_and_align():
@@ -29,6 +29,31 @@ def test_bucket_bounds_cover_and_align():
             assert all(lo % 64 == 0 for lo, hi in b if hi > lo)
 
 
+def test_slot_layout_partitions_the_vector():
+    for P in (1, 64, 1000, 10007, 10_000_000):
+        for world in (1, 2, 3, 8):
+            for rounds in (1, 2, 4):
+                lay = SlotLayout(P, world, rounds)
+                cover = []
+                for r in range(world):
+                    for k, (lo, hi) in enumerate(lay.slots(r)):
+                        if hi == lo:
+                            continue  # slot entirely past P
+                        assert lo % 64 == 0
+                        rlo, rhi = lay.round_range(k)
+                        assert rlo <= lo <= hi <= rhi
+                        cover.append((lo, hi))
+                cover.sort()
+                pos = 0
+                for lo, hi in cover:
+                    if hi > lo:
+                        assert lo == pos
+                        pos = hi
+                assert pos == P
+                if rounds == 1:
+                    assert [lay.slot(r, 0) for r in range(world)] == bucket_bounds(P, world)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -37,9 +62,13 @@ def _free_port():
     return p
 
 
-def _oracle_fold(X, w, s=None, **_):
+def _oracle_fold(X, w, s=None, out=None, **_):
     from oracle import fedavg_oracle as O
-    return torch.from_numpy(O.fedavg_stacked(X.numpy(), w, s))
+    res = torch.from_numpy(O.fedavg_stacked(np.ascontiguousarray(X.numpy()), w, s))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
 
 
 def _worker(rank, world, port, N, P, seed, scored, q):
@@ -78,4 +107,41 @@ def test_sharded_fold_gloo_matches_oracle(world, P, scored):
     for r in range(world):
         out = np.frombuffer(got[r], dtype=np.float32)
         assert out.shape == exp.shape
+        assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
+
+
+def _slot_worker(rank, world, port, N, P, rounds, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        agg = ShardedAggregator(fold=_oracle_fold)
+        lay = SlotLayout(P, world, rounds)
+        X = torch.zeros((N, lay.local_width))
+        for k, (lo, hi) in enumerate(lay.slots(rank)):
+            if hi > lo:
+                X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(synth.clients_f32(seed, N, lo, hi - lo))
+        w = synth.cardinalities(seed, N)
+        full = agg.aggregate_slots(X, w, None, lay)
+        q.put((rank, full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P,rounds", [(2, 10007, 3), (3, 5000, 2), (2, 64, 4)])
+def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds):
+    from oracle import fedavg_oracle as O
+    N, seed = 7, 23
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, N, P, rounds, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = O.fedavg_stacked(synth.clients_f32(seed, N, 0, P), synth.cardinalities(seed, N))
+    for r in range(world):
+        out = np.frombuffer(got[r], dtype=np.float32)
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
