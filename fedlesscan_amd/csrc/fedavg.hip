@@ -170,6 +170,45 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     }
 }
 
+// Balanced persistent form: the grid is the resident capacity (occupancy x
+// CUs) and block b owns the contiguous quad range [b*per, (b+1)*per), per =
+// ceil(nq / grid): every CU streams the same number of bytes, so there is no
+// partly-filled last wave of blocks.  Inside its range a block walks tiles of
+// C*kBlock quads; the same fold_quads body does the work.
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_balanced(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t per) {  // acc_in may alias out
+    const int64_t nq = P >> 2;
+    const int64_t ldq = ldx >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < nq ? lo + per : nq;
+    int64_t q0 = lo + threadIdx.x;
+    for (; q0 + (int64_t)(C - 1) * kBlock < hi; q0 += (int64_t)C * kBlock)
+        fold_quads<U, C, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+    for (; q0 < hi; q0 += kBlock)
+        fold_quads<U, 1, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+    if ((P & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) {
+        for (int64_t col = nq * 4; col < P; ++col) {
+            float acc;
+            int64_t i = 0;
+            if constexpr (ACC) {
+                acc = acc_in[col];
+            } else {
+                acc = term1<SCORED>(X[col], a[0], SCORED ? s[0] : 1.0f);
+                i = 1;
+            }
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
+            if constexpr (FIN) acc = acc / divisor;
+            out[col] = acc;
+        }
+    }
+}
+
 // One column per lane, any alignment / stride (fallback for unaligned input).
 template <bool SCORED, bool ACC, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
@@ -474,13 +513,60 @@ struct F32Variant {
 };
 // variant 0 is the shipped default (chosen from the on-device sweep)
 constexpr F32Variant kVariants[] = {
+    {"auto", 4, 0, true},  // U=4, C from the launch size (pick_quads)
     {"u4c4nt", 4, 4, true}, {"u8c1nt", 8, 1, true}, {"u16c1", 16, 1, false}, {"u4c1nt", 4, 1, true},
     {"u8c2nt", 8, 2, true}, {"u16c1nt", 16, 1, true}, {"u16c2nt", 16, 2, true}, {"u2c8nt", 2, 8, true},
     {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
+    // balanced persistent grid (resident capacity, equal contiguous share per block)
+    {"bal_u4c4nt", 4, 4, true}, {"bal_u4c2nt", 4, 2, true}, {"bal_u4c1nt", 4, 1, true},
+    {"bal_u8c1nt", 8, 1, true}, {"bal_u2c4nt", 2, 4, true}, {"bal_u8c2nt", 8, 2, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// Quads per lane for the "auto" variant: the widest per-block row run
+// (C * 4 KiB) that still leaves >= ~1000 blocks in the launch, i.e. about one
+// full wave of resident blocks (measured on MI355X, DESIGN.md 5: 10M columns
+// -> C=4, 2.5M -> C=2, 1M -> C=1; C=8 and persistent grids were slower).
+inline int pick_quads(int64_t P) {
+    const int64_t nq = P >> 2;
+    if (nq / (4 * kBlock) >= 1000) return 4;
+    if (nq / (2 * kBlock) >= 1000) return 2;
+    return 1;
+}
 constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2"};
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
+
+// Resident blocks of `kern` on the current device (occupancy API x CU count),
+// cached per (device, kernel).  The guide notes the API can over-report by one
+// block per CU for SGPR-heavy 256-thread kernels; for a plain (non-cooperative)
+// launch that only costs balance, never correctness.
+template <typename K>
+int resident_blocks(K kern) {
+    static thread_local int cache_dev[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    static thread_local int cache_val[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cache_dev[dev] == dev) return cache_val[dev];
+    int cus = 256, per_cu = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, 0) != hipSuccess || per_cu < 1)
+        per_cu = 4;
+    cache_dev[dev] = dev;
+    cache_val[dev] = cus * per_cu;
+    return cache_val[dev];
+}
+
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
+void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                     const float* s, const float* acc_in, float d, float* out) {
+    auto kern = k_fold_f32_balanced<U, C, NT, SC, ACC, FIN>;
+    const int64_t nq = P >> 2;
+    int64_t grid = resident_blocks(kern);
+    const int64_t tiles = (nq + kBlock - 1) / kBlock;  // never more blocks than 256-quad tiles
+    if (grid > tiles) grid = tiles > 0 ? tiles : 1;
+    const int64_t per = grid > 0 ? (nq + grid - 1) / grid : 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
+}
 
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
@@ -491,10 +577,14 @@ void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx
                        st, X, N, P, ldx, a, s, acc_in, d, out);
 }
 
-template <int U, int C, bool NT>
+template <int U, int C, bool NT, bool BAL = false>
 void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
-#define FA_V4(SC, ACC, FIN) launch_v4<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out)
+#define FA_V4(SC, ACC, FIN)                                                                   \
+    do {                                                                                      \
+        if constexpr (BAL) launch_balanced<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out); \
+        else launch_v4<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out);       \
+    } while (0)
     if (sc) {
         if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
         else     { if (fin) FA_V4(true, false, true); else FA_V4(true, false, false); }
@@ -540,19 +630,34 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         return check_launch("k_fold_f32_scalar");
     }
 #define FA_VF(U, C, NT) launch_v4_flags<U, C, NT>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VB(U, C) launch_v4_flags<U, C, true, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     switch (variant) {  // must match kVariants[]
-        case 0: FA_VF(4, 4, true); break;
-        case 1: FA_VF(8, 1, true); break;
-        case 2: FA_VF(16, 1, false); break;
-        case 3: FA_VF(4, 1, true); break;
-        case 4: FA_VF(8, 2, true); break;
-        case 5: FA_VF(16, 1, true); break;
-        case 6: FA_VF(16, 2, true); break;
-        case 7: FA_VF(2, 8, true); break;
-        case 8: FA_VF(4, 2, true); break;
-        default: FA_VF(2, 4, true); break;
+        case 0:
+            switch (pick_quads(P)) {
+                case 4: FA_VF(4, 4, true); break;
+                case 2: FA_VF(4, 2, true); break;
+                default: FA_VF(4, 1, true); break;
+            }
+            break;
+        case 1: FA_VF(4, 4, true); break;
+        case 2: FA_VF(8, 1, true); break;
+        case 3: FA_VF(16, 1, false); break;
+        case 4: FA_VF(4, 1, true); break;
+        case 5: FA_VF(8, 2, true); break;
+        case 6: FA_VF(16, 1, true); break;
+        case 7: FA_VF(16, 2, true); break;
+        case 8: FA_VF(2, 8, true); break;
+        case 9: FA_VF(4, 2, true); break;
+        case 10: FA_VF(2, 4, true); break;
+        case 11: FA_VB(4, 4); break;
+        case 12: FA_VB(4, 2); break;
+        case 13: FA_VB(4, 1); break;
+        case 14: FA_VB(8, 1); break;
+        case 15: FA_VB(2, 4); break;
+        default: FA_VB(8, 2); break;
     }
 #undef FA_VF
+#undef FA_VB
     return check_launch("k_fold_f32_v4");
 }
 

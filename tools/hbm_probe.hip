@@ -1,0 +1,162 @@
+// hbm_probe — measure achievable HBM read bandwidth on MI355X for several
+// access patterns, to calibrate the fold's roofline (not part of the product).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/build/hbm_probe tools/hbm_probe.hip
+//   tools/build/hbm_probe [GiB]
+//
+// Patterns (all read every byte of the buffer exactly once per launch):
+//   sweep   grid-stride over the whole buffer, 8 x 16 B loads in flight per lane
+//   chunk   each block streams its own contiguous chunk, 8 x 16 B per lane per step
+//   fold2d  the fold's shape: rows x cols fp32, a block reads C*4 KiB of every row
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e = (x);                                                                    \
+        if (e != hipSuccess) {                                                                 \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));           \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+template <bool NT>
+__device__ __forceinline__ f32x4 ld(const f32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT, int K>
+__global__ __launch_bounds__(256) void sweep(const f32x4* __restrict__ X, int64_t nq, float* sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; q + (K - 1) * stride < nq; q += K * stride) {
+        f32x4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = ld<NT>(X + q + k * stride);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc += v[k];
+    }
+    for (; q < nq; q += stride) acc += ld<NT>(X + q);
+    if (acc.x + acc.y + acc.z + acc.w == 123.456f) sink[0] = acc.x;  // keep loads live
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void chunk(const f32x4* __restrict__ X, int64_t nq, int64_t per, float* sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = lo + per < nq ? lo + per : nq;
+    int64_t q = lo + threadIdx.x;
+    for (; q + 7 * 256 < hi; q += 8 * 256) {
+        f32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = ld<NT>(X + q + k * 256);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; q < hi; q += 256) acc += ld<NT>(X + q);
+    if (acc.x + acc.y + acc.z + acc.w == 123.456f) sink[0] = acc.x;
+}
+
+template <int U, int C>
+__global__ __launch_bounds__(256) void fold2d(const f32x4* __restrict__ X, int64_t rows, int64_t ldq, float* sink) {
+    const int64_t q0 = (int64_t)blockIdx.x * (256 * C) + threadIdx.x;
+    f32x4 acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = f32x4{0, 0, 0, 0};
+    for (int64_t i = 0; i + U <= rows; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(X + (i + u) * ldq + q0 + c * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += v[u][c];
+    }
+    float t = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t += acc[c].x + acc[c].y + acc[c].z + acc[c].w;
+    if (t == 123.456f) sink[0] = t;
+}
+
+__global__ void fill(f32x4* X, int64_t nq) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256)
+        X[q] = f32x4{1.f, 2.f, 3.f, (float)(q & 1023)};
+}
+
+template <typename F>
+double time_ms(F launch, int reps = 7) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    launch();
+    launch();
+    CK(hipDeviceSynchronize());
+    float best[16];
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a));
+        launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&best[r], a, b));
+    }
+    // median
+    for (int i = 0; i < reps; ++i)
+        for (int j = i + 1; j < reps; ++j)
+            if (best[j] < best[i]) { float t = best[i]; best[i] = best[j]; best[j] = t; }
+    return best[reps / 2];
+}
+
+int main(int argc, char** argv) {
+    const double gib = argc > 1 ? atof(argv[1]) : 38.0;
+    const int64_t rows = 1024;
+    const int64_t cols = (int64_t)(gib * (1ll << 30) / 4 / rows) / 4096 * 4096;
+    const int64_t nq = rows * cols / 4;
+    const double bytes = (double)nq * 16;
+    f32x4* X;
+    float* sink;
+    CK(hipMalloc(&X, (size_t)bytes));
+    CK(hipMalloc(&sink, 64));
+    hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, X, nq);
+    CK(hipDeviceSynchronize());
+    printf("buffer %.2f GB (%lld rows x %lld cols fp32)\n", bytes / 1e9, (long long)rows, (long long)cols);
+    auto report = [&](const char* name, double ms) {
+        printf("%-28s %8.3f ms  %8.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    for (int g : {1024, 2048, 4096, 8192, 16384, 65535}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "sweep nt k8 grid %d", g);
+        report(nm, time_ms([&] { hipLaunchKernelGGL((sweep<true, 8>), dim3(g), dim3(256), 0, 0, X, nq, sink); }));
+    }
+    report("sweep plain k8 grid 8192",
+           time_ms([&] { hipLaunchKernelGGL((sweep<false, 8>), dim3(8192), dim3(256), 0, 0, X, nq, sink); }));
+    report("sweep nt k16 grid 4096",
+           time_ms([&] { hipLaunchKernelGGL((sweep<true, 16>), dim3(4096), dim3(256), 0, 0, X, nq, sink); }));
+    report("sweep nt k4 grid 16384",
+           time_ms([&] { hipLaunchKernelGGL((sweep<true, 4>), dim3(16384), dim3(256), 0, 0, X, nq, sink); }));
+    for (int64_t kb : {16, 64, 256, 1024, 4096}) {
+        int64_t per = kb * 1024 / 16;
+        int64_t grid = (nq + per - 1) / per;
+        char nm[64];
+        snprintf(nm, sizeof nm, "chunk nt %lld KiB/block", (long long)kb);
+        report(nm, time_ms([&] { hipLaunchKernelGGL((chunk<true>), dim3(grid), dim3(256), 0, 0, X, nq, per, sink); }));
+    }
+    const int64_t ldq = cols / 4;
+    report("fold2d u4c4", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<4, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("fold2d u4c2", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<4, 2>), dim3(ldq / 512), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("fold2d u4c1", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<4, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("fold2d u8c4", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<8, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    CK(hipFree(X));
+    return 0;
+}
