@@ -85,6 +85,32 @@ __global__ __launch_bounds__(256) void fold2d(const f32x4* __restrict__ X, int64
     if (t == 123.456f) sink[0] = t;
 }
 
+// tiled layout [P/T][rows][T]: block b owns tile b; rows of a tile are adjacent,
+// so a block streams rows*T*4 contiguous bytes.  T = 256*C*4 floats.
+template <int U, int C>
+__global__ __launch_bounds__(256) void fold_tiled(const f32x4* __restrict__ X, int64_t rows, float* sink) {
+    constexpr int TQ = 256 * C;  // quads per tile row
+    const f32x4* base = X + (int64_t)blockIdx.x * rows * TQ + threadIdx.x;
+    f32x4 acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = f32x4{0, 0, 0, 0};
+    for (int64_t i = 0; i + U <= rows; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(base + (i + u) * TQ + c * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += v[u][c];
+    }
+    float t = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t += acc[c].x + acc[c].y + acc[c].z + acc[c].w;
+    if (t == 123.456f) sink[0] = t;
+}
+
 __global__ void fill(f32x4* X, int64_t nq) {
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256)
         X[q] = f32x4{1.f, 2.f, 3.f, (float)(q & 1023)};
@@ -157,6 +183,22 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((fold2d<4, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, sink); }));
     report("fold2d u8c4", time_ms([&] {
         hipLaunchKernelGGL((fold2d<8, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("fold2d u8c2", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<8, 2>), dim3(ldq / 512), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("fold2d u16c1", time_ms([&] {
+        hipLaunchKernelGGL((fold2d<16, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, sink); }));
+    report("tiled u4c1 (T=4KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<4, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, sink); }));
+    report("tiled u8c1 (T=4KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<8, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, sink); }));
+    report("tiled u4c2 (T=8KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<4, 2>), dim3(ldq / 512), dim3(256), 0, 0, X, rows, sink); }));
+    report("tiled u4c4 (T=16KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<4, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, sink); }));
+    report("tiled u2c4 (T=16KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<2, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, sink); }));
+    report("tiled u8c4 (T=16KiB)", time_ms([&] {
+        hipLaunchKernelGGL((fold_tiled<8, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, sink); }));
     CK(hipFree(X));
     return 0;
 }
