@@ -434,3 +434,14 @@ def test_every_bf16_variant_writes_every_column(dev, lib, P):
                                            o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
         assert _bits_equal(o.cpu().numpy(), exp), (v, P)
         assert np.array_equal(ob.cpu().numpy().view(np.uint16), expb), (v, P)
+
+
+@pytest.mark.parametrize("strategy_name", ["fedlesscan", "fedavg"])
+def test_config1_mock_aggregator_on_gpu(dev, strategy_name):
+    """BASELINE config 1 end to end (store -> MockAggregator -> HIP fold -> NPZ
+    -> parameter store), bit-exact against the reference-generated golden."""
+    from test_host import config1_round
+    res, shapes, sha, exp = config1_round(strategy_name)
+    assert res.new_round_id == 11 and res.num_clients == 10
+    assert [list(s) for s in shapes] == exp["shapes"]
+    assert sha == exp["flat_sha256"]

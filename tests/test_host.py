@@ -295,3 +295,49 @@ def test_npz_views_match_np_load():
         assert all(np.array_equal(a, b) for a, b in zip(got, ref))
     assert npz_views(b"junk") is None
     assert npz_views(_savez([])) == []
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 1: mnist-demo (aggregator tolerance 2), 10 clients, mock
+# aggregator.  Plumbing checked against the reference-generated golden with the
+# oracle supplying the fold (the GPU version of this test is in test_gpu_parity).
+# ---------------------------------------------------------------------------
+def config1_round(strategy_name):
+    """Store the 10 mnist-demo client results, run one MockAggregator round,
+    return (result, output shapes, sha256 of the flat output, golden entry)."""
+    import hashlib
+    from fedlesscan_amd.config import aggregator_settings
+    from fedlesscan_amd.handler import MockAggregator
+    m = G.manifest()["mnist_c1"]
+    strategy, hp = aggregator_settings({"aggregator": {"hyperparams": {"tolerance": 2}}}, strategy_name)
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    params = G.parameters("mnist_c1")
+    rounds = m["round_ids"] if strategy == AggregationStrategy.PER_SESSION else [m["current_round"]] * 10
+    for i, (p, r) in enumerate(zip(params, rounds)):
+        blob = NpzWeightsSerializer().serialize(p)
+        st.save("mnist", r, f"client-{i}", ClientResult(parameters=SerializedParameters(
+            blob=blob, serializer=WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())),
+            cardinality=m["weights"][i]))
+    res = MockAggregator(AggregatorFunctionParams(session_id="mnist", round_id=m["current_round"],
+                                                  aggregation_strategy=strategy, aggregation_hyper_params=hp),
+                         st, ps).run_aggregator()
+    out = NpzWeightsSerializer().deserialize(ps.load("mnist", m["current_round"] + 1).blob)
+    flat = np.concatenate([o.ravel() for o in out])
+    key = "stall" if strategy == AggregationStrategy.PER_SESSION else "fedavg"
+    return res, [o.shape for o in out], hashlib.sha256(flat.tobytes()).hexdigest(), m["outputs"][key]
+
+
+@pytest.mark.parametrize("strategy_name", ["fedlesscan", "fedavg"])
+def test_config1_mock_aggregator_plumbing(oracle_fold, strategy_name):
+    res, shapes, sha, exp = config1_round(strategy_name)
+    assert res.new_round_id == 11 and res.num_clients == 10
+    assert [list(s) for s in shapes] == exp["shapes"]
+    assert sha == exp["flat_sha256"]
+
+
+def test_strategy_name_mapping():
+    from fedlesscan_amd.config import strategy_for
+    assert strategy_for("fedlesscan") == AggregationStrategy.PER_SESSION
+    assert strategy_for("fedavg") == AggregationStrategy.PER_ROUND
+    assert strategy_for("fedprox") == AggregationStrategy.PER_ROUND
+    assert strategy_for("unknown") == AggregationStrategy.PER_SESSION
