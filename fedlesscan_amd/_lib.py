@@ -50,6 +50,8 @@ _PROTOS = {
     "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
     "fa_num_bf16_variants": (_int, []),
     "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
+    "fa_npz_index": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int]),
+    "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,201 @@
+// Host-side ingest helpers of libfedavg_hip.so (no GPU involved).
+//
+// Client updates reach the aggregator as uncompressed NPZ blobs
+// (NpzWeightsSerializer, fedless/common/serialization.py:280-306; clients use
+// compressed=False by default, client.py:186-199).  fa_npz_index locates every
+// .npy member's raw payload inside the blob (zip / zip64 central directory ->
+// local header -> .npy header), so the engine can copy payloads straight into
+// pinned staging; fa_pack does that copy with several threads.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fedavg_hip.h"
+
+namespace {
+
+inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t rd32(const uint8_t* p) { return (uint32_t)rd16(p) | ((uint32_t)rd16(p + 2) << 16); }
+inline uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+
+constexpr uint32_t kEOCD = 0x06054b50, kZ64Loc = 0x07064b50, kZ64EOCD = 0x06064b50;
+constexpr uint32_t kCDir = 0x02014b50, kLocal = 0x04034b50;
+
+// dtype code from a numpy descr string ("<f4", "|u1", ...); 0 = not supported
+int dtype_code(const std::string& d, int* itemsize) {
+    if (d.size() < 3) return 0;
+    const char order = d[0];
+    if (order == '>') return 0;  // big-endian payloads are not copied raw
+    const std::string k = d.substr(1);
+    struct E { const char* s; int code; int sz; };
+    static const E table[] = {{"f4", FA_DT_F32, 4}, {"f8", FA_DT_F64, 8}, {"i4", FA_DT_I32, 4},
+                              {"i8", FA_DT_I64, 8}, {"f2", FA_DT_F16, 2}, {"u1", FA_DT_U8, 1},
+                              {"i1", FA_DT_I8, 1},  {"b1", FA_DT_BOOL, 1}};
+    for (const E& e : table)
+        if (k == e.s) {
+            *itemsize = e.sz;
+            return e.code;
+        }
+    return 0;
+}
+
+// Parse the python-dict header of a .npy file: {'descr': '<f4', 'fortran_order': False, 'shape': (3, 4), }
+bool parse_npy_header(const char* h, size_t n, std::string* descr, bool* fortran, std::vector<int64_t>* shape) {
+    std::string s(h, n);
+    auto key = [&](const char* k) -> size_t {
+        size_t p = s.find(std::string("'") + k + "'");
+        return p == std::string::npos ? p : s.find(':', p);
+    };
+    size_t p = key("descr");
+    if (p == std::string::npos) return false;
+    size_t q0 = s.find('\'', p), q1 = q0 == std::string::npos ? q0 : s.find('\'', q0 + 1);
+    if (q1 == std::string::npos) return false;
+    *descr = s.substr(q0 + 1, q1 - q0 - 1);
+    p = key("fortran_order");
+    if (p == std::string::npos) return false;
+    size_t v = s.find_first_not_of(" ", p + 1);
+    if (v == std::string::npos) return false;
+    *fortran = s.compare(v, 4, "True") == 0;
+    p = key("shape");
+    if (p == std::string::npos) return false;
+    size_t a = s.find('(', p), b = a == std::string::npos ? a : s.find(')', a);
+    if (b == std::string::npos) return false;
+    shape->clear();
+    const std::string dims = s.substr(a + 1, b - a - 1);
+    size_t i = 0;
+    while (i < dims.size()) {
+        while (i < dims.size() && (dims[i] == ' ' || dims[i] == ',')) ++i;
+        if (i >= dims.size()) break;
+        if (dims[i] < '0' || dims[i] > '9') return false;
+        int64_t x = 0;
+        while (i < dims.size() && dims[i] >= '0' && dims[i] <= '9') x = x * 10 + (dims[i++] - '0');
+        shape->push_back(x);
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+static int npz_index_impl(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* counts, int32_t* dtypes,
+                          int32_t* ndims, int64_t* shapes, int max_layers) {
+    if (!blob || len < 22) return -1;
+    // End of central directory: scan back over at most a 64 KiB comment
+    int64_t eocd = -1;
+    for (int64_t p = len - 22; p >= 0 && p >= len - 22 - 65535; --p)
+        if (rd32(blob + p) == kEOCD) {
+            eocd = p;
+            break;
+        }
+    if (eocd < 0) return -1;
+    uint64_t n_entries = rd16(blob + eocd + 10);
+    uint64_t cd_off = rd32(blob + eocd + 16);
+    if (eocd >= 20 && rd32(blob + eocd - 20) == kZ64Loc) {  // zip64
+        uint64_t z = rd64(blob + eocd - 20 + 8);
+        if (z + 56 > (uint64_t)len || rd32(blob + z) != kZ64EOCD) return -1;
+        n_entries = rd64(blob + z + 32);
+        cd_off = rd64(blob + z + 48);
+    }
+    if (n_entries > (uint64_t)max_layers) return -1;
+    uint64_t p = cd_off;
+    for (uint64_t e = 0; e < n_entries; ++e) {
+        if (p + 46 > (uint64_t)len || rd32(blob + p) != kCDir) return -1;
+        const uint16_t method = rd16(blob + p + 10);
+        uint64_t csize = rd32(blob + p + 20), usize = rd32(blob + p + 24);
+        const uint16_t nlen = rd16(blob + p + 28), xlen = rd16(blob + p + 30), clen = rd16(blob + p + 32);
+        uint64_t lho = rd32(blob + p + 42);
+        if (method != 0) return -1;  // compressed member: needs np.load
+        // zip64 extra field (0x0001): fields present only where the 32-bit value is saturated
+        uint64_t x = p + 46 + nlen, xend = x + xlen;
+        while (x + 4 <= xend && xend <= (uint64_t)len) {
+            const uint16_t id = rd16(blob + x), sz = rd16(blob + x + 2);
+            if (id == 1) {
+                uint64_t f = x + 4;
+                if (usize == 0xFFFFFFFFu) { usize = rd64(blob + f); f += 8; }
+                if (csize == 0xFFFFFFFFu) { csize = rd64(blob + f); f += 8; }
+                if (lho == 0xFFFFFFFFu) { lho = rd64(blob + f); f += 8; }
+            }
+            x += 4 + sz;
+        }
+        if (lho + 30 > (uint64_t)len || rd32(blob + lho) != kLocal) return -1;
+        const uint64_t data = lho + 30 + rd16(blob + lho + 26) + rd16(blob + lho + 28);
+        if (data + 10 > (uint64_t)len || memcmp(blob + data, "\x93NUMPY", 6) != 0) return -1;
+        const uint8_t major = blob[data + 6];
+        uint64_t hlen, hstart;
+        if (major == 1) { hlen = rd16(blob + data + 8); hstart = data + 10; }
+        else if ((major == 2 || major == 3) && data + 12 <= (uint64_t)len) { hlen = rd32(blob + data + 8); hstart = data + 12; }
+        else return -1;
+        if (hstart + hlen > (uint64_t)len) return -1;
+        std::string descr;
+        bool fortran = false;
+        std::vector<int64_t> shape;
+        if (!parse_npy_header((const char*)blob + hstart, hlen, &descr, &fortran, &shape)) return -1;
+        int itemsize = 0;
+        const int code = dtype_code(descr, &itemsize);
+        if (!code || fortran || shape.size() > 8) return -1;
+        int64_t count = 1;
+        for (int64_t d : shape) count *= d;
+        const uint64_t payload = hstart + hlen;
+        if (payload + (uint64_t)count * itemsize > data + csize || payload + (uint64_t)count * itemsize > (uint64_t)len)
+            return -1;
+        offsets[e] = (int64_t)payload;
+        counts[e] = count;
+        dtypes[e] = code;
+        ndims[e] = (int32_t)shape.size();
+        for (size_t k = 0; k < 8; ++k) shapes[e * 8 + k] = k < shape.size() ? shape[k] : 0;
+        p += 46 + nlen + xlen + clen;
+    }
+    return (int)n_entries;
+}
+
+int fa_npz_index(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* counts, int32_t* dtypes,
+                 int32_t* ndims, int64_t* shapes, int max_layers) {
+    try {  // nothing may unwind across the C ABI
+        return npz_index_impl(blob, len, offsets, counts, dtypes, ndims, shapes, max_layers);
+    } catch (...) {
+        return -1;
+    }
+}
+
+int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, const int64_t* sizes, int64_t n,
+            int nthreads) {
+    if (n < 0 || (n > 0 && (!dst || !dst_offsets || !srcs || !sizes))) return FA_ERR_ARG;
+    // prefix sums of the source sizes: the work is split by bytes, not ranges
+    std::vector<int64_t> off(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        if (sizes[i] < 0 || dst_offsets[i] < 0) return FA_ERR_ARG;
+        off[i + 1] = off[i] + sizes[i];
+    }
+    const int64_t total = off[n];
+    if (total == 0) return FA_OK;
+    int T = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, total >> 22));  // >= 4 MiB per thread
+    auto work = [&](int t) {
+        const int64_t b0 = total * t / T, b1 = total * (t + 1) / T;
+        int64_t i = std::upper_bound(off.begin(), off.end(), b0) - off.begin() - 1;
+        for (int64_t b = b0; b < b1 && i < n; ++i) {
+            const int64_t s0 = std::max(b, off[i]), s1 = std::min(b1, off[i + 1]);
+            if (s1 > s0)
+                memcpy((uint8_t*)dst + dst_offsets[i] + (s0 - off[i]), (const uint8_t*)srcs[i] + (s0 - off[i]),
+                       (size_t)(s1 - s0));
+            b = s1;
+        }
+    };
+    if (T == 1) {
+        work(0);
+        return FA_OK;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    return FA_OK;
+}
+
+}  // extern "C"

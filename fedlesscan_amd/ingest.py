@@ -15,7 +15,6 @@ accumulator, independent of the number of clients.
 from __future__ import annotations
 
 import os
-from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -34,17 +33,6 @@ class StreamingFold:
     has a score or none does.
     """
 
-    _pool: Optional[ThreadPoolExecutor] = None
-
-    @classmethod
-    def _copy_pool(cls) -> ThreadPoolExecutor:
-        # numpy releases the GIL for plain memcpy-style assignment, so rows of a
-        # chunk are packed into pinned memory by several host threads at once
-        if cls._pool is None:
-            n = int(os.environ.get("FEDAVG_COPY_THREADS", "0")) or min(8, os.cpu_count() or 1)
-            cls._pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="fedavg-pack")
-        return cls._pool
-
     def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
                  pitch_align: int = 64):
         if P <= 0:
@@ -54,7 +42,6 @@ class StreamingFold:
         self.ldx = ((P + pitch_align - 1) // pitch_align) * pitch_align
         self.R = max(1, chunk_rows)
         self.host = [torch.empty((self.R, self.ldx), dtype=torch.float32, pin_memory=True) for _ in range(2)]
-        self.hview = [h.numpy() for h in self.host]
         self.devbuf = [torch.empty((self.R, self.ldx), dtype=torch.float32, device=self.dev) for _ in range(2)]
         self.acc = torch.empty(P, dtype=torch.float32, device=self.dev)
         self.copy_stream = torch.cuda.Stream(device=self.dev)
@@ -70,7 +57,9 @@ class StreamingFold:
         self.chunk_s: List = [[], []]
         self.started = False
         self.rows = 0
-        self.pending: List = []
+        # per chunk: source layers and their byte offsets inside the pinned chunk
+        self.srcs: List = [[], []]
+        self.threads = int(os.environ.get("FEDAVG_COPY_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
     # -- producer side ------------------------------------------------------
     def _slot_ready(self, b: int):
@@ -88,18 +77,17 @@ class StreamingFold:
         b = self.buf
         if self.fill == 0:
             self._slot_ready(b)
-        dst = self.hview[b][self.fill]
         pieces = row if isinstance(row, (list, tuple)) else [row]
-        flats, total = [], 0
+        base = self.fill * self.ldx * 4
+        total = 0
         for layer in pieces:
-            flat = np.asarray(layer).reshape(-1)
-            if flat.dtype != np.float32:
-                raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {flat.dtype}")
-            flats.append(flat)
-            total += flat.size
+            arr = np.ascontiguousarray(layer)
+            if arr.dtype != np.float32:
+                raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {arr.dtype}")
+            self.srcs[b].append((arr, base + 4 * total))
+            total += arr.size
         if total != self.P:
             raise InvalidParameterShapeError(f"row has {total} parameters, expected {self.P}")
-        self.pending.append(self._copy_pool().submit(_pack_row, dst, flats))
         self.weights.append(weight)
         self.chunk_a[b].append(weight)
         self.chunk_s[b].append(score)
@@ -108,11 +96,22 @@ class StreamingFold:
         if self.fill == self.R:
             self._flush()
 
+    def _pack(self, b: int):
+        """Copy the chunk's layers into pinned buffer b with fa_pack (C++ threads, GIL released)."""
+        entries = self.srcs[b]
+        if not entries:
+            return
+        n = len(entries)
+        offs = np.fromiter((o for _, o in entries), dtype=np.int64, count=n)
+        ptrs = np.fromiter((a.ctypes.data for a, _ in entries), dtype=np.uint64, count=n)
+        sizes = np.fromiter((a.nbytes for a, _ in entries), dtype=np.int64, count=n)
+        _lib.call("fa_pack", self.host[b].data_ptr(), offs.ctypes.data, ptrs.ctypes.data, sizes.ctypes.data, n,
+                  self.threads)
+        self.srcs[b] = []
+
     def _flush(self, finalize: bool = False, total=None):
         b, n = self.buf, self.fill
-        for f in self.pending:  # every row of this chunk is packed before its H2D
-            f.result()
-        self.pending = []
+        self._pack(b)  # every row of this chunk is in pinned memory before its H2D
         if n:
             with torch.cuda.stream(self.copy_stream):
                 self.devbuf[b][:n].copy_(self.host[b][:n], non_blocking=True)
@@ -148,13 +147,6 @@ class StreamingFold:
             _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
         self._flush(finalize=True, total=total)
         return self.acc
-
-
-def _pack_row(dst: np.ndarray, flats) -> None:
-    off = 0
-    for flat in flats:
-        dst[off:off + flat.size] = flat
-        off += flat.size
 
 
 def stream_layers(rows_iter, shapes: Sequence[tuple], weights_iter=None, chunk_rows: int = 16,

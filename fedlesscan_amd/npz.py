@@ -111,9 +111,41 @@ def npz_views(blob) -> Optional[List[np.ndarray]]:
     return out
 
 
+_CODE_TO_DTYPE = {1: np.float32, 2: np.float64, 3: np.int32, 4: np.int64, 5: np.float16, 6: np.uint8,
+                  7: np.int8, 8: np.bool_}
+MAX_LAYERS = 4096
+
+
+def native_views(blob) -> Optional[List[np.ndarray]]:
+    """Same as npz_views, with the member index built by fa_npz_index (C++)."""
+    import ctypes
+    from . import _lib
+    L = _lib.load()
+    buf = memoryview(blob).cast("B")
+    n = len(buf)
+    if n == 0:
+        return None
+    src = np.frombuffer(buf, dtype=np.uint8)
+    offs = np.empty(MAX_LAYERS, np.int64)
+    cnts = np.empty(MAX_LAYERS, np.int64)
+    dts = np.empty(MAX_LAYERS, np.int32)
+    nds = np.empty(MAX_LAYERS, np.int32)
+    shp = np.empty(MAX_LAYERS * 8, np.int64)
+    k = L.fa_npz_index(src.ctypes.data_as(ctypes.c_void_p), n, offs.ctypes.data, cnts.ctypes.data,
+                       dts.ctypes.data, nds.ctypes.data, shp.ctypes.data, MAX_LAYERS)
+    if k < 0:
+        return None
+    out = []
+    for i in range(k):
+        dt = np.dtype(_CODE_TO_DTYPE[int(dts[i])])
+        shape = tuple(int(x) for x in shp[i * 8: i * 8 + int(nds[i])])
+        out.append(np.frombuffer(buf, dtype=dt, count=int(cnts[i]), offset=int(offs[i])).reshape(shape))
+    return out
+
+
 def read_layers(blob) -> List[np.ndarray]:
-    """Layers of an NPZ blob: zero-copy views when possible, np.load otherwise."""
-    v = npz_views(blob)
+    """Layers of an NPZ blob: zero-copy views (native index) when possible, np.load otherwise."""
+    v = native_views(blob)
     if v is not None:
         return v
     with io.BytesIO(bytes(blob)) as f:

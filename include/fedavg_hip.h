@@ -119,6 +119,25 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
 int fa_num_bf16_variants(void);
 const char* fa_bf16_variant_name(int variant);
 
+/* ---- host-side ingest (no GPU): NPZ wire format -> pinned staging ----------
+ * Client blobs are uncompressed NPZ archives (NpzWeightsSerializer,
+ * serialization.py:280-306, written by the client, client.py:186-199). */
+enum fa_dtype { FA_DT_F32 = 1, FA_DT_F64 = 2, FA_DT_I32 = 3, FA_DT_I64 = 4, FA_DT_F16 = 5,
+                FA_DT_U8 = 6, FA_DT_I8 = 7, FA_DT_BOOL = 8 };
+/* [host] Index the .npy members of an NPZ blob in archive order (= the order
+ * of list(np.load(f).values()), serialization.py:304-306): payload byte offset,
+ * element count, fa_dtype, ndim and shape (8 slots per layer).  Returns the
+ * number of layers, or -1 when the blob must go through np.load instead
+ * (compressed member, Fortran order, big-endian/object dtype, malformed, or
+ * more than max_layers members).  All arrays are [host] with max_layers slots. */
+int fa_npz_index(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* counts, int32_t* dtypes,
+                 int32_t* ndims, int64_t* shapes, int max_layers);
+/* [host] Copy n byte ranges: srcs[i] (sizes[i] bytes) -> dst + dst_offsets[i],
+ * split by bytes over up to nthreads threads (0 = hardware concurrency).  The
+ * pinned-staging packer of the ingest pipeline (fedlesscan_amd/ingest.py). */
+int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, const int64_t* sizes, int64_t n,
+            int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

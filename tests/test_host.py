@@ -341,3 +341,62 @@ def test_strategy_name_mapping():
     assert strategy_for("fedavg") == AggregationStrategy.PER_ROUND
     assert strategy_for("fedprox") == AggregationStrategy.PER_ROUND
     assert strategy_for("unknown") == AggregationStrategy.PER_SESSION
+
+
+def test_native_npz_index_matches_python_and_np_load():
+    from fedlesscan_amd.npz import native_views, npz_views
+    rng = np.random.default_rng(5)
+    cases = [
+        [np.arange(12, dtype=np.float32).reshape(3, 4), np.zeros((0, 5), np.float32)],
+        [np.float32(3.5) * np.ones(()), np.arange(7, dtype=np.int64), np.ones((2, 2, 2), np.float64)],
+        [rng.standard_normal((5, 5, 1, 32)).astype(np.float32), rng.standard_normal(32).astype(np.float32),
+         rng.integers(0, 9, (4, 3)).astype(np.int32), np.array([True, False]), np.arange(5, dtype=np.int8),
+         np.arange(6, dtype=np.uint8), np.ones(3, np.float16)],
+        [],
+    ]
+    for layers in cases:
+        blob = _savez(layers)
+        nv, pv = native_views(blob), npz_views(blob)
+        assert nv is not None and pv is not None and len(nv) == len(pv) == len(layers)
+        for a, b, c in zip(nv, pv, layers):
+            assert a.dtype == b.dtype == np.asarray(c).dtype and a.shape == b.shape == np.asarray(c).shape
+            assert np.array_equal(a, c) and not a.flags.owndata
+    assert native_views(_savez([np.ones(3, np.float32)], compressed=True)) is None
+    assert native_views(_savez([np.asfortranarray(np.ones((3, 4), np.float32))])) is None
+    assert native_views(_savez([np.ones(3, dtype=">f4")])) is None
+    assert native_views(b"not a zip") is None
+
+
+def test_native_npz_index_survives_corruption():
+    from fedlesscan_amd.npz import native_views
+    blob = bytearray(_savez([np.arange(100, dtype=np.float32), np.ones((3, 3), np.float64)]))
+    rng = np.random.default_rng(9)
+    for cut in range(0, len(blob), 37):  # truncations
+        native_views(bytes(blob[:cut]))
+    for _ in range(300):  # single-byte mutations: never crash, never read out of bounds
+        b = bytearray(blob)
+        b[rng.integers(0, len(b))] = rng.integers(0, 256)
+        v = native_views(bytes(b))
+        if v is not None:
+            assert sum(x.nbytes for x in v) <= len(b)
+
+
+def test_fa_pack_scatters_ranges():
+    L = _lib.load()
+    rng = np.random.default_rng(3)
+    srcs = [rng.integers(0, 255, rng.integers(0, 5_000_000), dtype=np.uint8) for _ in range(9)]
+    offs, pos = [], 0
+    for s in srcs:
+        pos += int(rng.integers(0, 100))
+        offs.append(pos)
+        pos += s.size
+    dst = np.zeros(pos + 10, np.uint8)
+    ptrs = np.array([s.ctypes.data for s in srcs], np.uint64)
+    sizes = np.array([s.size for s in srcs], np.int64)
+    o = np.array(offs, np.int64)
+    for threads in (1, 3, 0):
+        dst[:] = 0
+        assert L.fa_pack(dst.ctypes.data, o.ctypes.data, ptrs.ctypes.data, sizes.ctypes.data, len(srcs), threads) == 0
+        for s, off in zip(srcs, offs):
+            assert np.array_equal(dst[off:off + s.size], s)
+    assert L.fa_pack(None, None, None, None, -1, 1) == _lib.FA_ERR_ARG
