@@ -45,14 +45,6 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
-def _np_dtype_of(x) -> np.dtype:
-    if isinstance(x, torch.Tensor):
-        if x.dtype == torch.bfloat16:
-            return np.dtype("V2")  # marker; handled separately
-        return np.dtype(_TORCH_TO_NP[x.dtype])
-    return np.asarray(x).dtype
-
-
 def result_dtype(in_dtype: np.dtype, weights: Sequence, scores: Optional[Sequence] = None,
                  total=None) -> np.dtype:
     """dtype numpy gives `reduce(add, [x * n_i (* s_i)]) / sum(n)` (NEP 50 weak Python scalars)."""
