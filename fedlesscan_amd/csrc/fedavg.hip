@@ -231,40 +231,39 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
     out[c] = acc;
 }
 
-// List-of-rows form: xi[i] = device pointer to client i's P floats.  The row
+// List-of-rows form: xi[i] = device pointer to client i's P floats.  A lane
+// owns 4 columns; U rows are loaded ahead of the ordered adds.  The row
 // alignment test is wave-uniform (every lane reads the same pointer).
-template <bool SCORED>
+__device__ __forceinline__ f32x4 load_row4(const float* row, int64_t c0, int w) {
+    if (w == 4 && aligned16(row)) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0));
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < w; ++k) x[k] = row[c0 + k];
+    return x;
+}
+
+template <int U, bool SCORED>
 __global__ __launch_bounds__(kBlock) void k_fedavg_f32_ptrs(
     const float* const* __restrict__ xi, int64_t N, int64_t P,
     const float* __restrict__ a, const float* __restrict__ s, float divisor,
     float* __restrict__ out) {
-    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t c0 = q * 4;
+    const int64_t c0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     if (c0 >= P) return;
     const int w = (P - c0) >= 4 ? 4 : (int)(P - c0);
-    float acc[4];
-    for (int64_t i = 0; i < N; ++i) {
-        const float* row = xi[i];
-        float x[4] = {0.f, 0.f, 0.f, 0.f};
-        if (w == 4 && aligned16(row)) {
-            f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
-            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-        } else {
-            for (int k = 0; k < w; ++k) x[k] = row[c0 + k];
-        }
-        const float ai = a[i];
-        const float si = SCORED ? s[i] : 1.0f;
+    f32x4 acc = term4<SCORED>(load_row4(xi[0], c0, w), a[0], SCORED ? s[0] : 1.0f);
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        f32x4 v[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float t = term1<SCORED>(x[k], ai, si);
-            acc[k] = (i == 0) ? t : acc[k] + t;
-        }
+        for (int u = 0; u < U; ++u) v[u] = load_row4(xi[i + u], c0, w);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
     }
-    if (w == 4 && aligned16(out)) {
-        reinterpret_cast<f32x4*>(out + c0)[0] =
-            f32x4{acc[0] / divisor, acc[1] / divisor, acc[2] / divisor, acc[3] / divisor};
+    for (; i < N; ++i) acc = add4(acc, term4<SCORED>(load_row4(xi[i], c0, w), a[i], SCORED ? s[i] : 1.0f));
+    acc = div4(acc, divisor);
+    if (w == 4 && aligned16(out + c0)) {
+        *reinterpret_cast<f32x4*>(out + c0) = acc;
     } else {
-        for (int k = 0; k < w; ++k) out[c0 + k] = acc[k] / divisor;
+        for (int k = 0; k < w; ++k) out[c0 + k] = acc[k];
     }
 }
 
@@ -401,6 +400,53 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_scalar(
 // ---------------------------------------------------------------------------
 // float64 and integer folds: one column per lane, coalesced 8-byte loads.
 // ---------------------------------------------------------------------------
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// float64: a lane owns 2 columns (one 16-byte load per row), U rows ahead;
+// the odd last column (P % 2) goes to the lane with q == P/2.
+template <int U, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f64_v2(
+    const double* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const double* __restrict__ a, const double* __restrict__ s, double divisor,
+    double* __restrict__ out) {
+    const int64_t nq = P >> 1, ldq = ldx >> 1;
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q < nq) {
+        const f64x2* p = reinterpret_cast<const f64x2*>(X) + q;
+        f64x2 acc = __builtin_nontemporal_load(p) * a[0];
+        if constexpr (SCORED) acc = acc * s[0];
+        int64_t i = 1;
+        for (; i + U <= N; i += U) {
+            f64x2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldq);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                f64x2 t = v[u] * a[i + u];
+                if constexpr (SCORED) t = t * s[i + u];
+                acc = acc + t;
+            }
+        }
+        for (; i < N; ++i) {
+            f64x2 t = __builtin_nontemporal_load(p + i * ldq) * a[i];
+            if constexpr (SCORED) t = t * s[i];
+            acc = acc + t;
+        }
+        reinterpret_cast<f64x2*>(out)[q] = acc / divisor;
+    } else if (q == nq && (P & 1)) {
+        const int64_t c = P - 1;
+        double acc = X[c] * a[0];
+        if constexpr (SCORED) acc = acc * s[0];
+        for (int64_t i = 1; i < N; ++i) {
+            double t = X[i * ldx + c] * a[i];
+            if constexpr (SCORED) t = t * s[i];
+            acc = acc + t;
+        }
+        out[c] = acc / divisor;
+    }
+}
+
+// float64, one column per lane, any alignment / stride.
 template <bool SCORED>
 __global__ __launch_bounds__(kBlock) void k_fedavg_f64(
     const double* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
@@ -697,10 +743,10 @@ int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
     if (s)
-        hipLaunchKernelGGL(k_fedavg_f32_ptrs<true>, grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P, a,
+        hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, true>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P, a,
                            s, divisor, out);
     else
-        hipLaunchKernelGGL(k_fedavg_f32_ptrs<false>, grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P,
+        hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, false>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P,
                            a, s, divisor, out);
     return check_launch("k_fedavg_f32_ptrs");
 }
@@ -761,6 +807,15 @@ int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const doub
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
+    if (aligned16(X) && aligned16(out) && (ldx % 2 == 0)) {
+        if (s)
+            hipLaunchKernelGGL((k_fedavg_f64_v2<8, true>), grid_for((P >> 1) + 1), dim3(kBlock), 0, st, X, N, P,
+                               ldx, a, s, divisor, out);
+        else
+            hipLaunchKernelGGL((k_fedavg_f64_v2<8, false>), grid_for((P >> 1) + 1), dim3(kBlock), 0, st, X, N, P,
+                               ldx, a, s, divisor, out);
+        return check_launch("k_fedavg_f64_v2");
+    }
     if (s)
         hipLaunchKernelGGL(k_fedavg_f64<true>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s, divisor,
                            out);

@@ -445,3 +445,18 @@ def test_config1_mock_aggregator_on_gpu(dev, strategy_name):
     assert res.new_round_id == 11 and res.num_clients == 10
     assert [list(s) for s in shapes] == exp["shapes"]
     assert sha == exp["flat_sha256"]
+
+
+@pytest.mark.parametrize("N,P,offset", [(1, 1, 0), (3, 7, 0), (40, 1001, 0), (17, 4097, 0), (9, 1000, 1)])
+@pytest.mark.parametrize("scored", [False, True])
+def test_f64_shapes_and_tails(dev, N, P, offset, scored):
+    from fedlesscan_amd import engine
+    X = synth.clients_f32(500 + P, N, 0, P).astype(np.float64) * (1.0 + 1.0 / 3.0)
+    w = synth.cardinalities(500 + N, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(5, N, 10, 2)] if scored else None
+    big = torch.zeros((N, P + offset), dtype=torch.float64, device=dev)
+    big[:, offset:] = torch.from_numpy(X).to(dev)
+    got = engine.fold_stacked(big[:, offset:], w, sc, out=_sentinel(P, dev, torch.float64)).cpu().numpy()
+    exp = OL.fedavg_f64(X, np.array(w, np.float64), float(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float64))
+    assert _bits_equal(got, exp)

@@ -400,3 +400,13 @@ def test_fa_pack_scatters_ranges():
         for s, off in zip(srcs, offs):
             assert np.array_equal(dst[off:off + s.size], s)
     assert L.fa_pack(None, None, None, None, -1, 1) == _lib.FA_ERR_ARG
+
+
+def test_aggregate_metrics_matches_oracle():
+    from fedlesscan_amd.metrics import aggregate_metrics
+    raw = [{"cardinality": 10, "metrics": {"loss": 1.0, "accuracy": 0.5}},
+           {"cardinality": 30, "metrics": {"loss": 3.0, "accuracy": 0.9}},
+           {"cardinality": 7, "metrics": {"loss": 0.25, "accuracy": 0.1}}]
+    got = aggregate_metrics([TestMetrics(**r) for r in raw], ["loss", "accuracy"])
+    exp = O.weighted_metrics(raw, ["loss", "accuracy"])
+    assert got == exp
