@@ -566,6 +566,7 @@ constexpr F32Variant kVariants[] = {
     // balanced persistent grid (resident capacity, equal contiguous share per block)
     {"bal_u4c4nt", 4, 4, true}, {"bal_u4c2nt", 4, 2, true}, {"bal_u4c1nt", 4, 1, true},
     {"bal_u8c1nt", 8, 1, true}, {"bal_u2c4nt", 2, 4, true}, {"bal_u8c2nt", 8, 2, true},
+    {"u8c4nt", 8, 4, true}, {"u2c2nt", 2, 2, true}, {"u1c4nt", 1, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -700,7 +701,10 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 13: FA_VB(4, 1); break;
         case 14: FA_VB(8, 1); break;
         case 15: FA_VB(2, 4); break;
-        default: FA_VB(8, 2); break;
+        case 16: FA_VB(8, 2); break;
+        case 17: FA_VF(8, 4, true); break;
+        case 18: FA_VF(2, 2, true); break;
+        default: FA_VF(1, 4, true); break;
     }
 #undef FA_VF
 #undef FA_VB

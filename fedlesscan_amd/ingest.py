@@ -149,8 +149,7 @@ class StreamingFold:
         return self.acc
 
 
-def stream_layers(rows_iter, shapes: Sequence[tuple], weights_iter=None, chunk_rows: int = 16,
-                  device=None):
+def stream_layers(rows_iter, shapes: Sequence[tuple], chunk_rows: int = 16, device=None):
     """Convenience: fold an iterator of (layers, weight[, score]) tuples."""
     P = sum(int(np.prod(s)) if len(s) else 1 for s in shapes)
     sf = StreamingFold(P, chunk_rows=chunk_rows, device=device)

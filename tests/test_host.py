@@ -410,3 +410,18 @@ def test_aggregate_metrics_matches_oracle():
     got = aggregate_metrics([TestMetrics(**r) for r in raw], ["loss", "accuracy"])
     exp = O.weighted_metrics(raw, ["loss", "accuracy"])
     assert got == exp
+
+
+def test_handler_wraps_serialization_errors(oracle_fold):
+    from fedlesscan_amd import AggregationError
+    from fedlesscan_amd.handler import default_aggregation_handler
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    bad = ClientResult(parameters=SerializedParameters(
+        blob=b"definitely not an npz", serializer=WeightsSerializerConfig(type="npz",
+                                                                          params=NpzWeightsSerializerConfig())),
+        cardinality=3)
+    st.save("s", 1, "c0", bad)
+    cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
+    with pytest.raises(AggregationError):  # aggregation.py:164-165
+        default_aggregation_handler("s", 1, st, ps, cfg)
+    assert st.count_results_for_round("s", 1) == 1  # nothing deleted on failure
