@@ -559,7 +559,7 @@ struct F32Variant {
 };
 // variant 0 is the shipped default (chosen from the on-device sweep)
 constexpr F32Variant kVariants[] = {
-    {"auto", 4, 0, true},  // U=4, C from the launch size (pick_quads)
+    {"auto", 0, 0, true},  // C from the launch size (pick_quads); U=8 at C=4, else U=4
     {"u4c4nt", 4, 4, true}, {"u8c1nt", 8, 1, true}, {"u16c1", 16, 1, false}, {"u4c1nt", 4, 1, true},
     {"u8c2nt", 8, 2, true}, {"u16c1nt", 16, 1, true}, {"u16c2nt", 16, 2, true}, {"u2c8nt", 2, 8, true},
     {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
@@ -681,7 +681,7 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     switch (variant) {  // must match kVariants[]
         case 0:
             switch (pick_quads(P)) {
-                case 4: FA_VF(4, 4, true); break;
+                case 4: FA_VF(8, 4, true); break;
                 case 2: FA_VF(4, 2, true); break;
                 default: FA_VF(4, 1, true); break;
             }
