@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=0, help="override the config's client count (experiments)")
+    ap.add_argument("--params", type=int, default=0, help="override the config's parameter count (experiments)")
     ap.add_argument("--rounds", type=int, default=0,
                     help="exchange rounds per step (fold of round k+1 overlaps the all-gather of round k); "
                          "default 1 on one GPU, 4 on several")
@@ -213,6 +215,9 @@ def main():
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
     cfg = CONFIGS[args.config]
+    if args.clients or args.params:
+        cfg = (args.clients or cfg[0], args.params or cfg[1], *cfg[2:7],
+               cfg[7] + f" [override: {args.clients or cfg[0]} clients x {args.params or cfg[1]} params]")
     rounds = args.rounds or (1 if world == 1 else 4)
     wl = Workload(cfg, rank, world, dev, rounds)
     L = _lib.load()
