@@ -141,7 +141,8 @@ double time_ms(F launch, int reps = 7) {
 
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? atof(argv[1]) : 38.0;
-    const int64_t rows = 1024;
+    const int64_t rows = argc > 2 ? atoll(argv[2]) : 1024;
+    const bool pitch_only = argc > 3 && argv[3][0] == 'p';
     const int64_t cols = (int64_t)(gib * (1ll << 30) / 4 / rows) / 4096 * 4096;
     const int64_t nq = rows * cols / 4;
     const double bytes = (double)nq * 16;
@@ -156,6 +157,29 @@ int main(int argc, char** argv) {
         printf("%-28s %8.3f ms  %8.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
+    if (pitch_only) {
+        // same fold-shaped read, row pitch padded by `pad` quads (buffer has slack)
+        const int64_t ldq0 = cols / 4;
+        const int64_t slack = 65536 + 64;         // quads per row kept free for padding
+        const int64_t ncol_q = (ldq0 - slack) / 1024 * 1024;  // quads actually read per row
+        for (int64_t pad : {0, 16, 64, 256, 1024, 4096, 16384, 65536}) {
+            const int64_t ldq = ncol_q + pad;
+            // host-side bounds check before any launch: the last row must end inside the buffer
+            if ((rows - 1) * ldq + ncol_q > nq) {
+                fprintf(stderr, "pad %lld would overrun the buffer; skipped\n", (long long)pad);
+                continue;
+            }
+            char nm[64];
+            snprintf(nm, sizeof nm, "fold2d u8c4 pitch+%lldB", (long long)(pad * 16));
+            const double rb = (double)rows * ncol_q * 16;
+            double ms = time_ms([&] {
+                hipLaunchKernelGGL((fold2d<8, 4>), dim3(ncol_q / 1024), dim3(256), 0, 0, X, rows, ldq, sink); });
+            printf("%-28s %8.3f ms  %8.1f GB/s\n", nm, ms, rb / (ms * 1e-3) / 1e9);
+            fflush(stdout);
+        }
+        CK(hipFree(X));
+        return 0;
+    }
     for (int g : {1024, 2048, 4096, 8192, 16384, 65535}) {
         char nm[64];
         snprintf(nm, sizeof nm, "sweep nt k8 grid %d", g);
