@@ -37,6 +37,8 @@ _PROTOS = {
     "fa_fedavg_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_ptrs": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fold_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _f32, _int, _vp, _vp]),
+    "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),
+    "fa_finalize_f32": (_int, [_vp, _f32, _vp, _i64, _vp]),
     "fa_fedavg_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),

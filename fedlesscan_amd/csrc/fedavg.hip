@@ -482,6 +482,24 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_int(
     out[c] = (double)(T)acc / divisor;
 }
 
+// One client row into a running fold with scalar factors (fa_accumulate_f32):
+// acc = (first ? t : acc + t), t = fl(fl(x*a)*s).  s == 1 multiplies exactly.
+__global__ __launch_bounds__(kBlock) void k_accumulate_f32(float* acc, const float* __restrict__ x, float a,
+                                                            float s, int first, int64_t P) {
+    const int64_t c0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (c0 >= P) return;
+    if (c0 + 4 <= P && aligned16(acc + c0) && aligned16(x + c0)) {
+        f32x4 t = term4<true>(__builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + c0)), a, s);
+        f32x4* p = reinterpret_cast<f32x4*>(acc + c0);
+        *p = first ? t : add4(*p, t);
+    } else {
+        for (int64_t c = c0; c < P && c < c0 + 4; ++c) {
+            const float t = term1<true>(x[c], a, s);
+            acc[c] = first ? t : acc[c] + t;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // synthetic generator (bit-identical to fedlesscan_amd/synth.py)
 // ---------------------------------------------------------------------------
@@ -738,6 +756,18 @@ int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, con
 int fa_fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
                 const float* acc_in, float divisor, int finalize, float* out, void* stream) {
     return fold_f32(X, N, P, ldx, a, s, acc_in, divisor, finalize, out, stream, 0);
+}
+
+int fa_accumulate_f32(float* acc, const float* x, float a, float s, int first, int64_t P, void* stream) {
+    if (P < 0 || (P > 0 && (!acc || !x))) return fail(FA_ERR_ARG, "null acc/x or negative P");
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipLaunchKernelGGL(k_accumulate_f32, grid_for((P + 3) / 4), dim3(kBlock), 0, (hipStream_t)stream, acc, x, a, s,
+                       first, P);
+    return check_launch("k_accumulate_f32");
+}
+
+int fa_finalize_f32(const float* acc, float divisor, float* out, int64_t P, void* stream) {
+    return fold_f32(nullptr, 0, P, P, nullptr, nullptr, acc, divisor, 1, out, stream, 0);
 }
 
 int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,

@@ -75,6 +75,16 @@ int fa_fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx,
                 const float* a, const float* s, const float* acc_in,
                 float divisor, int finalize, float* out, void* stream);
 
+/* Single-row forms with scalar factors, for ingest that folds
+ * each client as it arrives:
+ *   fa_accumulate_f32: acc = first ? t : acc + t,  t = fl(fl(x*a) * s)
+ *                      (s = 1.0f for FedAvg: multiplying by 1 is exact)
+ *   fa_finalize_f32:   out = acc / divisor   (acc may alias out)
+ * Accumulating the rows in client order and finalising once is bit-identical
+ * to fa_fedavg_f32 over the stacked rows. */
+int fa_accumulate_f32(float* acc, const float* x, float a, float s, int first, int64_t P, void* stream);
+int fa_finalize_f32(const float* acc, float divisor, float* out, int64_t P, void* stream);
+
 /* bf16 updates (BASELINE config 4; no reference path: defined as exact upcast
  * to f32 + the f32 fold).  out_f32 [P] required; out_bf16 [P] optional (RNE). */
 int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,

@@ -454,3 +454,24 @@ def test_f64_shapes_and_tails(dev, N, P, offset, scored):
     exp = OL.fedavg_f64(X, np.array(w, np.float64), float(sum(w)),
                         s=None if sc is None else np.array(sc, np.float64))
     assert _bits_equal(got, exp)
+
+
+@pytest.mark.parametrize("P", [1, 5, 4096, 10001])
+@pytest.mark.parametrize("scored", [False, True])
+def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
+    L = lib.load()
+    N = 13
+    X = synth.clients_f32(600 + P, N, 0, P)
+    w = synth.cardinalities(600 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(600, N, 10, 2)] if scored else [1.0] * N
+    Xd = torch.from_numpy(X).to(dev)
+    acc = _sentinel(P, dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for i in range(N):
+        lib.check(L.fa_accumulate_f32(acc.data_ptr(), Xd[i].data_ptr(), float(np.float32(w[i])),
+                                      float(np.float32(sc[i])), int(i == 0), P, st), "acc")
+    out = _sentinel(P, dev)
+    lib.check(L.fa_finalize_f32(acc.data_ptr(), float(np.float32(sum(w))), out.data_ptr(), P, st), "fin")
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=np.array(sc, np.float32) if scored else None)
+    assert _bits_equal(out.cpu().numpy(), exp)
