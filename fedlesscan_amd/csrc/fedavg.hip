@@ -601,24 +601,24 @@ inline int pick_quads(int64_t P) {
 constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2"};
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
-// Resident blocks of `kern` on the current device (occupancy API x CU count),
-// cached per (device, kernel).  The guide notes the API can over-report by one
-// block per CU for SGPR-heavy 256-thread kernels; for a plain (non-cooperative)
-// launch that only costs balance, never correctness.
-template <typename K>
-int resident_blocks(K kern) {
-    static thread_local int cache_dev[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-    static thread_local int cache_val[16];
+// Resident blocks of one balanced-kernel instantiation on the current device
+// (occupancy API x CU count), cached per (instantiation, device).  The guide
+// notes the API can over-report by one block per CU for SGPR-heavy 256-thread
+// kernels; for a plain (non-cooperative) launch that only costs balance.
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
+int resident_blocks() {
+    static thread_local int cache[16] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-    if (cache_dev[dev] == dev) return cache_val[dev];
+    if (cache[dev] > 0) return cache[dev];
     int cus = 256, per_cu = 4;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fold_f32_balanced<U, C, NT, SC, ACC, FIN>, kBlock,
+                                                     0) != hipSuccess ||
+        per_cu < 1)
         per_cu = 4;
-    cache_dev[dev] = dev;
-    cache_val[dev] = cus * per_cu;
-    return cache_val[dev];
+    cache[dev] = cus * per_cu;
+    return cache[dev];
 }
 
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
@@ -626,7 +626,7 @@ void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64
                      const float* s, const float* acc_in, float d, float* out) {
     auto kern = k_fold_f32_balanced<U, C, NT, SC, ACC, FIN>;
     const int64_t nq = P >> 2;
-    int64_t grid = resident_blocks(kern);
+    int64_t grid = resident_blocks<U, C, NT, SC, ACC, FIN>();
     const int64_t tiles = (nq + kBlock - 1) / kBlock;  // never more blocks than 256-quad tiles
     if (grid > tiles) grid = tiles > 0 ? tiles : 1;
     const int64_t per = grid > 0 ? (nq + grid - 1) / grid : 0;
