@@ -128,14 +128,23 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
     for (int c = 0; c < C; ++c) out[c * kBlock] = FIN ? div4(acc[c], divisor) : acc[c];
 }
 
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
+// Bijective blockIdx remap that gives each of the 8 XCDs (blocks b and b+8
+// share one under round-robin dispatch) a contiguous range of column tiles.
+// Placement is a speed hint only; any placement gives the same result.
+__device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t n) {
+    const int64_t q = n / 8, r = n % 8, x = b % 8, k = b / 8;
+    return x * q + (x < r ? x : r) + k;
+}
+
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
     const float* acc_in, float divisor, float* out) {  // acc_in may alias out
     const int64_t nq = P >> 2;
     const int64_t ldq = ldx >> 2;
-    const int64_t q0 = (int64_t)blockIdx.x * (kBlock * C) + threadIdx.x;
+    const int64_t bid = XR ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t q0 = bid * (kBlock * C) + threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
     const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
     f32x4* O4 = reinterpret_cast<f32x4*>(out);
@@ -153,7 +162,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     // column tail: at most 3 columns, folded by the lane that would own quad
     // index nq under the C-quads-per-lane mapping (scalar loads, same order)
     const int64_t tb = nq / (kBlock * C), tl = (nq % (kBlock * C)) % kBlock;
-    if ((P & 3) && (int64_t)blockIdx.x == tb && (int64_t)threadIdx.x == tl) {
+    if ((P & 3) && bid == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = nq * 4; col < P; ++col) {
             float acc;
             int64_t i = 0;
@@ -585,6 +594,8 @@ constexpr F32Variant kVariants[] = {
     {"bal_u4c4nt", 4, 4, true}, {"bal_u4c2nt", 4, 2, true}, {"bal_u4c1nt", 4, 1, true},
     {"bal_u8c1nt", 8, 1, true}, {"bal_u2c4nt", 2, 4, true}, {"bal_u8c2nt", 8, 2, true},
     {"u8c4nt", 8, 4, true}, {"u2c2nt", 2, 2, true}, {"u1c4nt", 1, 4, true},
+    // XCD-contiguous block order (each XCD streams its own contiguous column range)
+    {"xcd_u8c4nt", 8, 4, true}, {"xcd_u4c1nt", 4, 1, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -633,22 +644,22 @@ void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
 }
 
-template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
     const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block));  // incl. the column-tail lane
-    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN>), grid, dim3(kBlock), 0,
+    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN, XR>), grid, dim3(kBlock), 0,
                        st, X, N, P, ldx, a, s, acc_in, d, out);
 }
 
-template <int U, int C, bool NT, bool BAL = false>
+template <int U, int C, bool NT, bool BAL = false, bool XR = false>
 void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
 #define FA_V4(SC, ACC, FIN)                                                                   \
     do {                                                                                      \
         if constexpr (BAL) launch_balanced<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out); \
-        else launch_v4<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out);       \
+        else launch_v4<U, C, NT, SC, ACC, FIN, XR>(st, X, N, P, ldx, a, s, acc_in, d, out);   \
     } while (0)
     if (sc) {
         if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
@@ -696,6 +707,8 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     }
 #define FA_VF(U, C, NT) launch_v4_flags<U, C, NT>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VB(U, C) launch_v4_flags<U, C, true, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VX(U, C) \
+    launch_v4_flags<U, C, true, false, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     switch (variant) {  // must match kVariants[]
         case 0:
             switch (pick_quads(P)) {
@@ -722,10 +735,13 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 16: FA_VB(8, 2); break;
         case 17: FA_VF(8, 4, true); break;
         case 18: FA_VF(2, 2, true); break;
-        default: FA_VF(1, 4, true); break;
+        case 19: FA_VF(1, 4, true); break;
+        case 20: FA_VX(8, 4); break;
+        default: FA_VX(4, 1); break;
     }
 #undef FA_VF
 #undef FA_VB
+#undef FA_VX
     return check_launch("k_fold_f32_v4");
 }
 
