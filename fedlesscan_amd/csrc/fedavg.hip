@@ -609,7 +609,8 @@ inline int pick_quads(int64_t P) {
     if (nq / (2 * kBlock) >= 1000) return 2;
     return 1;
 }
-constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2"};
+constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
+                                         "bf16u1c8", "bf16u2c8", "bf16u1c4"};
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 // Resident blocks of one balanced-kernel instantiation on the current device
@@ -827,7 +828,10 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             case 1: FA_BF(8, 1); break;
             case 2: FA_BF(4, 4); break;
             case 3: FA_BF(4, 2); break;
-            default: FA_BF(8, 2); break;
+            case 4: FA_BF(8, 2); break;
+            case 5: FA_BF(1, 8); break;
+            case 6: FA_BF(2, 8); break;
+            default: FA_BF(1, 4); break;
         }
 #undef FA_BF
         return check_launch("k_fedavg_bf16_v8");
