@@ -609,8 +609,18 @@ inline int pick_quads(int64_t P) {
     if (nq / (2 * kBlock) >= 1000) return 2;
     return 1;
 }
-constexpr const char* kBf16Variants[] = {"bf16u2c4", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
-                                         "bf16u1c8", "bf16u2c8", "bf16u1c4"};
+constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
+                                         "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4"};
+
+// bf16 "auto": octets per lane from the client count.  Sweeps on MI355X
+//  put the optimum near 8 MB per block (rows x C x 4 KiB):
+// 256 rows -> C=8 (u2c8), 512 -> C=4, 1024 -> C=2 (u8c2); C shrinks further
+// while the launch would have fewer than ~1000 blocks.
+inline int pick_octets(int64_t N, int64_t P) {
+    int c = N <= 384 ? 8 : (N <= 768 ? 4 : 2);
+    while (c > 1 && (P >> 3) / ((int64_t)c * kBlock) < 1000) c >>= 1;
+    return c;
+}
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 // Resident blocks of one balanced-kernel instantiation on the current device
@@ -824,14 +834,22 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                                N, P, ldx, a, s, divisor, out_f32, out_bf16);                               \
     }
         switch (variant) {  // must match kBf16Variants[]; 0 = default (on-device sweep)
-            case 0: FA_BF(2, 4); break;
+            case 0:
+                switch (pick_octets(N, P)) {
+                    case 8: FA_BF(2, 8); break;
+                    case 4: FA_BF(4, 4); break;
+                    case 2: FA_BF(8, 2); break;
+                    default: FA_BF(8, 1); break;
+                }
+                break;
             case 1: FA_BF(8, 1); break;
             case 2: FA_BF(4, 4); break;
             case 3: FA_BF(4, 2); break;
             case 4: FA_BF(8, 2); break;
             case 5: FA_BF(1, 8); break;
             case 6: FA_BF(2, 8); break;
-            default: FA_BF(1, 4); break;
+            case 7: FA_BF(1, 4); break;
+            default: FA_BF(2, 4); break;
         }
 #undef FA_BF
         return check_launch("k_fedavg_bf16_v8");
