@@ -10,6 +10,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -77,6 +80,82 @@ bool parse_npy_header(const char* h, size_t n, std::string* descr, bool* fortran
     }
     return true;
 }
+
+// Persistent host worker pool for fa_pack: creating threads per call cost
+// more than the copies of a 128 MB chunk.  run(T, f) executes f(0..T-1) on the
+// calling thread plus up to T-1 pool workers and returns when all are done.
+class PackPool {
+  public:
+    static PackPool& get() {
+        static PackPool pool;
+        return pool;
+    }
+    void run(int T, const std::function<void(int)>& f) {
+        std::unique_lock<std::mutex> call(call_mu_);  // one job at a time
+        ensure_workers(T - 1);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            ntasks_ = T;
+            next_ = 1;
+            pending_ = T - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        for (;;) {  // the caller helps drain the task list
+            int t;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (next_ >= ntasks_) break;
+                t = next_++;
+            }
+            f(t);
+            std::lock_guard<std::mutex> lk(mu_);
+            --pending_;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    ~PackPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void ensure_workers(int n) {
+        while ((int)workers_.size() < n) workers_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            while (job_ && next_ < ntasks_) {
+                const int t = next_++;
+                const std::function<void(int)>* f = job_;
+                lk.unlock();
+                (*f)(t);
+                lk.lock();
+                if (--pending_ == 0) done_cv_.notify_all();
+            }
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* job_ = nullptr;
+    int ntasks_ = 0, next_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 }  // namespace
 
@@ -190,11 +269,11 @@ int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, cons
         work(0);
         return FA_OK;
     }
-    std::vector<std::thread> th;
-    th.reserve(T - 1);
-    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    try {
+        PackPool::get().run(T, work);
+    } catch (...) {  // e.g. thread creation failure: finish on this thread
+        for (int t = 0; t < T; ++t) work(t);
+    }
     return FA_OK;
 }
 
