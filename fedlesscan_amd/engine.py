@@ -141,7 +141,7 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
 
 
 def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[Sequence] = None, *,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, total=None) -> torch.Tensor:
     """Same fold over separately allocated 1-D CUDA rows (no stacking copy for fp32)."""
     N = len(rows)
     if N == 0:
@@ -151,9 +151,9 @@ def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[
     for r in rows:
         if r.numel() != P or r.dtype != rows[0].dtype or not r.is_contiguous() or r.device != dev:
             raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
-    if rows[0].dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores) != np.float32:
-        return fold_stacked(torch.stack([r.reshape(-1) for r in rows]), weights, scores, out=out)
-    f = Factors(weights, scores, np.dtype(np.float32))
+    if rows[0].dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32:
+        return fold_stacked(torch.stack([r.reshape(-1) for r in rows]), weights, scores, out=out, total=total)
+    f = Factors(weights, scores, np.dtype(np.float32), total=total)
     a, s = f.to(dev)
     ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).to(dev)
     out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
@@ -213,10 +213,18 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
     for _, lis in groups.items():
         sizes = [int(np.prod(shapes[li])) if len(shapes[li]) else 1 for li in lis]
         P = sum(sizes)
-        if (not on_device and P > 0 and dtypes[lis[0]] == np.float32
-                and result_dtype(np.dtype(np.float32), total_weights, sc) == np.float32):
+        fp32_result = result_dtype(np.dtype(np.float32), total_weights, sc) == np.float32
+        if (not on_device and P > 0 and dtypes[lis[0]] == np.float32 and fp32_result):
             # host fp32 rows: pipelined pinned-chunk H2D + in-order chunked fold (bit-identical)
             res = _stream_group(parameters, n_eff, lis, P, w, sc, sum(total_weights), dev)
+        elif on_device and dtypes[lis[0]] == torch.float32 and fp32_result and all(
+                parameters[i][li].is_contiguous() for i in range(n_eff) for li in lis):
+            # device fp32 layers: fold each layer straight from the clients' own
+            # tensors through a row-pointer list -- no stacking copy
+            for li in lis:
+                rows = [parameters[i][li].reshape(-1) for i in range(n_eff)]
+                outs[li] = fold_rows(rows, w, sc, total=sum(total_weights)).reshape(shapes[li])
+            continue
         else:
             X = _stack_group(parameters, n_eff, lis, sizes, P, dev, on_device)
             res = fold_stacked(X, w, sc, total=sum(total_weights))

@@ -475,3 +475,22 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
     exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
                         s=np.array(sc, np.float32) if scored else None)
     assert _bits_equal(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("case,prefix", [("f32_small", "fedavg"), ("f32_small", "stall"), ("f32_n60", "fedavg"),
+                                         ("n1", "fedavg"), ("f64_n40", "fedavg"), ("specials", "fedavg")])
+def test_device_tensor_inputs_match_golden(dev, case, prefix):
+    """Layers already on the GPU (a device-resident simulation): fp32 goes through
+    the pointer-list fold with no stacking copy; other dtypes are stacked."""
+    from fedlesscan_amd import engine
+    m = G.manifest()[case]
+    params = [[torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in p] for p in G.parameters(case)]
+    scores = None
+    if prefix == "stall":
+        scores = [(f["round_id"] + 1) / (m["current_round"] + 1) for f in G.feats(case)]
+    out = engine.aggregate_layers(params, m["weights"], scores)
+    exp = G.expected(case, prefix)
+    assert len(out) == len(exp)
+    for a, b in zip(out, exp):
+        assert a.is_cuda and tuple(a.shape) == b.shape
+        assert _bits_equal(a.cpu().numpy(), b), (case, prefix)
