@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
+#include <vector>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -83,6 +84,41 @@ __global__ __launch_bounds__(256) void fold2d(const f32x4* __restrict__ X, int64
 #pragma unroll
     for (int c = 0; c < C; ++c) t += acc[c].x + acc[c].y + acc[c].z + acc[c].w;
     if (t == 123.456f) sink[0] = t;
+}
+
+// fold2d plus the real fold's extra work, to bisect the gap to the product
+// kernel: W = multiply by a per-row weight read through the scalar cache,
+// S = store the [cols] result.
+template <int U, int C, bool W, bool S>
+__global__ __launch_bounds__(256) void fold2d_x(const f32x4* __restrict__ X, int64_t rows, int64_t ldq,
+                                                 const float* __restrict__ w, f32x4* __restrict__ out,
+                                                 float* sink) {
+    const int64_t q0 = (int64_t)blockIdx.x * (256 * C) + threadIdx.x;
+    f32x4 acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = f32x4{0, 0, 0, 0};
+    for (int64_t i = 0; i + U <= rows; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(X + (i + u) * ldq + q0 + c * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float wi = W ? w[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += W ? v[u][c] * wi : v[u][c];
+        }
+    }
+    if constexpr (S) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) out[q0 + c * 256] = acc[c];
+    } else {
+        float t = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) t += acc[c].x + acc[c].y + acc[c].z + acc[c].w;
+        if (t == 123.456f) sink[0] = t;
+    }
 }
 
 // tiled layout [P/T][rows][T]: block b owns tile b; rows of a tile are adjacent,
@@ -199,6 +235,24 @@ int main(int argc, char** argv) {
         report(nm, time_ms([&] { hipLaunchKernelGGL((chunk<true>), dim3(grid), dim3(256), 0, 0, X, nq, per, sink); }));
     }
     const int64_t ldq = cols / 4;
+    {
+        float* w;
+        f32x4* o;
+        CK(hipMalloc(&w, rows * sizeof(float)));
+        CK(hipMalloc(&o, ldq * sizeof(f32x4)));
+        std::vector<float> hw(rows, 3.0f);
+        CK(hipMemcpy(w, hw.data(), rows * sizeof(float), hipMemcpyHostToDevice));
+        report("fold2d_x u8c4 (read only)", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, false, false>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u8c4 +weights", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, false>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u8c4 +store", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, false, true>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u8c4 +weights+store", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, true>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        CK(hipFree(w));
+        CK(hipFree(o));
+    }
     report("fold2d u4c4", time_ms([&] {
         hipLaunchKernelGGL((fold2d<4, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, sink); }));
     report("fold2d u4c2", time_ms([&] {
