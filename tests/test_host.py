@@ -425,3 +425,16 @@ def test_handler_wraps_serialization_errors(oracle_fold):
     with pytest.raises(AggregationError):  # aggregation.py:164-165
         default_aggregation_handler("s", 1, st, ps, cfg)
     assert st.count_results_for_round("s", 1) == 1  # nothing deleted on failure
+
+
+def test_aggregator_settings_from_yaml(tmp_path):
+    from fedlesscan_amd.config import aggregator_settings
+    p = tmp_path / "exp.yaml"
+    p.write_text("aggregator:\n  hyperparams:\n    tolerance: 2\n    aggregate_online: true\n"
+                 "  function:\n    params: {type: openfaas, url: http://x}\n    type: openfaas\n"
+                 "clients:\n  hyperparams: {epochs: 5}\n")
+    strategy, hp = aggregator_settings(str(p), "fedlesscan")
+    assert strategy == AggregationStrategy.PER_SESSION
+    assert hp.tolerance == 2 and hp.aggregate_online is True and hp.test_batch_size == 10
+    strategy, hp = aggregator_settings({}, "fedavg")
+    assert strategy == AggregationStrategy.PER_ROUND and hp.tolerance == 0
