@@ -91,7 +91,7 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 // lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
 // multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
 // ---------------------------------------------------------------------------
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false>
 __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
                                            const float* __restrict__ a, const float* __restrict__ s,
                                            const f32x4* acc_in, float divisor, f32x4* out) {
@@ -125,7 +125,11 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
         for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * kBlock), ai, si));
     }
 #pragma unroll
-    for (int c = 0; c < C; ++c) out[c * kBlock] = FIN ? div4(acc[c], divisor) : acc[c];
+    for (int c = 0; c < C; ++c) {
+        const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
+        if constexpr (NTS) __builtin_nontemporal_store(r, out + c * kBlock);
+        else out[c * kBlock] = r;
+    }
 }
 
 // Bijective blockIdx remap that gives each of the 8 XCDs (blocks b and b+8
@@ -136,7 +140,7 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t n) {
     return x * q + (x < r ? x : r) + k;
 }
 
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
@@ -150,7 +154,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
     f32x4* O4 = reinterpret_cast<f32x4*>(out);
     if (q0 + (int64_t)(C - 1) * kBlock < nq) {
         // every quad of this lane is in range (all blocks but the last)
-        fold_quads<U, C, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
+                                                    O4 + q0);
         return;
     }
 #pragma unroll
@@ -596,6 +601,8 @@ constexpr F32Variant kVariants[] = {
     {"u8c4nt", 8, 4, true}, {"u2c2nt", 2, 2, true}, {"u1c4nt", 1, 4, true},
     // XCD-contiguous block order (each XCD streams its own contiguous column range)
     {"xcd_u8c4nt", 8, 4, true}, {"xcd_u4c1nt", 4, 1, true},
+    // non-temporal output stores
+    {"u8c4nt_nts", 8, 4, true}, {"xcd_u8c4nt_nts", 8, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -655,22 +662,22 @@ void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
 }
 
-template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false>
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false, bool NTS = false>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
     const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block));  // incl. the column-tail lane
-    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN, XR>), grid, dim3(kBlock), 0,
+    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN, XR, NTS>), grid, dim3(kBlock), 0,
                        st, X, N, P, ldx, a, s, acc_in, d, out);
 }
 
-template <int U, int C, bool NT, bool BAL = false, bool XR = false>
+template <int U, int C, bool NT, bool BAL = false, bool XR = false, bool NTS = false>
 void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
 #define FA_V4(SC, ACC, FIN)                                                                   \
     do {                                                                                      \
         if constexpr (BAL) launch_balanced<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out); \
-        else launch_v4<U, C, NT, SC, ACC, FIN, XR>(st, X, N, P, ldx, a, s, acc_in, d, out);   \
+        else launch_v4<U, C, NT, SC, ACC, FIN, XR, NTS>(st, X, N, P, ldx, a, s, acc_in, d, out); \
     } while (0)
     if (sc) {
         if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
@@ -720,6 +727,8 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #define FA_VB(U, C) launch_v4_flags<U, C, true, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VX(U, C) \
     launch_v4_flags<U, C, true, false, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VS(U, C, XR) \
+    launch_v4_flags<U, C, true, false, XR, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     switch (variant) {  // must match kVariants[]
         case 0:
             switch (pick_quads(P)) {
@@ -748,11 +757,14 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 18: FA_VF(2, 2, true); break;
         case 19: FA_VF(1, 4, true); break;
         case 20: FA_VX(8, 4); break;
-        default: FA_VX(4, 1); break;
+        case 21: FA_VX(4, 1); break;
+        case 22: FA_VS(8, 4, false); break;
+        default: FA_VS(8, 4, true); break;
     }
 #undef FA_VF
 #undef FA_VB
 #undef FA_VX
+#undef FA_VS
     return check_launch("k_fold_f32_v4");
 }
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void fold2d(const f32x4* __restrict__ X, int64
 // fold2d plus the real fold's extra work, to bisect the gap to the product
 // kernel: W = multiply by a per-row weight read through the scalar cache,
 // S = store the [cols] result.
-template <int U, int C, bool W, bool S>
+template <int U, int C, bool W, int S>
 __global__ __launch_bounds__(256) void fold2d_x(const f32x4* __restrict__ X, int64_t rows, int64_t ldq,
                                                  const float* __restrict__ w, f32x4* __restrict__ out,
                                                  float* sink) {
@@ -110,9 +110,12 @@ __global__ __launch_bounds__(256) void fold2d_x(const f32x4* __restrict__ X, int
             for (int c = 0; c < C; ++c) acc[c] += W ? v[u][c] * wi : v[u][c];
         }
     }
-    if constexpr (S) {
+    if constexpr (S == 1) {
 #pragma unroll
         for (int c = 0; c < C; ++c) out[q0 + c * 256] = acc[c];
+    } else if constexpr (S == 2) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) __builtin_nontemporal_store(acc[c], out + q0 + c * 256);
     } else {
         float t = 0;
 #pragma unroll
@@ -243,13 +246,19 @@ int main(int argc, char** argv) {
         std::vector<float> hw(rows, 3.0f);
         CK(hipMemcpy(w, hw.data(), rows * sizeof(float), hipMemcpyHostToDevice));
         report("fold2d_x u8c4 (read only)", time_ms([&] {
-            hipLaunchKernelGGL((fold2d_x<8, 4, false, false>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+            hipLaunchKernelGGL((fold2d_x<8, 4, false, 0>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         report("fold2d_x u8c4 +weights", time_ms([&] {
-            hipLaunchKernelGGL((fold2d_x<8, 4, true, false>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, 0>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         report("fold2d_x u8c4 +store", time_ms([&] {
-            hipLaunchKernelGGL((fold2d_x<8, 4, false, true>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+            hipLaunchKernelGGL((fold2d_x<8, 4, false, 1>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         report("fold2d_x u8c4 +weights+store", time_ms([&] {
-            hipLaunchKernelGGL((fold2d_x<8, 4, true, true>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, 1>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u8c4 +weights+ntstore", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, 2>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u4c1 +weights+store", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<4, 1, true, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("fold2d_x u4c1 read only", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<4, 1, false, 0>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         CK(hipFree(w));
         CK(hipFree(o));
     }
