@@ -150,6 +150,33 @@ __global__ __launch_bounds__(256) void fold_tiled(const f32x4* __restrict__ X, i
     if (t == 123.456f) sink[0] = t;
 }
 
+// tiled layout with the fold's extras (per-row weights, non-temporal output store)
+template <int U, int C>
+__global__ __launch_bounds__(256) void fold_tiled_x(const f32x4* __restrict__ X, int64_t rows,
+                                                     const float* __restrict__ w, f32x4* __restrict__ out) {
+    constexpr int TQ = 256 * C;
+    const f32x4* base = X + (int64_t)blockIdx.x * rows * TQ + threadIdx.x;
+    f32x4 acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = f32x4{0, 0, 0, 0};
+    for (int64_t i = 0; i + U <= rows; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(base + (i + u) * TQ + c * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float wi = w[i + u];
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += v[u][c] * wi;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+        __builtin_nontemporal_store(acc[c], out + (int64_t)blockIdx.x * TQ + threadIdx.x + c * 256);
+}
+
 __global__ void fill(f32x4* X, int64_t nq) {
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256)
         X[q] = f32x4{1.f, 2.f, 3.f, (float)(q & 1023)};
@@ -259,6 +286,14 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((fold2d_x<4, 1, true, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         report("fold2d_x u4c1 read only", time_ms([&] {
             hipLaunchKernelGGL((fold2d_x<4, 1, false, 0>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
+        report("tiled_x u8c1 +w+nts (T=4KiB)", time_ms([&] {
+            hipLaunchKernelGGL((fold_tiled_x<8, 1>), dim3(ldq / 256), dim3(256), 0, 0, X, rows, w, o); }));
+        report("tiled_x u4c2 +w+nts (T=8KiB)", time_ms([&] {
+            hipLaunchKernelGGL((fold_tiled_x<4, 2>), dim3(ldq / 512), dim3(256), 0, 0, X, rows, w, o); }));
+        report("tiled_x u8c4 +w+nts (T=16KiB)", time_ms([&] {
+            hipLaunchKernelGGL((fold_tiled_x<8, 4>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, w, o); }));
+        report("fold2d_x u8c4 +w+nts (again)", time_ms([&] {
+            hipLaunchKernelGGL((fold2d_x<8, 4, true, 2>), dim3(ldq / 1024), dim3(256), 0, 0, X, rows, ldq, w, o, sink); }));
         CK(hipFree(w));
         CK(hipFree(o));
     }
