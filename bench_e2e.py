@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """End-to-end aggregation rate from host-resident serialized client blobs.
 
-    python bench_e2e.py [--clients N] [--params P] [--reps R]
+    python bench_e2e.py [--clients N] [--params P] [--reps R] [--bson]
 
 What the reference's aggregator function actually does per round
 (aggregation.py:87-97, fed_avg_aggregator.py:57-92): N ClientResult objects
@@ -13,6 +13,12 @@ holding NPZ blobs -> decode -> weighted fold -> parameters.  Timed here:
   cpu_ref   the oracle's restatement of the same call (np.load decode + numpy
             fold on one core), i.e. the reference's own cost on this host
   h2d       pinned host->device copy bandwidth of the same bytes (PCIe bound)
+
+With --bson the results start where the reference keeps them: one BSON
+document per client in the (in-memory) result store, as GridFS holds them
+(client_daos.py:73).  gpu_e2e then includes the store read and the native BSON
+walk (blob stays a view); cpu_ref includes pymongo's bson.decode (the
+reference's own codec, client_daos.py:142) before the np.load + numpy fold.
 
 Rates are input bytes (N * P * 4) per second.  Results are compared bit for bit.
 Writes one JSON line (rank 0, one GPU).  Not the headline metric: DESIGN.md.
@@ -67,6 +73,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--bson", action="store_true", help="start from BSON documents in the result store")
     a = ap.parse_args()
     from oracle import fedavg_oracle as O  # checker + CPU reference timing only
     N, P = a.clients, a.params
@@ -78,14 +85,28 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
 
+    store = None
+    if a.bson:
+        from fedlesscan_amd.store import InMemoryClientResultStore
+        store = InMemoryClientResultStore()
+        for i, cr in enumerate(results(blobs, cards)):
+            store.save("bench", 1, f"client-{i}", cr)
+
+    def one_round(crs):
+        if store is not None:
+            agg = FedAvgAggregator()
+            feats, it = agg.select_aggregation_candidates(store, "bench", 1)
+            return agg.aggregate(list(it), feats)
+        return FedAvgAggregator().aggregate(crs, None)
+
     # warm up the pipeline (pinned allocations, library load)
     FedAvgAggregator().aggregate(results(blobs[: min(N, 4)], cards[: min(N, 4)]), None)
     torch.cuda.synchronize()
     ts, out = [], None
     for _ in range(a.reps):
-        crs = results(blobs, cards)
+        crs = None if store is not None else results(blobs, cards)
         t0 = time.perf_counter()
-        out, _ = FedAvgAggregator().aggregate(crs, None)
+        out, _ = one_round(crs)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     t_gpu = sorted(ts)[len(ts) // 2]
@@ -108,13 +129,19 @@ def main():
 
     res = {
         "metric": "end-to-end aggregation GB/s from host NPZ blobs (not the headline)",
+        "source": "BSON documents in the result store" if a.bson else "ClientResult objects holding NPZ blobs",
         "clients": N, "params": P, "input_bytes": in_bytes, "gen_s": round(gen_s, 1),
         "gpu_e2e_s": round(t_gpu, 4), "gpu_e2e_gbs": round(in_bytes / t_gpu / 1e9, 2),
         "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),
     }
     if not a.no_cpu:
-        dicts = [{"blob": b, "cardinality": c} for b, c in zip(blobs, cards)]
         t0 = time.perf_counter()
+        if store is not None:
+            import bson  # pymongo's codec: the reference's own decode (CPU leg only)
+            docs = [bson.decode(store._files[d["file_id"]]) for d in store._docs]
+            dicts = [{"blob": d["parameters"]["blob"], "cardinality": d["cardinality"]} for d in docs]
+        else:
+            dicts = [{"blob": b, "cardinality": c} for b, c in zip(blobs, cards)]
         ref, _ = O.aggregate_fedavg(dicts)
         t_cpu = time.perf_counter() - t0
         res["cpu_ref_s"] = round(t_cpu, 3)

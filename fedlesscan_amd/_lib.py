@@ -54,6 +54,7 @@ _PROTOS = {
     "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
     "fa_npz_index": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int]),
     "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
+    "fa_bson_elements": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
 }
 
 _lock = threading.Lock()

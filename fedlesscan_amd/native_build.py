@@ -15,7 +15,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "fedavg.hip")
-HOST_SRC = os.path.join(PKG, "csrc", "ingest_host.cpp")
+HOST_SRCS = [os.path.join(PKG, "csrc", f) for f in ("ingest_host.cpp", "bson_host.cpp")]
 HDR = os.path.join(REPO, "include", "fedavg_hip.h")
 OUT_DIR = os.path.join(PKG, "_native")
 LIB = os.path.join(OUT_DIR, "libfedavg_hip.so")
@@ -38,7 +38,7 @@ def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, HOST_SRC, HDR))
+    return any(os.path.getmtime(p) > t for p in (SRC, *HOST_SRCS, HDR))
 
 
 def build(force: bool = False, isa_dir: str | None = None) -> str:
@@ -46,7 +46,7 @@ def build(force: bool = False, isa_dir: str | None = None) -> str:
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, SRC, HOST_SRC]
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, SRC, *HOST_SRCS]
     if isa_dir:
         os.makedirs(isa_dir, exist_ok=True)
         cmd.insert(1, "-save-temps")

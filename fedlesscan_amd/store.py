@@ -15,6 +15,11 @@ reported afterwards; those semantics are restated here:
 Iteration order is insertion order; an upsert of an existing
 (session, round, client) key keeps its position (Mongo natural order keeps a
 replaced document's record slot).
+
+Each stored result is what GridFS holds in the reference: the BSON bytes of
+`result.dict()` (client_daos.py:73, 369), written by fedlesscan_amd.bsondoc.
+Loading parses them back (client_daos.py:142, 397); results come back with the
+NPZ blob as a zero-copy view into those bytes, so the ingest never copies it.
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ import itertools
 import threading
 from typing import Dict, Iterator, List, Optional, Tuple
 
+from . import bsondoc
 from .common.models import ClientResult, SerializedParameters
 
 
@@ -32,13 +38,13 @@ class DocumentNotLoadedException(Exception):
 class InMemoryClientResultStore:
     def __init__(self):
         self._docs: List[dict] = []
-        self._files: Dict[int, ClientResult] = {}
+        self._files: Dict[int, bytes] = {}  # file_id -> BSON document (the GridFS file)
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
 
     def save(self, session_id: str, round_id: int, client_id: str, result, overwrite: bool = True):
-        if isinstance(result, dict):
-            result = ClientResult.model_validate(result)
+        # client_daos.py:55-56, 73: a ClientResult is dumped, a dict is stored as given
+        data = bsondoc.encode(result.model_dump() if isinstance(result, ClientResult) else result)
         with self._lock:
             key = (session_id, round_id, client_id)
             existing = next((d for d in self._docs
@@ -47,7 +53,7 @@ class InMemoryClientResultStore:
                 raise ValueError(f"Client result for session {session_id} and round {round_id} for client "
                                  f"{client_id} already exists. Force overwrite with overwrite=True")
             file_id = next(self._ids)
-            self._files[file_id] = result.model_copy(deep=True)
+            self._files[file_id] = data
             doc = {"session_id": session_id, "round_id": round_id, "client_id": client_id, "file_id": file_id}
             if existing is not None:
                 self._files.pop(existing["file_id"], None)
@@ -59,7 +65,7 @@ class InMemoryClientResultStore:
     def load(self, session_id: str, round_id: int, client_id: str) -> ClientResult:
         for d in self._docs:
             if (d["session_id"], d["round_id"], d["client_id"]) == (session_id, round_id, client_id):
-                return self._files[d["file_id"]].model_copy(deep=True)
+                return bsondoc.client_result_from_bson(self._files[d["file_id"]])
         raise DocumentNotLoadedException(
             f"Client result for session {session_id} and round {round_id} for client {client_id} not found.")
 
@@ -70,7 +76,7 @@ class InMemoryClientResultStore:
                 raise DocumentNotLoadedException(
                     f"GridFS file with results in session {session_id},{round_id} and client round "
                     f"{d['round_id']} not found.")
-            yield f.model_copy(deep=True)
+            yield bsondoc.client_result_from_bson(f)
 
     def load_results_for_round(self, session_id: str, round_id: int) -> Tuple[List[dict], Iterator[ClientResult]]:
         dicts = [dict(d) for d in self._docs if d["session_id"] == session_id and d["round_id"] == round_id]
@@ -112,25 +118,26 @@ class InMemoryParameterStore:
     """ParameterDao (client_daos.py:351-437): global model blob per (session, round)."""
 
     def __init__(self):
-        self._params: Dict[Tuple[str, int], SerializedParameters] = {}
+        self._params: Dict[Tuple[str, int], bytes] = {}  # (session, round) -> BSON document
 
     def save(self, session_id: str, round_id: int, params: SerializedParameters, overwrite: bool = True):
         key = (session_id, round_id)
         if key in self._params and not overwrite:
             raise ValueError(f"Parameters for session {session_id} and round {round_id} already exist")
-        self._params[key] = params
+        self._params[key] = bsondoc.encode(params.model_dump())
 
     def load(self, session_id: str, round_id: int) -> SerializedParameters:
         try:
-            return self._params[(session_id, round_id)]
+            data = self._params[(session_id, round_id)]
         except KeyError:
             raise DocumentNotLoadedException(f"Parameters for session {session_id} round {round_id} not found")
+        return bsondoc.parameters_from_bson(data)
 
     def load_latest(self, session_id: str) -> SerializedParameters:
         rounds = [r for (s, r) in self._params if s == session_id]
         if not rounds:
             raise DocumentNotLoadedException(f"No parameters for session {session_id}")
-        return self._params[(session_id, max(rounds))]
+        return self.load(session_id, max(rounds))
 
     def get_latest_round(self, session_id: str) -> Optional[int]:
         rounds = [r for (s, r) in self._params if s == session_id]

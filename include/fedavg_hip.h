@@ -148,6 +148,27 @@ int fa_npz_index(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* co
 int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, const int64_t* sizes, int64_t n,
             int nthreads);
 
+/* ---- host-side ingest (no GPU): the persisted BSON document -----------------
+ * The reference stores each ClientResult as bson.encode(result.dict()) in
+ * GridFS (client_daos.py:73) and reads it back with
+ * ClientResult.parse_obj(bson.decode(file.read())) (client_daos.py:142), a
+ * decode that copies the NPZ blob.  fa_bson_elements replaces the walk inside
+ * bson.decode for one document level: for the document starting at
+ * buf[doc_off] it reports, per element in order, the type byte, the name
+ * (offset, length without NUL) and the value (offset, length):
+ *   string/code/symbol -> the UTF-8 bytes without NUL; binary -> the payload
+ *   (subtype in subtypes[], old subtype 2 unwrapped); document/array -> the
+ *   embedded document itself (walk it with doc_off = its offset); fixed-size
+ *   scalars -> their 1/4/8/12/16 bytes; null/undefined/min/max key -> length 0.
+ * Offsets are relative to buf.  Returns the element count (only the first
+ * max_elems are written; any output array may be NULL), or a negative
+ * FA_BSON_* code.  Every length is bounds-checked against the enclosing
+ * document. */
+enum fa_bson_status { FA_BSON_MALFORMED = -1, FA_BSON_UNSUPPORTED = -2 };
+int64_t fa_bson_elements(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types,
+                         int64_t* name_offs, int32_t* name_lens, int64_t* val_offs, int64_t* val_lens,
+                         uint8_t* subtypes, int64_t max_elems);
+
 #ifdef __cplusplus
 }
 #endif
