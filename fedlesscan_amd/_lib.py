@@ -55,6 +55,7 @@ _PROTOS = {
     "fa_npz_index": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int]),
     "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
     "fa_bson_elements": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
+    "fa_bson_walk": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
 }
 
 _lock = threading.Lock()

@@ -11,8 +11,8 @@ BSON document in GridFS:
 `bson` there is pymongo's codec (pymongo~=3.11.3, requirements/requirements.txt:8;
 bsonspec.org 1.1).  This module restates the part of it those documents use:
 
-  decode(data, zero_copy)   element walk by the native fa_bson_elements (C++,
-                            bounds-checked); binary subtype 0 comes back as a
+  decode(data, zero_copy)   element table from one native fa_bson_walk call
+                            (C++, bounds-checked); binary subtype 0 comes back as a
                             memoryview into `data` when zero_copy, so a 40 MB NPZ
                             blob is never copied on its way to pinned staging
   encode(doc)               byte-identical to bson.encode for dict / list /
@@ -30,9 +30,9 @@ values raise InvalidBSON: no persisted FedLesScan document holds them.
 """
 from __future__ import annotations
 
-import ctypes
 import datetime as _dt
 import struct
+import threading
 from enum import Enum
 from typing import Any, Dict, Tuple
 
@@ -79,80 +79,81 @@ class ObjectId(bytes):
 _EPOCH = _dt.datetime(1970, 1, 1)
 _I32, _I64, _F64 = struct.Struct("<i"), struct.Struct("<q"), struct.Struct("<d")
 _MAX_ELEMS = 64
+FA_BSON_MALFORMED, FA_BSON_UNSUPPORTED = -1, -2  # include/fedavg_hip.h
 
 
-def _elements(buf: memoryview, arr: np.ndarray, off: int):
-    """[(type, name, value_offset, value_length, subtype)] of the document at off."""
-    L = _lib.load()
-    cap = _MAX_ELEMS
+class _Scratch:
+    """Output arrays for fa_bson_walk, one set per thread, grown on demand."""
+
+    def __init__(self, cap: int = _MAX_ELEMS):
+        self.grow(cap)
+
+    def grow(self, cap: int):
+        self.cap = cap
+        self.ty = np.empty(cap, np.uint8)
+        self.pa = np.empty(cap, np.int32)
+        self.no = np.empty(cap, np.int64)
+        self.nl = np.empty(cap, np.int32)
+        self.vo = np.empty(cap, np.int64)
+        self.vl = np.empty(cap, np.int64)
+        self.st = np.empty(cap, np.uint8)
+        self.ptrs = [a.ctypes.data for a in (self.ty, self.pa, self.no, self.nl, self.vo, self.vl, self.st)]
+
+
+_tls = threading.local()
+
+
+def _walk(buf: memoryview, base: int):
+    """Flat pre-order element table of the whole document (one native call)."""
+    sc = getattr(_tls, "scratch", None)
+    if sc is None:
+        sc = _tls.scratch = _Scratch()
+    fn = _lib.load().fa_bson_walk
     while True:
-        ty = np.empty(cap, np.uint8)
-        no = np.empty(cap, np.int64)
-        nl = np.empty(cap, np.int32)
-        vo = np.empty(cap, np.int64)
-        vl = np.empty(cap, np.int64)
-        st = np.empty(cap, np.uint8)
-        n = L.fa_bson_elements(arr.ctypes.data_as(ctypes.c_void_p), len(buf), off, ty.ctypes.data,
-                               no.ctypes.data, nl.ctypes.data, vo.ctypes.data, vl.ctypes.data, st.ctypes.data,
-                               cap)
-        if n == -2:
-            raise InvalidBSON(f"unsupported BSON element type in document at offset {off}")
+        n = fn(base, len(buf), 0, *sc.ptrs, sc.cap)
+        if n == FA_BSON_UNSUPPORTED:
+            raise InvalidBSON("unsupported BSON element type")
         if n < 0:
-            raise InvalidBSON(f"malformed BSON document at offset {off}")
-        if n <= cap:
-            return [(int(ty[k]), int(no[k]), int(nl[k]), int(vo[k]), int(vl[k]), int(st[k])) for k in range(n)]
-        cap = int(n)
+            raise InvalidBSON("malformed BSON document")
+        if n <= sc.cap:
+            return (sc.ty[:n].tolist(), sc.pa[:n].tolist(), sc.no[:n].tolist(), sc.nl[:n].tolist(),
+                    sc.vo[:n].tolist(), sc.vl[:n].tolist(), sc.st[:n].tolist())
+        sc.grow(int(n))
 
 
-def _decode_doc(buf: memoryview, arr: np.ndarray, off: int, zero_copy: bool, as_list: bool):
-    out_d: Dict[str, Any] = {}
-    out_l = []
-    for t, no, nl, vo, vl, st in _elements(buf, arr, off):
-        if t == 0x01:
-            v = _F64.unpack_from(buf, vo)[0]
-        elif t == 0x02:
-            try:
-                v = str(buf[vo:vo + vl], "utf-8")
-            except UnicodeDecodeError as e:
-                raise InvalidBSON(f"invalid UTF-8 string: {e}") from e
-        elif t in (0x03, 0x04):
-            v = _decode_doc(buf, arr, vo, zero_copy, t == 0x04)
-        elif t == 0x05:
-            raw = buf[vo:vo + vl]
-            if st == 0:
-                v = raw if zero_copy else raw.tobytes()
-            else:
-                v = Binary(raw.tobytes(), st)
-        elif t in (0x06, 0x0A):
-            v = None
-        elif t == 0x07:
-            v = ObjectId(buf[vo:vo + 12].tobytes())
-        elif t == 0x08:
-            v = buf[vo] == 1
-        elif t == 0x09:
-            ms = _I64.unpack_from(buf, vo)[0]
-            try:
-                v = _EPOCH + _dt.timedelta(milliseconds=ms)
-            except OverflowError as e:
-                raise InvalidBSON(f"datetime out of range: {ms} ms") from e
-        elif t == 0x10:
-            v = _I32.unpack_from(buf, vo)[0]
-        elif t == 0x11:
-            inc, ts = struct.unpack_from("<II", buf, vo)
-            v = (ts, inc)
-        elif t == 0x12:
-            v = Int64(_I64.unpack_from(buf, vo)[0])
-        else:
-            raise InvalidBSON(f"BSON type 0x{t:02x} is not used by persisted FedLesScan documents")
-        if as_list:
-            out_l.append(v)
-        else:
-            try:
-                name = str(buf[no:no + nl], "utf-8")
-            except UnicodeDecodeError as e:
-                raise InvalidBSON(f"invalid UTF-8 key: {e}") from e
-            out_d[name] = v
-    return out_l if as_list else out_d
+def _scalar(buf: memoryview, t: int, vo: int, vl: int, st: int, zero_copy: bool):
+    if t == 0x01:
+        return _F64.unpack_from(buf, vo)[0]
+    if t == 0x02:
+        try:
+            return str(buf[vo:vo + vl], "utf-8")
+        except UnicodeDecodeError as e:
+            raise InvalidBSON(f"invalid UTF-8 string: {e}") from e
+    if t == 0x05:
+        raw = buf[vo:vo + vl]
+        if st == 0:
+            return raw if zero_copy else raw.tobytes()
+        return Binary(raw.tobytes(), st)
+    if t in (0x06, 0x0A):
+        return None
+    if t == 0x07:
+        return ObjectId(buf[vo:vo + 12].tobytes())
+    if t == 0x08:
+        return buf[vo] == 1
+    if t == 0x09:
+        ms = _I64.unpack_from(buf, vo)[0]
+        try:
+            return _EPOCH + _dt.timedelta(milliseconds=ms)
+        except OverflowError as e:
+            raise InvalidBSON(f"datetime out of range: {ms} ms") from e
+    if t == 0x10:
+        return _I32.unpack_from(buf, vo)[0]
+    if t == 0x11:
+        inc, ts = struct.unpack_from("<II", buf, vo)
+        return (ts, inc)
+    if t == 0x12:
+        return Int64(_I64.unpack_from(buf, vo)[0])
+    raise InvalidBSON(f"BSON type 0x{t:02x} is not used by persisted FedLesScan documents")
 
 
 def decode(data, zero_copy: bool = False) -> Dict[str, Any]:
@@ -162,8 +163,27 @@ def decode(data, zero_copy: bool = False) -> Dict[str, Any]:
         raise InvalidBSON("not enough data for a BSON document")
     if _I32.unpack_from(buf, 0)[0] != len(buf):
         raise InvalidBSON("BSON document length does not match the data")
-    arr = np.frombuffer(buf, dtype=np.uint8)
-    return _decode_doc(buf, arr, 0, zero_copy, False)
+    arr = np.frombuffer(buf, dtype=np.uint8)  # keeps the address valid for the walk
+    ty, pa, no, nl, vo, vl, st = _walk(buf, arr.ctypes.data)
+    root: Dict[str, Any] = {}
+    containers: Dict[int, Any] = {-1: root}
+    for k in range(len(ty)):
+        t = ty[k]
+        if t == 0x03:
+            v = containers[k] = {}
+        elif t == 0x04:
+            v = containers[k] = []
+        else:
+            v = _scalar(buf, t, vo[k], vl[k], st[k], zero_copy)
+        parent = containers[pa[k]]
+        if isinstance(parent, list):
+            parent.append(v)
+        else:
+            try:
+                parent[str(buf[no[k]:no[k] + nl[k]], "utf-8")] = v
+            except UnicodeDecodeError as e:
+                raise InvalidBSON(f"invalid UTF-8 key: {e}") from e
+    return root
 
 
 # ---------------------------------------------------------------------------

@@ -4,16 +4,18 @@
 // `self._gridfs.put(bson.encode(result.dict()))` (client_daos.py:73), and reads
 // it back with `ClientResult.parse_obj(bson.decode(results_file.read()))`
 // (client_daos.py:142).  bson.decode copies the NPZ blob out of the document
-// into a fresh bytes object.  fa_bson_elements only locates each element of one
-// document level, so the host mirror (fedlesscan_amd/bsondoc.py) hands the blob
-// on as a view into the GridFS bytes and the ingest packs it straight into
-// pinned staging (fa_npz_index + fa_pack).
+// into a fresh bytes object.  fa_bson_elements (one document level) and
+// fa_bson_walk (the whole tree, one call) only locate the elements, so the host
+// mirror (fedlesscan_amd/bsondoc.py) hands the blob on as a view into the
+// GridFS bytes and the ingest packs it straight into pinned staging
+// (fa_npz_index + fa_pack).
 //
 // Format: bsonspec.org 1.1, little-endian.  document = int32 total_len,
 // element*, 0x00; element = type byte, cstring name, value.  Every length is
 // checked against the enclosing document before it is used.
 #include <cstdint>
 #include <cstring>
+#include <climits>
 
 #include "fedavg_hip.h"
 
@@ -45,12 +47,11 @@ struct Walk {
     }
 };
 
-}  // namespace
-
-extern "C" int64_t fa_bson_elements(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types,
-                                    int64_t* name_offs, int32_t* name_lens, int64_t* val_offs,
-                                    int64_t* val_lens, uint8_t* subtypes, int64_t max_elems) {
-    if (!buf || buf_len < 5 || doc_off < 0 || doc_off > buf_len - 5 || max_elems < 0) return FA_BSON_MALFORMED;
+// One document level: calls sink(t, name_off, name_len, val_off, val_len, sub)
+// per element in order; returns the element count or a FA_BSON_* code.
+template <class Sink>
+int64_t walk_level(const uint8_t* buf, int64_t buf_len, int64_t doc_off, Sink&& sink) {
+    if (!buf || buf_len < 5 || doc_off < 0 || doc_off > buf_len - 5) return FA_BSON_MALFORMED;
     int32_t total;
     std::memcpy(&total, buf + doc_off, 4);
     if (total < 5 || (int64_t)total > buf_len - doc_off) return FA_BSON_MALFORMED;
@@ -118,16 +119,66 @@ extern "C" int64_t fa_bson_elements(const uint8_t* buf, int64_t buf_len, int64_t
                 return FA_BSON_UNSUPPORTED;
         }
         if (next > last) return FA_BSON_MALFORMED;
-        if (n < max_elems) {
-            if (types) types[n] = t;
-            if (name_offs) name_offs[n] = name_off;
-            if (name_lens) name_lens[n] = (int32_t)name_len;
-            if (val_offs) val_offs[n] = voff;
-            if (val_lens) val_lens[n] = vlen;
-            if (subtypes) subtypes[n] = sub;
-        }
+        const int64_t rc = sink(t, name_off, name_len, voff, vlen, sub);
+        if (rc < 0) return rc;
         ++n;
         p = next;
     }
     return p == last ? n : FA_BSON_MALFORMED;
+}
+
+struct Out {
+    uint8_t* types; int32_t* parents; int64_t* name_offs; int32_t* name_lens;
+    int64_t* val_offs; int64_t* val_lens; uint8_t* subtypes; int64_t max;
+    void put(int64_t k, uint8_t t, int32_t parent, int64_t no, int64_t nl, int64_t vo, int64_t vl, uint8_t sub) const {
+        if (k >= max) return;
+        if (types) types[k] = t;
+        if (parents) parents[k] = parent;
+        if (name_offs) name_offs[k] = no;
+        if (name_lens) name_lens[k] = (int32_t)nl;
+        if (val_offs) val_offs[k] = vo;
+        if (val_lens) val_lens[k] = vl;
+        if (subtypes) subtypes[k] = sub;
+    }
+};
+
+constexpr int kMaxDepth = 100;
+
+// pre-order: each element, then (for documents and arrays) its subtree
+int64_t walk_tree(const uint8_t* buf, int64_t buf_len, int64_t doc_off, int32_t parent, int depth,
+                  const Out& out, int64_t* count) {
+    if (depth > kMaxDepth) return FA_BSON_MALFORMED;
+    return walk_level(buf, buf_len, doc_off, [&](uint8_t t, int64_t no, int64_t nl, int64_t vo, int64_t vl,
+                                                 uint8_t sub) -> int64_t {
+        const int64_t me = (*count)++;
+        if (me > INT32_MAX) return FA_BSON_MALFORMED;
+        out.put(me, t, parent, no, nl, vo, vl, sub);
+        if (t == 0x03 || t == 0x04) return walk_tree(buf, buf_len, vo, (int32_t)me, depth + 1, out, count);
+        return 0;
+    });
+}
+
+}  // namespace
+
+extern "C" int64_t fa_bson_elements(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types,
+                                    int64_t* name_offs, int32_t* name_lens, int64_t* val_offs,
+                                    int64_t* val_lens, uint8_t* subtypes, int64_t max_elems) {
+    if (max_elems < 0) return FA_BSON_MALFORMED;
+    const Out out{types, nullptr, name_offs, name_lens, val_offs, val_lens, subtypes, max_elems};
+    int64_t k = 0;
+    return walk_level(buf, buf_len, doc_off, [&](uint8_t t, int64_t no, int64_t nl, int64_t vo, int64_t vl,
+                                                 uint8_t sub) -> int64_t {
+        out.put(k++, t, -1, no, nl, vo, vl, sub);
+        return 0;
+    });
+}
+
+extern "C" int64_t fa_bson_walk(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types,
+                                int32_t* parents, int64_t* name_offs, int32_t* name_lens, int64_t* val_offs,
+                                int64_t* val_lens, uint8_t* subtypes, int64_t max_elems) {
+    if (max_elems < 0) return FA_BSON_MALFORMED;
+    const Out out{types, parents, name_offs, name_lens, val_offs, val_lens, subtypes, max_elems};
+    int64_t count = 0;
+    const int64_t rc = walk_tree(buf, buf_len, doc_off, -1, 0, out, &count);
+    return rc < 0 ? rc : count;
 }

@@ -168,6 +168,14 @@ enum fa_bson_status { FA_BSON_MALFORMED = -1, FA_BSON_UNSUPPORTED = -2 };
 int64_t fa_bson_elements(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types,
                          int64_t* name_offs, int32_t* name_lens, int64_t* val_offs, int64_t* val_lens,
                          uint8_t* subtypes, int64_t max_elems);
+/* [host] The whole tree of the document at buf[doc_off] in one call, in
+ * pre-order: every element, then (for a document or array) its subtree.
+ * parents[k] is the index of element k's enclosing document/array element, or
+ * -1 at the top level; the other arrays as fa_bson_elements.  Nesting deeper
+ * than 100 levels is FA_BSON_MALFORMED.  Returns the total element count. */
+int64_t fa_bson_walk(const uint8_t* buf, int64_t buf_len, int64_t doc_off, uint8_t* types, int32_t* parents,
+                     int64_t* name_offs, int32_t* name_lens, int64_t* val_offs, int64_t* val_lens,
+                     uint8_t* subtypes, int64_t max_elems);
 
 #ifdef __cplusplus
 }

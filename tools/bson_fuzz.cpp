@@ -1,8 +1,10 @@
-// ASan/UBSan fuzz of fa_bson_elements (host only, no GPU):
+// ASan/UBSan fuzz of fa_bson_elements and fa_bson_walk (host only, no GPU):
 //   g++ -std=c++17 -g -O1 -fsanitize=address,undefined -Iinclude tools/bson_fuzz.cpp \
 //       fedlesscan_amd/csrc/bson_host.cpp -o tools/build/bson_fuzz && tools/build/bson_fuzz seed.bson
 // Every truncation of the seed, then random 1-4 byte mutations; each parse walks
-// nested documents/arrays recursively, as fedlesscan_amd/bsondoc.py does.
+// nested documents/arrays recursively with fa_bson_elements and must agree
+// with the one-call fa_bson_walk (same verdict, same element count, parents
+// pointing at earlier document/array elements).
 #include <cstdio>
 #include <cstdint>
 #include <random>
@@ -32,6 +34,24 @@ static int64_t walk(const uint8_t* b, int64_t n, int64_t off, int depth) {
     return total;
 }
 
+static int64_t both(const uint8_t* b, int64_t n) {
+    const int64_t r = walk(b, n, 0, 0);
+    static uint8_t ty[4096], st[4096];
+    static int32_t pa[4096], nl[4096];
+    static int64_t no[4096], vo[4096], vl[4096];
+    const int64_t w = fa_bson_walk(b, n, 0, ty, pa, no, nl, vo, vl, st, 4096);
+    if ((r < 0) != (w < 0) || (r >= 0 && r != w)) {
+        std::fprintf(stderr, "walk mismatch: levels %lld, tree %lld\n", (long long)r, (long long)w);
+        std::abort();
+    }
+    for (int64_t k = 0; k < w && k < 4096; ++k)
+        if (pa[k] >= k || (pa[k] >= 0 && ty[pa[k]] != 0x03 && ty[pa[k]] != 0x04) || vo[k] + vl[k] > n) {
+            std::fprintf(stderr, "bad tree element %lld\n", (long long)k);
+            std::abort();
+        }
+    return r;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     FILE* f = std::fopen(argv[1], "rb");
@@ -43,15 +63,15 @@ int main(int argc, char** argv) {
     long ok = 0, bad = 0;
     for (size_t cut = 0; cut <= n; ++cut) {
         std::vector<uint8_t> c(seed.begin(), seed.begin() + cut);  // exact-size heap buffer
-        (walk(c.data(), (int64_t)cut, 0, 0) >= 0 ? ok : bad)++;
+        (both(c.data(), (int64_t)cut) >= 0 ? ok : bad)++;
     }
     std::mt19937 rng(7);
     for (int it = 0; it < 300000; ++it) {
         std::vector<uint8_t> c = seed;
         for (int j = 0, m = 1 + rng() % 4; j < m; ++j) c[rng() % n] = (uint8_t)rng();
-        (walk(c.data(), (int64_t)n, 0, 0) >= 0 ? ok : bad)++;
+        (both(c.data(), (int64_t)n) >= 0 ? ok : bad)++;
     }
     std::printf("bson fuzz: %ld accepted, %ld rejected, seed walk = %lld elements\n", ok, bad,
-                (long long)walk(seed.data(), (int64_t)n, 0, 0));
+                (long long)both(seed.data(), (int64_t)n));
     return 0;
 }
