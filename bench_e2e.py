@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """End-to-end aggregation rate from host-resident serialized client blobs.
 
-    python bench_e2e.py [--clients N] [--params P] [--reps R] [--bson]
+    python bench_e2e.py [--clients N] [--params P] [--reps R] [--bson [--pinned-store]]
 
 What the reference's aggregator function actually does per round
 (aggregation.py:87-97, fed_avg_aggregator.py:57-92): N ClientResult objects
@@ -19,6 +19,8 @@ document per client in the (in-memory) result store, as GridFS holds them
 (client_daos.py:73).  gpu_e2e then includes the store read and the native BSON
 walk (blob stays a view); cpu_ref includes pymongo's bson.decode (the
 reference's own codec, client_daos.py:142) before the np.load + numpy fold.
+--pinned-store keeps those documents in page-locked memory: the ingest then
+DMAs every layer straight from its document, with no packing copy.
 
 Rates are input bytes (N * P * 4) per second.  Results are compared bit for bit.
 Writes one JSON line (rank 0, one GPU).  Not the headline metric: DESIGN.md.
@@ -74,6 +76,7 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--bson", action="store_true", help="start from BSON documents in the result store")
+    ap.add_argument("--pinned-store", action="store_true", help="with --bson: documents in page-locked memory")
     a = ap.parse_args()
     from oracle import fedavg_oracle as O  # checker + CPU reference timing only
     N, P = a.clients, a.params
@@ -86,9 +89,9 @@ def main():
     torch.cuda.set_device(dev)
 
     store = None
-    if a.bson:
+    if a.bson or a.pinned_store:
         from fedlesscan_amd.store import InMemoryClientResultStore
-        store = InMemoryClientResultStore()
+        store = InMemoryClientResultStore(pinned=a.pinned_store)
         for i, cr in enumerate(results(blobs, cards)):
             store.save("bench", 1, f"client-{i}", cr)
 
@@ -110,6 +113,8 @@ def main():
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     t_gpu = sorted(ts)[len(ts) // 2]
+    from fedlesscan_amd.ingest import StreamingFold
+    routes = dict(StreamingFold.stats)
 
     # decode-only (zero-copy views) and pinned H2D of the same bytes
     from fedlesscan_amd.npz import read_layers
@@ -129,16 +134,18 @@ def main():
 
     res = {
         "metric": "end-to-end aggregation GB/s from host NPZ blobs (not the headline)",
-        "source": "BSON documents in the result store" if a.bson else "ClientResult objects holding NPZ blobs",
+        "source": ("BSON documents in a page-locked result store" if a.pinned_store else
+                   "BSON documents in the result store" if a.bson else "ClientResult objects holding NPZ blobs"),
         "clients": N, "params": P, "input_bytes": in_bytes, "gen_s": round(gen_s, 1),
         "gpu_e2e_s": round(t_gpu, 4), "gpu_e2e_gbs": round(in_bytes / t_gpu / 1e9, 2),
         "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),
+        "ingest_rows": routes,
     }
     if not a.no_cpu:
         t0 = time.perf_counter()
         if store is not None:
             import bson  # pymongo's codec: the reference's own decode (CPU leg only)
-            docs = [bson.decode(store._files[d["file_id"]]) for d in store._docs]
+            docs = [bson.decode(bytes(store._files[d["file_id"]])) for d in store._docs]
             dicts = [{"blob": d["parameters"]["blob"], "cardinality": d["cardinality"]} for d in docs]
         else:
             dicts = [{"blob": b, "cardinality": c} for b, c in zip(blobs, cards)]

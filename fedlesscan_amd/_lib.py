@@ -56,6 +56,10 @@ _PROTOS = {
     "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
     "fa_bson_elements": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
     "fa_bson_walk": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
+    "fa_host_is_pinned": (_int, [_vp, _i64]),
+    "fa_host_alloc": (_int, [_vp, _i64]),
+    "fa_host_free": (_int, [_vp]),
+    "fa_copy_h2d": (_int, [_vp, _vp, _i64, _vp]),
 }
 
 _lock = threading.Lock()

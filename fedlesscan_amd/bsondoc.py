@@ -265,6 +265,24 @@ def encode(doc: Dict[str, Any]) -> bytes:
     return b"".join(parts)
 
 
+def encode_into(doc: Dict[str, Any], alloc) -> memoryview:
+    """encode(doc) written into alloc(size), a writable byte buffer of exactly
+    `size` bytes (e.g. pinned.pinned_bytes); same bytes, same single copy."""
+    if not isinstance(doc, dict):
+        raise TypeError(f"encode_into() takes a dict, not {type(doc)}")
+    parts: list = []
+    size = _encode_doc(parts, doc.items())
+    out = memoryview(alloc(size)).cast("B")
+    if len(out) != size:
+        raise ValueError(f"alloc returned {len(out)} bytes, expected {size}")
+    pos = 0
+    for part in parts:
+        n = memoryview(part).nbytes
+        out[pos:pos + n] = memoryview(part).cast("B")
+        pos += n
+    return out
+
+
 # ---------------------------------------------------------------------------
 # the two persisted document kinds
 # ---------------------------------------------------------------------------

@@ -959,4 +959,49 @@ int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, 
     return check_launch("k_read_sweep");
 }
 
+// ---- host staging: page-locked documents and direct DMA ---------------------
+int fa_host_is_pinned(const void* p, int64_t n) {
+    if (!p || n <= 0) return 0;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // unregistered pageable memory: not an error for the caller
+        return 0;
+    }
+    if (at.type != hipMemoryTypeHost) return 0;
+    // the whole range must lie inside that one allocation
+    hipDeviceptr_t start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(start), q = reinterpret_cast<uintptr_t>(p);
+    return q >= lo && q + (uint64_t)n <= lo + size ? 1 : 0;
+}
+
+int fa_host_alloc(void** p, int64_t n) {
+    if (!p || n <= 0) return fail(FA_ERR_ARG, "fa_host_alloc: bad size %lld", (long long)n);
+    *p = nullptr;
+    hipError_t e = hipHostMalloc(p, (size_t)n, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipHostMalloc(%lld): %s", (long long)n, hipGetErrorString(e));
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+int fa_host_free(void* p) {
+    if (!p) return FA_OK;
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipHostFree: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+int fa_copy_h2d(void* dst, const void* src, int64_t n, void* stream) {
+    if (n < 0 || (n && (!dst || !src))) return fail(FA_ERR_ARG, "fa_copy_h2d: bad arguments");
+    if (n == 0) return FA_OK;
+    hipError_t e = hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipMemcpyAsync H2D: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
 }  // extern "C"

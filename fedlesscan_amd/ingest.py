@@ -9,6 +9,12 @@ once at the end).  Folding in chunks with a carried accumulator performs the
 same additions in the same order, so the result is bit-identical to one
 fa_fedavg_f32 over all rows (tests/test_gpu_parity.py checks this).
 
+Rows whose layers already sit in page-locked memory (a pinned result store,
+fedlesscan_amd.pinned) skip the packing copy: each layer is DMA'd from where it
+lies straight into its row of the device chunk (fa_copy_h2d on the copy
+stream), as soon as the row is added.  Other rows are packed with fa_pack and
+copied in runs of consecutive packed rows.
+
 Memory: 2 pinned + 2 device chunks of chunk_rows x P floats and one [P]
 accumulator, independent of the number of clients.
 """
@@ -33,8 +39,11 @@ class StreamingFold:
     has a score or none does.
     """
 
+    # process-wide row counts by ingest route (diagnostics; tests check the route)
+    stats = {"direct_rows": 0, "packed_rows": 0}
+
     def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
-                 pitch_align: int = 64):
+                 pitch_align: int = 64, direct: bool = True):
         if P <= 0:
             raise InvalidParameterShapeError("StreamingFold needs P > 0")
         self.P = P
@@ -59,6 +68,11 @@ class StreamingFold:
         self.rows = 0
         # per chunk: source layers and their byte offsets inside the pinned chunk
         self.srcs: List = [[], []]
+        # per chunk: which rows were DMA'd directly, and the arrays those copies read
+        self.row_direct: List = [[], []]
+        self.keep: List = [[], []]
+        self.direct = direct
+        self.direct_rows = 0
         self.threads = int(os.environ.get("FEDAVG_COPY_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
     # -- producer side ------------------------------------------------------
@@ -68,6 +82,7 @@ class StreamingFold:
         if self.fold_pending[b]:
             self.fold_done[b].synchronize()
             self.fold_pending[b] = False
+        self.keep[b] = []  # their direct copies finished before that fold ran
 
     def add(self, row, weight, score: Optional[float] = None):
         if self.scored is None:
@@ -80,14 +95,29 @@ class StreamingFold:
         pieces = row if isinstance(row, (list, tuple)) else [row]
         base = self.fill * self.ldx * 4
         total = 0
+        arrs = []
         for layer in pieces:
             arr = np.ascontiguousarray(layer)
             if arr.dtype != np.float32:
                 raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {arr.dtype}")
-            self.srcs[b].append((arr, base + 4 * total))
+            arrs.append((arr, base + 4 * total))
             total += arr.size
         if total != self.P:
             raise InvalidParameterShapeError(f"row has {total} parameters, expected {self.P}")
+        L = _lib.load()
+        if self.direct and all(L.fa_host_is_pinned(a.ctypes.data, a.nbytes) for a, _ in arrs if a.nbytes):
+            dst = self.devbuf[b].data_ptr()
+            cs = self.copy_stream.cuda_stream
+            for a, off in arrs:
+                _lib.check(L.fa_copy_h2d(dst + off, a.ctypes.data, a.nbytes, cs), "fa_copy_h2d")
+            self.keep[b].extend(a for a, _ in arrs)
+            self.row_direct[b].append(True)
+            self.direct_rows += 1
+            StreamingFold.stats["direct_rows"] += 1
+        else:
+            self.srcs[b].extend(arrs)
+            self.row_direct[b].append(False)
+            StreamingFold.stats["packed_rows"] += 1
         self.weights.append(weight)
         self.chunk_a[b].append(weight)
         self.chunk_s[b].append(score)
@@ -114,7 +144,17 @@ class StreamingFold:
         self._pack(b)  # every row of this chunk is in pinned memory before its H2D
         if n:
             with torch.cuda.stream(self.copy_stream):
-                self.devbuf[b][:n].copy_(self.host[b][:n], non_blocking=True)
+                direct = self.row_direct[b]
+                r = 0
+                while r < n:  # runs of packed rows; direct rows are already on their way
+                    if direct[r]:
+                        r += 1
+                        continue
+                    r1 = r + 1
+                    while r1 < n and not direct[r1]:
+                        r1 += 1
+                    self.devbuf[b][r:r1].copy_(self.host[b][r:r1], non_blocking=True)
+                    r = r1
                 self.h2d_done[b].record(self.copy_stream)
             self.compute.wait_event(self.h2d_done[b])
             a = torch.tensor(np.array([np.float32(w) for w in self.chunk_a[b]], np.float32)).to(
@@ -138,6 +178,7 @@ class StreamingFold:
             _lib.check(L.fa_fold_f32(None, 0, self.P, self.ldx, None, None, self.acc.data_ptr(), div, 1,
                                      self.acc.data_ptr(), st), "fa_fold_f32(finalize)")
         self.chunk_a[b], self.chunk_s[b] = [], []
+        self.row_direct[b] = []
         self.fill = 0
         self.buf ^= 1
 
@@ -146,6 +187,11 @@ class StreamingFold:
         if self.rows == 0:
             _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
         self._flush(finalize=True, total=total)
+        if self.keep[0] or self.keep[1]:
+            # direct copies read the callers' arrays: they must be done before
+            # the caller may free them
+            self.copy_stream.synchronize()
+            self.keep = [[], []]
         return self.acc
 
 

@@ -20,6 +20,9 @@ Each stored result is what GridFS holds in the reference: the BSON bytes of
 `result.dict()` (client_daos.py:73, 369), written by fedlesscan_amd.bsondoc.
 Loading parses them back (client_daos.py:142, 397); results come back with the
 NPZ blob as a zero-copy view into those bytes, so the ingest never copies it.
+With pinned=True the documents are written into page-locked memory
+(fedlesscan_amd.pinned, needs a GPU): the ingest then DMAs every layer straight
+from the document to the device, with no host-side packing copy.
 """
 from __future__ import annotations
 
@@ -36,15 +39,21 @@ class DocumentNotLoadedException(Exception):
 
 
 class InMemoryClientResultStore:
-    def __init__(self):
+    def __init__(self, pinned: bool = False):
         self._docs: List[dict] = []
-        self._files: Dict[int, bytes] = {}  # file_id -> BSON document (the GridFS file)
+        self._files: Dict[int, bytes] = {}  # file_id -> BSON document (the GridFS file; pinned: a memoryview)
+        self.pinned = pinned
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
 
     def save(self, session_id: str, round_id: int, client_id: str, result, overwrite: bool = True):
         # client_daos.py:55-56, 73: a ClientResult is dumped, a dict is stored as given
-        data = bsondoc.encode(result.model_dump() if isinstance(result, ClientResult) else result)
+        doc = result.model_dump() if isinstance(result, ClientResult) else result
+        if self.pinned:
+            from .pinned import pinned_bytes
+            data = bsondoc.encode_into(doc, pinned_bytes)
+        else:
+            data = bsondoc.encode(doc)
         with self._lock:
             key = (session_id, round_id, client_id)
             existing = next((d for d in self._docs

@@ -129,6 +129,20 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
 int fa_num_bf16_variants(void);
 const char* fa_bf16_variant_name(int variant);
 
+/* ---- host staging: page-locked documents and direct DMA ---------------------
+ * A result store that keeps documents in page-locked memory lets the ingest
+ * DMA each client's layers straight from the document into the device chunk,
+ * with no host-side packing copy (fedlesscan_amd/ingest.py, store.py).
+ *   fa_host_is_pinned: 1 if [p, p+n) lies inside ONE page-locked host
+ *     allocation known to the HIP runtime (hipHostMalloc, hipHostRegister,
+ *     torch pinned memory), else 0.  Never fails.
+ *   fa_host_alloc / fa_host_free: hipHostMalloc / hipHostFree.
+ *   fa_copy_h2d: hipMemcpyAsync host -> device of n bytes on stream. */
+int fa_host_is_pinned(const void* p, int64_t n);
+int fa_host_alloc(void** p, int64_t n);
+int fa_host_free(void* p);
+int fa_copy_h2d(void* dst, const void* src, int64_t n, void* stream);
+
 /* ---- host-side ingest (no GPU): NPZ wire format -> pinned staging ----------
  * Client blobs are uncompressed NPZ archives (NpzWeightsSerializer,
  * serialization.py:280-306, written by the client, client.py:186-199). */

@@ -302,15 +302,16 @@ def test_npz_views_match_np_load():
 # aggregator.  Plumbing checked against the reference-generated golden with the
 # oracle supplying the fold (the GPU version of this test is in test_gpu_parity).
 # ---------------------------------------------------------------------------
-def config1_round(strategy_name):
+def config1_round(strategy_name, pinned=False):
     """Store the 10 mnist-demo client results, run one MockAggregator round,
-    return (result, output shapes, sha256 of the flat output, golden entry)."""
+    return (result, output shapes, sha256 of the flat output, golden entry).
+    pinned=True keeps the stored documents in page-locked memory (GPU only)."""
     import hashlib
     from fedlesscan_amd.config import aggregator_settings
     from fedlesscan_amd.handler import MockAggregator
     m = G.manifest()["mnist_c1"]
     strategy, hp = aggregator_settings({"aggregator": {"hyperparams": {"tolerance": 2}}}, strategy_name)
-    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    st, ps = InMemoryClientResultStore(pinned=pinned), InMemoryParameterStore()
     params = G.parameters("mnist_c1")
     rounds = m["round_ids"] if strategy == AggregationStrategy.PER_SESSION else [m["current_round"]] * 10
     for i, (p, r) in enumerate(zip(params, rounds)):
