@@ -16,6 +16,7 @@ computed by libfedavg_hip.so on the GPU, or the call raises.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -236,7 +237,8 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
     return outs
 
 
-STREAM_CHUNK_BYTES = 128 << 20  # pinned staging per chunk (two chunks in flight)
+# pinned staging per chunk (two chunks in flight); FEDAVG_STREAM_CHUNK_MB overrides
+STREAM_CHUNK_BYTES = int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "256")) << 20
 
 
 def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:

@@ -51,6 +51,10 @@ class StreamingFold:
         self.ldx = ((P + pitch_align - 1) // pitch_align) * pitch_align
         self.R = max(1, chunk_rows)
         self.host = [torch.empty((self.R, self.ldx), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        # per-chunk factors [a; s] travel with the chunk's rows on the copy
+        # stream, from pinned memory (a pageable H2D could stall the producer)
+        self.fac_host = [torch.empty((2, self.R), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        self.fac_dev = [torch.empty((2, self.R), dtype=torch.float32, device=self.dev) for _ in range(2)]
         self.devbuf = [torch.empty((self.R, self.ldx), dtype=torch.float32, device=self.dev) for _ in range(2)]
         self.acc = torch.empty(P, dtype=torch.float32, device=self.dev)
         self.copy_stream = torch.cuda.Stream(device=self.dev)
@@ -155,14 +159,16 @@ class StreamingFold:
                         r1 += 1
                     self.devbuf[b][r:r1].copy_(self.host[b][r:r1], non_blocking=True)
                     r = r1
+                fh = self.fac_host[b].numpy()
+                fh[0, :n] = [np.float32(w) for w in self.chunk_a[b]]  # fl32(n_i), numpy's rounding
+                scored = self.chunk_s[b][0] is not None
+                if scored:
+                    fh[1, :n] = [np.float32(x) for x in self.chunk_s[b]]
+                self.fac_dev[b].copy_(self.fac_host[b], non_blocking=True)
                 self.h2d_done[b].record(self.copy_stream)
             self.compute.wait_event(self.h2d_done[b])
-            a = torch.tensor(np.array([np.float32(w) for w in self.chunk_a[b]], np.float32)).to(
-                self.dev, non_blocking=True)
-            s = None
-            if self.chunk_s[b][0] is not None:
-                s = torch.tensor(np.array([np.float32(x) for x in self.chunk_s[b]], np.float32)).to(
-                    self.dev, non_blocking=True)
+            a = self.fac_dev[b][0]
+            s = self.fac_dev[b][1] if scored else None
         div = float(np.float32(sum(self.weights) if total is None else total)) if finalize else 0.0
         L = _lib.load()
         st = self.compute.cuda_stream
