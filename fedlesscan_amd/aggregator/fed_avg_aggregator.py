@@ -59,6 +59,15 @@ def decode_results(results: Iterable[ClientResult], default_cardinality):
     return params, cards, metrics
 
 
+def decoded_rows(results: Iterable[ClientResult], default_cardinality, metrics: list):
+    """Lazy decode_results: yields (layers, cardinality), collects test metrics."""
+    for r in results:
+        p, c, m = decode_result(r, default_cardinality)
+        if m:
+            metrics.append(m)
+        yield p, c
+
+
 def chunked(items: Iterable, n: int) -> Iterator[list]:
     """Full chunks of n, then the remainder (fed_avg_aggregator.py:99-109)."""
     buf: list = []
@@ -89,8 +98,14 @@ class FedAvgAggregator(ParameterAggregator):
 
     def aggregate(self, client_results: Iterator[ClientResult], client_feats: Optional[List[dict]] = None,
                   default_cardinality: Optional[float] = None) -> Tuple[Parameters, Optional[List[TestMetrics]]]:
-        params, cards, metrics = decode_results(client_results, default_cardinality)
-        return self._aggregate(params, cards), (metrics or None)
+        if type(self)._aggregate is not FedAvgAggregator._aggregate:
+            # a subclass's own _aggregate gets the decoded lists, as in the reference
+            params, cards, metrics = decode_results(client_results, default_cardinality)
+            return self._aggregate(params, cards), (metrics or None)
+        metrics: list = []
+        out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
+                                       None, device=self.device)
+        return out, (metrics or None)
 
 
 class StreamFedAvgAggregator(FedAvgAggregator):

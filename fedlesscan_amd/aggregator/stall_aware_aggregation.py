@@ -21,7 +21,7 @@ import numpy as np
 from .. import engine
 from ..common.models import AggregationHyperParams, ClientResult, Parameters, TestMetrics
 from .exceptions import InsufficientClientResults
-from .fed_avg_aggregator import chunked, decode_results
+from .fed_avg_aggregator import chunked, decode_results, decoded_rows
 from .parameter_aggregator import ParameterAggregator
 
 
@@ -51,8 +51,13 @@ class StallAwareAggregator(ParameterAggregator):
 
     def aggregate(self, client_results: Iterator[ClientResult], client_feats: List[dict],
                   default_cardinality: Optional[float] = None) -> Tuple[Parameters, Optional[List[TestMetrics]]]:
-        params, cards, metrics = decode_results(client_results, default_cardinality)
-        return self._aggregate(client_feats, params, cards), (metrics or None)
+        if type(self)._aggregate is not StallAwareAggregator._aggregate:
+            params, cards, metrics = decode_results(client_results, default_cardinality)
+            return self._aggregate(client_feats, params, cards), (metrics or None)
+        metrics: list = []
+        out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
+                                       self._score_clients(client_feats), device=self.device)
+        return out, (metrics or None)
 
 
 class StreamStallAwareAggregator(StallAwareAggregator):

@@ -190,7 +190,11 @@ class ShardedAggregator:
             host[i] = row[lo:hi]
         X = torch.from_numpy(host).to(dev)
         full = self.aggregate(X, list(weights[:n]), None if scores is None else list(scores[:n]), P=P)
-        flat = full.cpu().numpy()
+        if full.is_cuda:
+            from . import engine
+            flat = engine.to_host(full)
+        else:
+            flat = full.numpy()
         outs, off = [], 0
         for shp, sz in zip(shapes, sizes):
             outs.append(flat[off:off + sz].reshape(shp))

@@ -111,3 +111,59 @@ def test_pinned_bson_documents_round_trip(dev):
     blob = cr["parameters"]["blob"]
     assert isinstance(blob, memoryview) and bytes(blob) == d["parameters"]["blob"]
     assert is_pinned(np.frombuffer(blob, np.uint8).ctypes.data, len(blob))
+
+
+def _rows(N, P, seed, shapes=((10, 10), (7,), None)):
+    X = synth.clients_f32(seed, N, 0, P)
+    out = []
+    for i in range(N):
+        r, layers, off = X[i], [], 0
+        for shp in shapes:
+            n = int(np.prod(shp)) if shp else P - off
+            layers.append(r[off:off + n].reshape(shp) if shp else r[off:off + n])
+            off += n
+        out.append(layers)
+    return out
+
+
+def _same_outputs(a, b):
+    return len(a) == len(b) and all(x.shape == y.shape and x.dtype == y.dtype and G.same_bits(x, y)
+                                    for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("case", ["plain", "scored", "short_scores", "f64_weight_late", "f64_layer_late",
+                                  "ragged_beyond_scores", "int_layers", "one_row"])
+def test_aggregate_decoded_equals_materialised(dev, case):
+    """The overlapped decode+fold entry gives exactly what aggregate_layers gives
+    on the materialised lists, including every fallback."""
+    from fedlesscan_amd import engine
+    N, P = 13, 2200
+    rows = _rows(N, P, 31)
+    w = list(synth.cardinalities(31, N))
+    sc = [(r + 1) / 11 for r in synth.round_ids(31, N, 10, 2)]
+    scores = None
+    if case == "scored":
+        scores = sc
+    elif case == "short_scores":
+        scores = sc[:5]
+    elif case == "f64_weight_late":
+        w[7] = np.float64(w[7])  # a strong scalar: numpy promotes the whole fold to float64
+    elif case == "f64_layer_late":
+        rows[6] = [x.astype(np.float64) for x in rows[6]]
+    elif case == "ragged_beyond_scores":
+        scores = sc[:4]
+        rows[9] = rows[9][:2]  # never folded (zip truncation), only its weight counts
+    elif case == "int_layers":
+        rows = [[(x * 100).astype(np.int32) for x in r] for r in rows]
+    elif case == "one_row":
+        rows, w = rows[:1], w[:1]
+    if case == "f64_layer_late":
+        from fedlesscan_amd.aggregator.exceptions import InvalidParameterShapeError
+        with pytest.raises(InvalidParameterShapeError):
+            engine.aggregate_layers(rows, w, scores, device=dev)
+        with pytest.raises(InvalidParameterShapeError):
+            engine.aggregate_decoded(iter(list(zip(rows, w))), scores, device=dev)
+        return
+    exp = engine.aggregate_layers(rows, w, scores, device=dev)
+    got = engine.aggregate_decoded(iter(list(zip(rows, w))), scores, device=dev)
+    assert _same_outputs(got, exp)

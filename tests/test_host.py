@@ -191,7 +191,14 @@ def oracle_fold(monkeypatch):
         if scores is None:
             return O.fedavg_literal(parameters[:n], list(weights))
         return _stall(parameters[:n], list(weights), list(scores))
+    def fake_decoded(items, scores=None, device=None):
+        rows, ws = [], []
+        for layers, w in items:
+            rows.append(layers)
+            ws.append(w)
+        return fake(rows, ws, scores) if rows else []
     monkeypatch.setattr(engine, "aggregate_layers", fake)
+    monkeypatch.setattr(engine, "aggregate_decoded", fake_decoded)
 
 
 def _stall(params, weights, scores):
