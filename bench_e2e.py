@@ -19,8 +19,9 @@ document per client in the (in-memory) result store, as GridFS holds them
 (client_daos.py:73).  gpu_e2e then includes the store read and the native BSON
 walk (blob stays a view); cpu_ref includes pymongo's bson.decode (the
 reference's own codec, client_daos.py:142) before the np.load + numpy fold.
---pinned-store keeps those documents in page-locked memory: the ingest then
-DMAs every layer straight from its document, with no packing copy.
+--pinned-store keeps those documents in page-locked memory and turns on the
+direct route: the ingest DMAs every layer straight from its document, with no
+packing copy (engine.DIRECT_DMA).
 
 Rates are input bytes (N * P * 4) per second.  Results are compared bit for bit.
 Writes one JSON line (rank 0, one GPU).  Not the headline metric: DESIGN.md.
@@ -89,6 +90,9 @@ def main():
     torch.cuda.set_device(dev)
 
     store = None
+    if a.pinned_store:
+        from fedlesscan_amd import engine
+        engine.DIRECT_DMA = True
     if a.bson or a.pinned_store:
         from fedlesscan_amd.store import InMemoryClientResultStore
         store = InMemoryClientResultStore(pinned=a.pinned_store)

@@ -9,11 +9,14 @@ once at the end).  Folding in chunks with a carried accumulator performs the
 same additions in the same order, so the result is bit-identical to one
 fa_fedavg_f32 over all rows (tests/test_gpu_parity.py checks this).
 
-Rows whose layers already sit in page-locked memory (a pinned result store,
-fedlesscan_amd.pinned) skip the packing copy: each layer is DMA'd from where it
-lies straight into its row of the device chunk (fa_copy_h2d on the copy
-stream), as soon as the row is added.  Other rows are packed with fa_pack and
-copied in runs of consecutive packed rows.
+With direct=True, rows whose layers already sit in page-locked memory (a
+pinned result store, fedlesscan_amd.pinned) skip the packing copy: each layer
+is DMA'd from where it lies straight into its row of the device chunk
+(fa_copy_h2d on the copy stream), as soon as the row is added.  Other rows are
+packed with fa_pack and copied in runs of consecutive packed rows.  It is off
+by default: on MI355X hosts the 16-thread pack fully overlaps the DMA, and one
+copy per chunk beat one copy per layer; it pays where host memcpy
+bandwidth, not PCIe, is the limit.
 
 Memory: 2 pinned + 2 device chunks of chunk_rows x P floats and one [P]
 accumulator, independent of the number of clients.
@@ -43,7 +46,7 @@ class StreamingFold:
     stats = {"direct_rows": 0, "packed_rows": 0}
 
     def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
-                 pitch_align: int = 64, direct: bool = True):
+                 pitch_align: int = 64, direct: bool = False):
         if P <= 0:
             raise InvalidParameterShapeError("StreamingFold needs P > 0")
         self.P = P

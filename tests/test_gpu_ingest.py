@@ -56,7 +56,7 @@ def test_direct_and_packed_rows_mix(dev, chunk_rows, pattern, scored):
         else:
             rows.append(X[i].copy())
     before = dict(StreamingFold.stats)
-    sf = StreamingFold(P, chunk_rows=chunk_rows, device=dev)
+    sf = StreamingFold(P, chunk_rows=chunk_rows, device=dev, direct=True)
     sf.acc.fill_(float("nan"))
     for i in range(N):
         r = rows[i]
@@ -87,11 +87,13 @@ def test_direct_off_packs_everything(dev):
 
 
 @pytest.mark.parametrize("strategy_name", ["fedlesscan", "fedavg"])
-def test_config1_pinned_store_direct_route(dev, strategy_name):
-    """BASELINE config 1 through a pinned result store: every client row takes
-    the direct DMA route, and the round is bit-exact against the reference's
-    golden output."""
+def test_config1_pinned_store_direct_route(dev, strategy_name, monkeypatch):
+    """BASELINE config 1 through a pinned result store with the direct DMA
+    route on: every client row takes it, and the round is bit-exact against the
+    reference's golden output."""
+    from fedlesscan_amd import engine
     from fedlesscan_amd.ingest import StreamingFold
+    monkeypatch.setattr(engine, "DIRECT_DMA", True)
     from test_host import config1_round
     before = StreamingFold.stats["direct_rows"]
     res, shapes, sha, exp = config1_round(strategy_name, pinned=True)
