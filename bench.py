@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=8)
     ap.add_argument("--clients", type=int, default=0, help="override the config's client count (experiments)")
     ap.add_argument("--params", type=int, default=0, help="override the config's parameter count (experiments)")
     ap.add_argument("--rounds", type=int, default=0,

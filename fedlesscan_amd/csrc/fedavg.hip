@@ -140,14 +140,13 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t n) {
     return x * q + (x < r ? x : r) + k;
 }
 
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false, bool NTS = false>
-__global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
-    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
-    const float* __restrict__ a, const float* __restrict__ s,
-    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+// One tile: C*kBlock quads of every client row (tile index bid).
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
+__device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__ X, int64_t N, int64_t P,
+                                          int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
+                                          const float* acc_in, float divisor, float* out) {
     const int64_t nq = P >> 2;
     const int64_t ldq = ldx >> 2;
-    const int64_t bid = XR ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t q0 = bid * (kBlock * C) + threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
     const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
@@ -182,6 +181,30 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
             out[col] = acc;
         }
     }
+}
+
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false, bool NTS = false>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    const int64_t bid = XR ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    fold_tile<U, C, NT, SCORED, ACC, FIN, NTS>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+}
+
+// Grid-stride form: a small grid (about one block per CU) walks the tiles in
+// order, tile = blockIdx.x + k*gridDim.x, so at any moment the running blocks
+// stream ADJACENT column tiles of the same client rows (one contiguous band,
+// rows visited in near lock-step) and each block streams many rows per tile.
+// On MI355X this reads HBM faster than one block per tile with several
+// resident per CU.
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_gs(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t ntiles) {  // acc_in may alias out
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
+        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
 
 // Balanced persistent form: the grid is the resident capacity (occupancy x
@@ -219,6 +242,152 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_balanced(
             for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
             if constexpr (FIN) acc = acc / divisor;
             out[col] = acc;
+        }
+    }
+}
+
+// Narrow models: LDS-staged client rows.
+//   When P is small (a few hundred thousand parameters: the MNIST CNN, the
+//   speech CNN, a 1M-param bucket), one lane per quad gives too few lanes to
+//   keep enough bytes in flight on 256 CUs.  Here a block owns only TQ quads
+//   (TQ*16 B of every client row) and ALL its NW waves load: each chunk of R
+//   client rows is read with R*TQ/(NW*64) independent 16-byte loads per lane
+//   and parked in LDS; wave 0 then folds the chunk from LDS in client order
+//   (lane = one quad) while the next chunk's loads are already in flight.  The
+//   adds stay one lane per column, strictly in row order: bit-identical to
+//   every other fold.  The partial quad of the P%4 tail columns is staged
+//   like a full one (element loads, zero-filled) and only its real columns
+//   are stored.  Per-chunk factors a[], s[] are staged in LDS too.
+template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    constexpr int NT = NW * 64;
+    constexpr int LQ = R * TQ / NT;  // quads each thread loads per chunk
+    static_assert(TQ <= 64 && (R * TQ) % NT == 0 && R <= NT, "tile shape");
+    __shared__ f32x4 tile[R * TQ];
+    __shared__ float fa[R], fs[SCORED ? R : 1];
+    const int64_t nq = P >> 2;
+    const int64_t nqa = (P + 3) >> 2;  // quads incl. the partial tail quad
+    const int64_t q0 = (int64_t)blockIdx.x * TQ;
+    const int tq = (int)((nqa - q0) < TQ ? (nqa - q0) : TQ);
+    const int64_t ldq = ldx >> 2;
+    const int t = threadIdx.x;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    f32x4 v[LQ];
+    float fv = 0.f, sv = 0.f;
+    // Interior blocks (TQ full quads) stream their full chunks through a loop
+    // whose loads carry no checks and no control flow: a branch between a
+    // load and its use (the tail-quad loop, or a join with a checked path)
+    // makes the compiler wait for the load right after issuing it, which
+    // would serialise the chunk loads with the fold.  The last block and the
+    // last partial chunk take the checked path, outside that loop.
+    auto load_full = [&](int64_t c) {  // chunk c: rows [c*R, c*R + R), every quad in range
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int e = t + j * NT;
+            v[j] = __builtin_nontemporal_load(X4 + (c * R + e / TQ) * ldq + q0 + e % TQ);
+        }
+        if (t < R) {
+            fv = a[c * R + t];
+            if constexpr (SCORED) sv = s[c * R + t];
+        }
+    };
+    auto load_checked = [&](int64_t c) {
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int e = t + j * NT, r = e / TQ, qq = e % TQ;
+            const int64_t row = c * R + r, q = q0 + qq;
+            if (row < N && qq < tq) {
+                if (q < nq) {
+                    v[j] = __builtin_nontemporal_load(X4 + row * ldq + q);
+                } else {  // partial tail quad: P%4 real columns
+                    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+                    for (int k = 0; k < (int)(P & 3); ++k) x[k] = X[row * ldx + q * 4 + k];
+                    v[j] = x;
+                }
+            }
+        }
+        if (t < R && c * R + t < N) {
+            fv = a[c * R + t];
+            if constexpr (SCORED) sv = s[c * R + t];
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) tile[t + j * NT] = v[j];
+        if (t < R) {
+            fa[t] = fv;
+            if constexpr (SCORED) fs[t] = sv;
+        }
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (ACC) {
+        if (t < tq) {
+            const int64_t q = q0 + t;
+            if (q < nq) {
+                acc = reinterpret_cast<const f32x4*>(acc_in)[q];
+            } else {
+                for (int k = 0; k < (int)(P & 3); ++k) acc[k] = acc_in[q * 4 + k];
+            }
+        }
+    }
+    // fold the staged chunk c (rows valid rows) in client order, lane = quad
+    auto fold = [&](int64_t c, int rows) {
+        if (t < tq) {
+            int r = 0;
+            if (!ACC && c == 0) {
+                acc = term4<SCORED>(tile[t], fa[0], SCORED ? fs[0] : 1.0f);
+                r = 1;
+            }
+            // 8 LDS reads in flight ahead of the ordered adds (the reads are
+            // independent, only the adds are ordered)
+            for (; r + 8 <= rows; r += 8) {
+                f32x4 x[8];
+                float f[8], g[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    x[k] = tile[(r + k) * TQ + t];
+                    f[k] = fa[r + k];
+                    g[k] = SCORED ? fs[r + k] : 1.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc = add4(acc, term4<SCORED>(x[k], f[k], g[k]));
+            }
+            for (; r < rows; ++r) acc = add4(acc, term4<SCORED>(tile[r * TQ + t], fa[r], SCORED ? fs[r] : 1.0f));
+        }
+    };
+    const bool interior = q0 + TQ <= nq;
+    const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
+    if (nfull > 0) {
+        load_full(0);
+        stash();
+        __syncthreads();
+        for (int64_t c = 0; c + 1 < nfull; ++c) {
+            load_full(c + 1);  // in flight while wave 0 folds chunk c
+            fold(c, R);
+            __syncthreads();  // chunk c consumed
+            stash();
+            __syncthreads();  // chunk c+1 staged
+        }
+        fold(nfull - 1, R);
+        __syncthreads();
+    }
+    for (int64_t c = nfull; c * R < N; ++c) {  // the rest, checked (no overlap)
+        load_checked(c);
+        stash();
+        __syncthreads();
+        fold(c, (N - c * R) < R ? (int)(N - c * R) : R);
+        __syncthreads();
+    }
+    if (t < tq) {
+        const f32x4 res = FIN ? div4(acc, divisor) : acc;
+        const int64_t q = q0 + t;
+        if (q < nq) {
+            __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q);
+        } else {
+            for (int k = 0; k < (int)(P & 3); ++k) out[q * 4 + k] = res[k];
         }
     }
 }
@@ -591,7 +760,7 @@ struct F32Variant {
 };
 // variant 0 is the shipped default (chosen from the on-device sweep)
 constexpr F32Variant kVariants[] = {
-    {"auto", 0, 0, true},  // C from the launch size (pick_quads); U=8 at C=4, else U=4; nt stores
+    {"auto", 0, 0, true},  // pick_f32(N, P)
     {"u4c4nt", 4, 4, true}, {"u8c1nt", 8, 1, true}, {"u16c1", 16, 1, false}, {"u4c1nt", 4, 1, true},
     {"u8c2nt", 8, 2, true}, {"u16c1nt", 16, 1, true}, {"u16c2nt", 16, 2, true}, {"u2c8nt", 2, 8, true},
     {"u4c2nt", 4, 2, true}, {"u2c4nt", 2, 4, true},
@@ -603,18 +772,46 @@ constexpr F32Variant kVariants[] = {
     {"xcd_u8c4nt", 8, 4, true}, {"xcd_u4c1nt", 4, 1, true},
     // non-temporal output stores
     {"u8c4nt_nts", 8, 4, true}, {"xcd_u8c4nt_nts", 8, 4, true},
+    // LDS-staged narrow fold (k_fold_f32_lds): lds_w<waves>r<rows per chunk>t<quads per block>
+    {"lds_w16r128t64", 0, 0, true}, {"lds_w8r64t64", 0, 0, true}, {"lds_w4r64t64", 0, 0, true},
+    {"lds_w8r128t32", 0, 0, true}, {"lds_w8r64t32", 0, 0, true}, {"lds_w16r64t64", 0, 0, true},
+    {"lds_w4r128t32", 0, 0, true}, {"lds_w8r128t64", 0, 0, true}, {"lds_w4r64t32", 0, 0, true},
+    {"lds_w8r96t32", 0, 0, true},
+    // grid-stride over tiles, gs<k> = k blocks per CU; _nts = non-temporal output stores
+    {"gs1_u8c4nt_nts", 8, 4, true}, {"gs1_u4c4nt_nts", 4, 4, true}, {"gs2_u8c4nt_nts", 8, 4, true},
+    {"gs1_u2c4nt", 2, 4, true}, {"gs1_u8c4nt", 8, 4, true}, {"gs1_u4c4nt", 4, 4, true},
+    {"gs2_u4c4nt", 4, 4, true}, {"gs1_u8c2nt", 8, 2, true}, {"gs4_u4c4nt", 4, 4, true},
+    {"gs1_u2c8nt_nts", 2, 8, true}, {"gs1_u4c8nt_nts", 4, 8, true}, {"gs1_u2c16nt_nts", 2, 16, true},
+    {"gs1_u1c16nt_nts", 1, 16, true}, {"v4_pickq_nts", 0, 0, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-// Quads per lane for the "auto" variant: the widest per-block row run
-// (C * 4 KiB) that still leaves >= ~1000 blocks in the launch, i.e. about one
-// full wave of resident blocks (measured on MI355X, DESIGN.md 5: 10M columns
-// -> C=4, 2.5M -> C=2, 1M -> C=1; C=8 and persistent grids were slower).
+// Quads per lane of the round-1 row-streaming policy (kept as variant
+// "v4_pickq_nts" for comparison): the widest per-block row run (C * 4 KiB)
+// that still leaves >= ~1000 blocks in the launch.
 inline int pick_quads(int64_t P) {
     const int64_t nq = P >> 2;
     if (nq / (4 * kBlock) >= 1000) return 4;
     if (nq / (2 * kBlock) >= 1000) return 2;
     return 1;
+}
+
+// The "auto" fp32 fold, from interleaved variant sweeps over model sizes x
+// client counts on MI355X (profiles/r01_sweep_shapes.log):
+//   P < 256K params           LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
+//                             (one lane per quad cannot fill the chip: 2.4x)
+//   N < 256 clients, P < 4M   one quad per lane, 4 rows ahead, plain stores
+//   N >= 256, P < 2M          grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
+//   N >= 256, P in [2M, 8M)   LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   otherwise (C3, C5)        grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
+enum class F32Pick { kLdsW4, kLdsW8, kU4C1, kGs1U8C4 };
+inline F32Pick pick_f32(int64_t N, int64_t P) {
+    const int64_t nq = P >> 2;
+    if (nq < (1 << 16)) return F32Pick::kLdsW4;
+    if (N < 256) return nq < (1 << 20) ? F32Pick::kU4C1 : F32Pick::kGs1U8C4;
+    if (nq < (1 << 19)) return F32Pick::kGs1U8C4;
+    if (nq < (1 << 21)) return F32Pick::kLdsW8;
+    return F32Pick::kGs1U8C4;
 }
 constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
                                          "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4"};
@@ -662,6 +859,44 @@ void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
 }
 
+// Compute units of the current device (cached per device).
+int cu_count() {
+    static thread_local int cache[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cache[dev] > 0) return cache[dev];
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    cache[dev] = cus;
+    return cus;
+}
+
+// Grid-stride fold: grid = min(tiles, per_cu x CUs).
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool NTS>
+void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+               const float* s, const float* acc_in, float d, float* out) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;  // incl. the column-tail lane
+    int64_t grid = (int64_t)per_cu * cu_count();
+    if (grid > tiles) grid = tiles;
+    hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS>), dim3((unsigned)grid), dim3(kBlock), 0, st, X,
+                       N, P, ldx, a, s, acc_in, d, out, tiles);
+}
+
+template <int U, int C, bool NTS>
+void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+#define FA_G(SC, ACC, FIN) launch_gs<U, C, true, SC, ACC, FIN, NTS>(st, per_cu, X, N, P, ldx, a, s, acc_in, d, out)
+    if (sc) {
+        if (acc) { if (fin) FA_G(true, true, true); else FA_G(true, true, false); }
+        else     { if (fin) FA_G(true, false, true); else FA_G(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_G(false, true, true); else FA_G(false, true, false); }
+        else     { if (fin) FA_G(false, false, true); else FA_G(false, false, false); }
+    }
+#undef FA_G
+}
+
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false, bool NTS = false>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
@@ -694,6 +929,28 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
                    const float* s, const float* acc_in, float d, float* out) {
     hipLaunchKernelGGL((k_fold_f32_scalar<SC, ACC, FIN>), grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx,
                        a, s, acc_in, d, out);
+}
+
+// LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
+template <int NW, int R, int TQ>
+int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
+    if (blocks * NW * 64 > (int64_t)0xFFFFFFFF)  // work-items per launch dimension
+        return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
+    const dim3 grid((unsigned)blocks), block(NW * 64);
+#define FA_L(SC, ACC, FIN)                                                                                   \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN>), grid, block, 0, st, X, N, P, ldx, a, s, \
+                       acc_in, d, out)
+    if (sc) {
+        if (acc) { if (fin) FA_L(true, true, true); else FA_L(true, true, false); }
+        else     { if (fin) FA_L(true, false, true); else FA_L(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_L(false, true, true); else FA_L(false, true, false); }
+        else     { if (fin) FA_L(false, false, true); else FA_L(false, false, false); }
+    }
+#undef FA_L
+    return FA_OK;
 }
 
 int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
@@ -729,13 +986,18 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     launch_v4_flags<U, C, true, false, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VS(U, C, XR) \
     launch_v4_flags<U, C, true, false, XR, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VG(K, U, C, NTS) \
+    launch_gs_flags<U, C, NTS>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VL(NW, R, TQ) \
+    launch_lds_flags<NW, R, TQ>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+    int rc = FA_OK;
     switch (variant) {  // must match kVariants[]
-        case 0:  // auto: non-temporal loads AND stores (the block-end store of a plain
-                 // variant costs ~2 % of the fold)
-            switch (pick_quads(P)) {
-                case 4: FA_VS(8, 4, false); break;
-                case 2: FA_VS(4, 2, false); break;
-                default: FA_VS(4, 1, false); break;
+        case 0:  // auto (pick_f32)
+            switch (pick_f32(N, P)) {
+                case F32Pick::kLdsW4: rc = FA_VL(4, 64, 32); break;
+                case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
+                case F32Pick::kU4C1: FA_VF(4, 1, true); break;
+                default: FA_VG(1, 8, 4, true); break;
             }
             break;
         case 1: FA_VF(4, 4, true); break;
@@ -760,13 +1022,46 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 20: FA_VX(8, 4); break;
         case 21: FA_VX(4, 1); break;
         case 22: FA_VS(8, 4, false); break;
-        default: FA_VS(8, 4, true); break;
+        case 23: FA_VS(8, 4, true); break;
+        case 24: rc = FA_VL(16, 128, 64); break;
+        case 25: rc = FA_VL(8, 64, 64); break;
+        case 26: rc = FA_VL(4, 64, 64); break;
+        case 27: rc = FA_VL(8, 128, 32); break;
+        case 28: rc = FA_VL(8, 64, 32); break;
+        case 29: rc = FA_VL(16, 64, 64); break;
+        case 30: rc = FA_VL(4, 128, 32); break;
+        case 31: rc = FA_VL(8, 128, 64); break;
+        case 32: rc = FA_VL(4, 64, 32); break;
+        case 33: rc = FA_VL(8, 96, 32); break;
+        case 34: FA_VG(1, 8, 4, true); break;
+        case 35: FA_VG(1, 4, 4, true); break;
+        case 36: FA_VG(2, 8, 4, true); break;
+        case 37: FA_VG(1, 2, 4, false); break;
+        case 38: FA_VG(1, 8, 4, false); break;
+        case 39: FA_VG(1, 4, 4, false); break;
+        case 40: FA_VG(2, 4, 4, false); break;
+        case 41: FA_VG(1, 8, 2, false); break;
+        case 42: FA_VG(4, 4, 4, false); break;
+        case 43: FA_VG(1, 2, 8, true); break;
+        case 44: FA_VG(1, 4, 8, true); break;
+        case 45: FA_VG(1, 2, 16, true); break;
+        case 46: FA_VG(1, 1, 16, true); break;
+        default:  // v4_pickq_nts: the round-1 policy
+            switch (pick_quads(P)) {
+                case 4: FA_VS(8, 4, false); break;
+                case 2: FA_VS(4, 2, false); break;
+                default: FA_VS(4, 1, false); break;
+            }
+            break;
     }
 #undef FA_VF
 #undef FA_VB
 #undef FA_VX
 #undef FA_VS
-    return check_launch("k_fold_f32_v4");
+#undef FA_VL
+#undef FA_VG
+    if (rc) return rc;
+    return check_launch("fold_f32");
 }
 
 }  // namespace

@@ -477,6 +477,60 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
     assert _bits_equal(out.cpu().numpy(), exp)
 
 
+def _lds_variants(L):
+    return [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"lds_")]
+
+
+@pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
+@pytest.mark.parametrize("P", [1, 3, 4, 255, 257, 4099, 16388])
+def test_lds_variants_chunk_and_tile_edges(dev, lib, N, P):
+    """The LDS-staged fold across its chunk (R rows) and tile (TQ quads)
+    boundaries and the partial tail quad: plain, stall-aware, and a chunked
+    continuation (acc carried, divide at the end), all bit-exact vs the oracle."""
+    L = lib.load()
+    X = torch.from_numpy(synth.clients_f32(700 + N, N, 0, P)).to(dev)
+    w = synth.cardinalities(700 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(700 + N, N, 10, 2)]
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Xh = X.cpu().numpy()
+    exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    variants = _lds_variants(L)
+    assert len(variants) >= 4
+    for v in variants:
+        for sp, e in ((None, exp), (s, exp_s)):
+            o = _sentinel(P, dev)
+            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+                                              None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v),
+                      "lds variant")
+            assert _bits_equal(o.cpu().numpy(), e), (L.fa_variant_name(v), N, P, sp is not None)
+
+
+@pytest.mark.parametrize("N,P", [(300, 10007), (1024, 67267)])
+def test_auto_fold_narrow_models(dev, lib, N, P):
+    """Narrow-model shapes through the default entry point and a 3-way chunked
+    continuation (the streaming-ingest call pattern)."""
+    L = lib.load()
+    X = torch.from_numpy(synth.clients_f32(800 + N, N, 0, P)).to(dev)
+    w = synth.cardinalities(800 + P, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
+    o = _sentinel(P, dev)
+    lib.check(L.fa_fedavg_f32(X.data_ptr(), N, P, P, a.data_ptr(), None, div, o.data_ptr(), st), "auto")
+    assert _bits_equal(o.cpu().numpy(), exp)
+    acc = _sentinel(P, dev)
+    cuts = [0, N // 3, N // 3 + 1, N]
+    for k, (r0, r1) in enumerate(zip(cuts[:-1], cuts[1:])):
+        lib.check(L.fa_fold_f32(X[r0].data_ptr(), r1 - r0, P, P, a[r0:].data_ptr(), None,
+                                None if k == 0 else acc.data_ptr(), div, int(r1 == N), acc.data_ptr(), st), "f")
+    assert _bits_equal(acc.cpu().numpy(), exp)
+
+
 @pytest.mark.parametrize("case,prefix", [("f32_small", "fedavg"), ("f32_small", "stall"), ("f32_n60", "fedavg"),
                                          ("n1", "fedavg"), ("f64_n40", "fedavg"), ("specials", "fedavg")])
 def test_device_tensor_inputs_match_golden(dev, case, prefix):
