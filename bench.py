@@ -233,8 +233,11 @@ def main():
         for _ in range(2):
             for v in range(nvar):
                 wl.launch(v)
+        order = list(range(nvar))
+        rng = np.random.default_rng(12345)
         for _ in range(max(args.steps, 5)):
-            for v in range(nvar):  # interleaved rounds in one process
+            rng.shuffle(order)  # a fresh order each round: no variant always runs first
+            for v in order:  # interleaved rounds in one process
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for k in range(rounds):

@@ -535,13 +535,12 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
 template <int U, int C, bool SCORED>
-__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
-    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
-    const float* __restrict__ a, const float* __restrict__ s, float divisor,
-    float* __restrict__ out, uint16_t* __restrict__ outb) {
+__device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
+                                          int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
+                                          float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
     const int64_t no = P >> 3;  // full octets
     const int64_t ldo = ldx >> 3;
-    const int64_t o0 = (int64_t)blockIdx.x * (kBlock * C) + threadIdx.x;
+    const int64_t o0 = bid * (kBlock * C) + threadIdx.x;
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
     if (o0 + (int64_t)(C - 1) * kBlock < no) {
         fold_octets<U, C, SCORED>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
@@ -553,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
         if (o < no) fold_octets<U, 1, SCORED>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
     const int64_t tb = no / (kBlock * C), tl = (no % (kBlock * C)) % kBlock;
-    if ((P & 7) && (int64_t)blockIdx.x == tb && (int64_t)threadIdx.x == tl) {
+    if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = no * 8; col < P; ++col) {
             float acc = term1<SCORED>(bf2f(X[col]), a[0], SCORED ? s[0] : 1.0f);
             for (int64_t i = 1; i < N; ++i)
@@ -563,6 +562,24 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
             if (outb) outb[col] = f2bf_rne(acc);
         }
     }
+}
+
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb) {
+    bf16_tile<U, C, SCORED>(blockIdx.x, X, N, P, ldx, a, s, divisor, out, outb);
+}
+
+// grid-stride over octet tiles, as k_fold_f32_gs
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_gs(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles) {
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
+        bf16_tile<U, C, SCORED>(bid, X, N, P, ldx, a, s, divisor, out, outb);
 }
 
 template <bool SCORED>
@@ -714,27 +731,29 @@ __global__ __launch_bounds__(kBlock) void k_synth(OutT* __restrict__ X, int64_t 
     }
 }
 
-// contiguous streaming read (calibration ceiling for the fold): grid-stride,
-// 8 independent 16-byte non-temporal loads in flight per lane.
+// Contiguous streaming read (calibration ceiling for the fold): block b reads
+// its own contiguous 64 KiB chunk (16 independent 16-byte non-temporal loads
+// per lane, all issued before the first use), the fastest pure-read pattern
+// measured on MI355X (tools/hbm_probe.hip "chunk nt 64 KiB/block").
+constexpr int kSweepQuads = 16 * kBlock;  // 64 KiB per block
 __global__ __launch_bounds__(kBlock) void k_read_sweep(const f32x4* __restrict__ X, int64_t nq,
-                                                        float* __restrict__ sink) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; q + 7 * stride < nq; q += 8 * stride) {
-        f32x4 v[8];
+                                                        float* __restrict__ sink, int64_t sink_len) {
+    const int64_t q0 = (int64_t)blockIdx.x * kSweepQuads + threadIdx.x;
+    f32x4 v[16];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(X + q + k * stride);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = add4(acc, v[k]);
+    for (int k = 0; k < 16; ++k) {
+        const int64_t q = q0 + (int64_t)k * kBlock;
+        v[k] = q < nq ? __builtin_nontemporal_load(X + q) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (; q < nq; q += stride) acc = add4(acc, __builtin_nontemporal_load(X + q));
+    f32x4 acc = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) acc = add4(acc, v[k]);
     float t = acc.x + acc.y + acc.z + acc.w;
     for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
     __shared__ float red[kBlock / 64];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
     __syncthreads();
-    if (threadIdx.x == 0) sink[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) sink[blockIdx.x % sink_len] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ---------------------------------------------------------------------------
@@ -783,6 +802,7 @@ constexpr F32Variant kVariants[] = {
     {"gs2_u4c4nt", 4, 4, true}, {"gs1_u8c2nt", 8, 2, true}, {"gs4_u4c4nt", 4, 4, true},
     {"gs1_u2c8nt_nts", 2, 8, true}, {"gs1_u4c8nt_nts", 4, 8, true}, {"gs1_u2c16nt_nts", 2, 16, true},
     {"gs1_u1c16nt_nts", 1, 16, true}, {"v4_pickq_nts", 0, 0, true},
+    {"gs1_u16c4nt_nts", 16, 4, true}, {"gs1_u16c2nt_nts", 16, 2, true}, {"gs1_u12c4nt_nts", 12, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -796,25 +816,24 @@ inline int pick_quads(int64_t P) {
     return 1;
 }
 
-// The "auto" fp32 fold, from interleaved variant sweeps over model sizes x
-// client counts on MI355X (profiles/r01_sweep_shapes.log):
-//   P < 256K params           LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
-//                             (one lane per quad cannot fill the chip: 2.4x)
-//   N < 256 clients, P < 4M   one quad per lane, 4 rows ahead, plain stores
-//   N >= 256, P < 2M          grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
-//   N >= 256, P in [2M, 8M)   LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
-//   otherwise (C3, C5)        grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
-enum class F32Pick { kLdsW4, kLdsW8, kU4C1, kGs1U8C4 };
+// The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
+// model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log):
+//   P < 256K params               LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
+//                                 (one lane per quad cannot fill the chip: 2-2.4x)
+//   N >= 256 and 2M <= P < 8M     LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   otherwise (C2, C3, C5, ...)   grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
+enum class F32Pick { kLdsW4, kLdsW8, kGs1U8C4 };
 inline F32Pick pick_f32(int64_t N, int64_t P) {
     const int64_t nq = P >> 2;
     if (nq < (1 << 16)) return F32Pick::kLdsW4;
-    if (N < 256) return nq < (1 << 20) ? F32Pick::kU4C1 : F32Pick::kGs1U8C4;
-    if (nq < (1 << 19)) return F32Pick::kGs1U8C4;
-    if (nq < (1 << 21)) return F32Pick::kLdsW8;
+    if (N >= 256 && nq >= (1 << 19) && nq < (1 << 21)) return F32Pick::kLdsW8;
     return F32Pick::kGs1U8C4;
 }
 constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
-                                         "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4"};
+                                         "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4",
+                                         // grid-stride, gs<k> = k blocks per CU
+                                         "bf16gs1u8c4", "bf16gs1u8c2", "bf16gs1u4c4", "bf16gs2u8c2",
+                                         "bf16gs1u16c2", "bf16gs2u4c4"};
 
 // bf16 "auto": octets per lane from the client count.  Sweeps on MI355X
 //  put the optimum near 8 MB per block (rows x C x 4 KiB):
@@ -996,7 +1015,6 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
             switch (pick_f32(N, P)) {
                 case F32Pick::kLdsW4: rc = FA_VL(4, 64, 32); break;
                 case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
-                case F32Pick::kU4C1: FA_VF(4, 1, true); break;
                 default: FA_VG(1, 8, 4, true); break;
             }
             break;
@@ -1046,13 +1064,17 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 44: FA_VG(1, 4, 8, true); break;
         case 45: FA_VG(1, 2, 16, true); break;
         case 46: FA_VG(1, 1, 16, true); break;
-        default:  // v4_pickq_nts: the round-1 policy
+        case 48: FA_VG(1, 16, 4, true); break;
+        case 49: FA_VG(1, 16, 2, true); break;
+        case 50: FA_VG(1, 12, 4, true); break;
+        case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
                 case 2: FA_VS(4, 2, false); break;
                 default: FA_VS(4, 1, false); break;
             }
             break;
+        default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
 #undef FA_VB
@@ -1141,8 +1163,27 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X,              \
                                N, P, ldx, a, s, divisor, out_f32, out_bf16);                               \
     }
+#define FA_BG(K, U, C)                                                                                     \
+    {                                                                                                      \
+        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);           \
+        const int64_t tiles = (units + per_block - 1) / per_block;                                         \
+        int64_t g = (int64_t)(K) * cu_count();                                                             \
+        if (g > tiles) g = tiles;                                                                          \
+        if (s)                                                                                             \
+            hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, X,  \
+                               N, P, ldx, a, s, divisor, out_f32, out_bf16, tiles);                        \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, X, \
+                               N, P, ldx, a, s, divisor, out_f32, out_bf16, tiles);                        \
+    }
         switch (variant) {  // must match kBf16Variants[]; 0 = default (on-device sweep)
             case 0:
+                // per-GPU C4 buckets (256 x 12.5M): grid-stride 8 rows x 2 octets, +7 %
+                // over the row-streaming pick; the full 100M model: pick_octets
+                if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
+                    FA_BG(1, 8, 2);
+                    break;
+                }
                 switch (pick_octets(N, P)) {
                     case 8: FA_BF(2, 8); break;
                     case 4: FA_BF(4, 4); break;
@@ -1157,9 +1198,16 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             case 5: FA_BF(1, 8); break;
             case 6: FA_BF(2, 8); break;
             case 7: FA_BF(1, 4); break;
-            default: FA_BF(2, 4); break;
+            case 8: FA_BF(2, 4); break;
+            case 9: FA_BG(1, 8, 4); break;
+            case 10: FA_BG(1, 8, 2); break;
+            case 11: FA_BG(1, 4, 4); break;
+            case 12: FA_BG(2, 8, 2); break;
+            case 13: FA_BG(1, 16, 2); break;
+            default: FA_BG(2, 4, 4); break;
         }
 #undef FA_BF
+#undef FA_BG
         return check_launch("k_fedavg_bf16_v8");
     }
     if (s)
@@ -1248,9 +1296,11 @@ int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream) {
     if (n < 0 || !X || !sink || sink_len <= 0 || !aligned16(X) || (n & 3))
         return fail(FA_ERR_ARG, "read sweep needs 16-B aligned X, n %% 4 == 0, sink_len > 0");
-    int64_t grid = sink_len < 65535 ? sink_len : 65535;
+    const int64_t nq = n >> 2, grid = (nq + kSweepQuads - 1) / kSweepQuads;
+    if (grid > 0x7FFFFFFF) return fail(FA_ERR_ARG, "read sweep too large");
+    if (grid == 0) { g_err[0] = 0; return FA_OK; }
     hipLaunchKernelGGL(k_read_sweep, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream,
-                       reinterpret_cast<const f32x4*>(X), n >> 2, sink);
+                       reinterpret_cast<const f32x4*>(X), nq, sink, sink_len);
     return check_launch("k_read_sweep");
 }
 

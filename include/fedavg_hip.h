@@ -111,8 +111,9 @@ int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t s
                  int64_t row0, int64_t col0, void* stream);
 int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
                   int64_t row0, int64_t col0, void* stream);
-/* Contiguous read-only sweep of n floats (16 B/lane) -> one partial per block
- * in sink[grid]: the streaming-read ceiling the fold is compared with. */
+/* Contiguous read-only sweep of n floats, one 64 KiB chunk per block (16 B
+ * per lane) -> one partial per block in sink[block % sink_len] (values are
+ * meaningless): the streaming-read ceiling the fold is compared with. */
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
 /* Tuning entry: fa_fedavg_f32 with an explicit kernel variant;
  * variant 0 = the default.  Returns FA_ERR_ARG for an unknown variant. */
