@@ -509,6 +509,26 @@ def test_lds_variants_chunk_and_tile_edges(dev, lib, N, P):
             assert _bits_equal(o.cpu().numpy(), e), (L.fa_variant_name(v), N, P, sp is not None)
 
 
+@pytest.mark.parametrize("N,P,pad", [(9, 1030, 2), (300, 65537, 63), (5, 300001, 3), (257, 2_100_003, 61),
+                                     (260, 300_000, 0)])
+@pytest.mark.parametrize("scored", [False, True])
+def test_auto_picks_with_row_pitch(dev, lib, N, P, pad, scored):
+    """Every kernel the auto policy picks (LDS-staged 4/8 waves, grid-stride),
+    on a 16-B aligned row pitch ldx > P, with the P % 4 tail columns."""
+    from fedlesscan_amd import engine
+    ldx = P + pad + (-(P + pad)) % 4
+    Xh = synth.clients_f32(900 + N, N, 0, P)
+    big = torch.zeros((N, ldx), dtype=torch.float32, device=dev)
+    big[:, :P] = torch.from_numpy(Xh).to(dev)
+    big[:, P:] = float("nan")  # the pitch padding must never be read
+    w = synth.cardinalities(900 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(900 + N, N, 10, 2)] if scored else None
+    got = engine.fold_stacked(big[:, :P], w, sc, out=_sentinel(P, dev)).cpu().numpy()
+    exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    assert _bits_equal(got, exp)
+
+
 @pytest.mark.parametrize("N,P", [(300, 10007), (1024, 67267)])
 def test_auto_fold_narrow_models(dev, lib, N, P):
     """Narrow-model shapes through the default entry point and a 3-way chunked
