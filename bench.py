@@ -330,7 +330,9 @@ def main():
     total_bytes = float(tb.item()) * args.steps
     value = total_bytes / elapsed / 1e9
     achieved = wl.bytes / (kern_avg * 1e-3) / 1e9
-    traffic, traffic_src = read_traffic(args.config)
+    # the committed PMC pass measured exactly this launch: the unmodified config, one fold per step
+    traffic, traffic_src = (read_traffic(args.config) if not (args.clients or args.params) and rounds == 1
+                            else (None, None))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
