@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
+    ap.add_argument("--splitn", action="store_true",
+                    help="time the opt-in split-client fold (fa_fedavg_f32_splitn, NOT bit-exact) instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=8)
@@ -142,7 +144,9 @@ class Workload:
         sub, W = self.layout.sub, self.layout.local_width
         x = self.X.data_ptr() + k * sub * self.X.element_size()
         o = self.out.data_ptr() + k * sub * 4
-        if self.dtype == "f32":
+        if self.dtype == "f32" and variant < 0:  # opt-in split-client fold
+            rc = L.fa_fedavg_f32_splitn(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st)
+        elif self.dtype == "f32":
             rc = L.fa_fedavg_f32_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st, variant)
         else:
             rc = L.fa_fedavg_bf16_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, None, st,
@@ -219,6 +223,8 @@ def main():
         cfg = (args.clients or cfg[0], args.params or cfg[1], *cfg[2:7],
                cfg[7] + f" [override: {args.clients or cfg[0]} clients x {args.params or cfg[1]} params]")
     rounds = args.rounds or (1 if world == 1 else 4)
+    if args.splitn:
+        args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds)
     L = _lib.load()
     lay = wl.layout
@@ -362,8 +368,8 @@ def main():
                 "parallelism": f"param-bucket x{world}" + (
                     f" + RCCL all_gather in {rounds} rounds overlapped with the fold" if world > 1 else ""),
                 "rounds": rounds,
-                "variant": (L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name)(
-                    args.variant).decode(),
+                "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
+                (L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name)(args.variant).decode(),
             },
             "roofline": {
                 "bound": "hbm",

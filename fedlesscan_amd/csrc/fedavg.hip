@@ -392,6 +392,85 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     }
 }
 
+// Split-client fold (opt-in, NOT bit-exact; fa_fedavg_f32_splitn).
+//   For models too narrow to fill the chip even with LDS staging, the
+//   clients of every column are cut into S = 4*NW contiguous slices.  A block
+//   owns 16 quads (64 columns); lane l of wave w folds quad l%16 over slice
+//   4*w + l/16, in client order, 8 rows ahead.  The S partial sums are then
+//   combined in a FIXED pairwise tree -- two wavefront shuffles (slice pairs,
+//   then pairs of pairs), then the waves' partials through LDS -- so the
+//   result is deterministic run to run, but it is a different association
+//   than the reference's left fold: it differs in the last bits (normwise
+//   error measured in tests/test_gpu_parity.py and DESIGN.md 5).
+template <int NW, bool SCORED>
+__global__ __launch_bounds__(NW * 64) void k_fold_f32_splitn(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor, float* __restrict__ out) {
+    constexpr int S = 4 * NW;  // client slices
+    constexpr int U = 8;
+    __shared__ f32x4 part[NW][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qq = lane & 15, slice = 4 * w + (lane >> 4);
+    const int64_t nq = P >> 2, q = (int64_t)blockIdx.x * 16 + qq;
+    const int64_t ns = (N + S - 1) / S;
+    const int64_t r0 = slice * ns < N ? slice * ns : N, r1 = r0 + ns < N ? r0 + ns : N;
+    const int64_t ldq = ldx >> 2;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if ((int64_t)blockIdx.x * 16 + 16 <= nq) {  // block-uniform: 16 full quads, no checks in the loop
+        const f32x4* p = reinterpret_cast<const f32x4*>(X) + q;
+        int64_t i = r0;
+        if (i < r1) {
+            acc = term4<SCORED>(__builtin_nontemporal_load(p + i * ldq), a[i], SCORED ? s[i] : 1.0f);
+            ++i;
+        }
+        for (; i + U <= r1; i += U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldq);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
+        }
+        for (; i < r1; ++i)
+            acc = add4(acc, term4<SCORED>(__builtin_nontemporal_load(p + i * ldq), a[i], SCORED ? s[i] : 1.0f));
+    } else if (q * 4 < P) {  // last block: full and partial quads, element loads
+        const int w4 = (P - q * 4) < 4 ? (int)(P - q * 4) : 4;
+        for (int64_t i = r0; i < r1; ++i) {
+            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < w4; ++k) x[k] = X[i * ldx + q * 4 + k];
+            const f32x4 t = term4<SCORED>(x, a[i], SCORED ? s[i] : 1.0f);
+            acc = i == r0 ? t : add4(acc, t);
+        }
+    }
+    // fixed tree: slice pairs (xor 16), pairs of pairs (xor 32); fp add is
+    // commutative, so both lanes of a pair hold the same bits
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+        f32x4 o;
+        o.x = __shfl_xor(acc.x, off);
+        o.y = __shfl_xor(acc.y, off);
+        o.z = __shfl_xor(acc.z, off);
+        o.w = __shfl_xor(acc.w, off);
+        acc = add4(acc, o);
+    }
+    if (lane < 16) part[w][qq] = acc;
+    __syncthreads();
+    if (w == 0 && lane < 16 && q * 4 < P) {
+        f32x4 t[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) t[k] = part[k][qq];
+#pragma unroll
+        for (int stride = 1; stride < NW; stride <<= 1)  // ((p0+p1)+(p2+p3))+...
+#pragma unroll
+            for (int k = 0; k + stride < NW; k += 2 * stride) t[k] = add4(t[k], t[k + stride]);
+        const f32x4 r = div4(t[0], divisor);
+        if (q < nq) {
+            __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(out) + q);
+        } else {
+            for (int k = 0; k < (int)(P & 3); ++k) out[q * 4 + k] = r[k];
+        }
+    }
+}
+
 // One column per lane, any alignment / stride (fallback for unaligned input).
 template <bool SCORED, bool ACC, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
@@ -1125,6 +1204,26 @@ int fa_accumulate_f32(float* acc, const float* x, float a, float s, int first, i
 
 int fa_finalize_f32(const float* acc, float divisor, float* out, int64_t P, void* stream) {
     return fold_f32(nullptr, 0, P, P, nullptr, nullptr, acc, divisor, 1, out, stream, 0);
+}
+
+int fa_fedavg_f32_splitn(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                         float divisor, float* out, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(X) || (ldx % 4) || !aligned16(out))
+        return fail(FA_ERR_ARG, "fa_fedavg_f32_splitn needs 16-B aligned X and out and ldx %% 4 == 0");
+    constexpr int NW = 8;
+    const int64_t blocks = (((P + 3) >> 2) + 15) / 16;
+    if (blocks > 0x7FFFFFFF / (NW * 64)) return fail(FA_ERR_ARG, "P too large for fa_fedavg_f32_splitn");
+    hipStream_t st = (hipStream_t)stream;
+    if (s)
+        hipLaunchKernelGGL((k_fold_f32_splitn<NW, true>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, X, N, P,
+                           ldx, a, s, divisor, out);
+    else
+        hipLaunchKernelGGL((k_fold_f32_splitn<NW, false>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, X, N, P,
+                           ldx, a, s, divisor, out);
+    return check_launch("k_fold_f32_splitn");
 }
 
 int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,

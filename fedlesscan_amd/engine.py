@@ -89,13 +89,17 @@ def _check_matrix(X: torch.Tensor) -> tuple[int, int, int]:
 
 
 def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] = None, *,
-                 out: Optional[torch.Tensor] = None, want_bf16: bool = False, total=None):
+                 out: Optional[torch.Tensor] = None, want_bf16: bool = False, total=None,
+                 exact: bool = True):
     """FedAvg (scores None) / stall-aware fold over the rows of X, in row order.
 
     `total` overrides the divisor sum (used when zip() truncated the rows but
     the reference still divides by the sum of every weight).  Returns `out`
     ([P] tensor in the result dtype); with bf16 input and want_bf16=True
-    returns (out_f32, out_bf16).
+    returns (out_f32, out_bf16).  exact=False (fp32 only) opts into the
+    split-client fold, fa_fedavg_f32_splitn: faster on very narrow models,
+    deterministic, but NOT bit-identical to the reference (a different
+    association of the same sum).
     """
     N, P, ldx = _check_matrix(X)
     if len(weights) != N or (scores is not None and len(scores) != N):
@@ -133,8 +137,11 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
     a, s = f.to(dev)
     out = out if out is not None else torch.empty(P, dtype=_NP_TO_TORCH[dt], device=dev)
     if dt == np.float32:
-        _lib.call("fa_fedavg_f32", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
-                  out.data_ptr(), st)
+        # the split-client kernel needs 16-B aligned rows; any other layout
+        # takes the exact fold, which is bit-identical to the reference
+        split = not exact and X.data_ptr() % 16 == 0 and ldx % 4 == 0 and out.data_ptr() % 16 == 0
+        name = "fa_fedavg_f32_splitn" if split else "fa_fedavg_f32"
+        _lib.call(name, X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), st)
     else:
         _lib.call("fa_fedavg_f64", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
                   out.data_ptr(), st)

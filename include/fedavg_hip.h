@@ -57,6 +57,17 @@ int fa_fedavg_f32(const float* X, int64_t N, int64_t P, int64_t ldx,
                   const float* a, const float* s, float divisor,
                   float* out, void* stream);
 
+/* OPT-IN, NOT BIT-EXACT.  The same weighted mean for models too narrow to
+ * fill the GPU (a few thousand to ~100K params): each column's clients are
+ * cut into 32 contiguous slices folded in order, and the partial sums are
+ * combined in a fixed pairwise tree (wavefront shuffles, then LDS).  Results
+ * are deterministic run to run but differ from the reference's left fold
+ * (fed_avg_aggregator.py:38-41) in the last bits: a different association
+ * of the same sum.  Needs 16-B aligned X and out, ldx % 4 == 0. */
+int fa_fedavg_f32_splitn(const float* X, int64_t N, int64_t P, int64_t ldx,
+                         const float* a, const float* s, float divisor,
+                         float* out, void* stream);
+
 /* Same fold over N separately allocated client rows: xi is a [device] array of
  * N [device] pointers, each to P floats (the list-of-arrays form the reference
  * passes: fed_avg_aggregator.py:32-35). */
