@@ -36,6 +36,7 @@ _PROTOS = {
     "fa_last_error": (ctypes.c_char_p, []),
     "fa_fedavg_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_ptrs": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
+    "fa_fedavg_f32_ptrs_aligned": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_splitn": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fold_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _f32, _int, _vp, _vp]),
     "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),

@@ -529,6 +529,75 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_f32_ptrs(
     }
 }
 
+// List-of-rows form with every row 16-B aligned (fa_fedavg_f32_ptrs_aligned):
+// the tile structure of the stacked fold (C quads per lane, U rows ahead) with
+// row i's base read from xi[i] (a wave-uniform scalar load).  No branch sits
+// between the loads and their use.
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void fold_quads_rows(const float* const* __restrict__ xi, int64_t q0, int64_t N,
+                                                const float* __restrict__ a, const float* __restrict__ s,
+                                                float divisor, f32x4* __restrict__ out) {
+    f32x4 acc[C];
+    {
+        const f32x4* r = reinterpret_cast<const f32x4*>(xi[0]) + q0;
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(__builtin_nontemporal_load(r + c * kBlock), a0, s0);
+    }
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const f32x4* r = reinterpret_cast<const f32x4*>(xi[i + u]) + q0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(v[u][c], ai, si));
+        }
+    }
+    for (; i < N; ++i) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(xi[i]) + q0;
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(__builtin_nontemporal_load(r + c * kBlock), ai, si));
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) __builtin_nontemporal_store(div4(acc[c], divisor), out + c * kBlock);
+}
+
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_rows_gs(
+    const float* const* __restrict__ xi, int64_t N, int64_t P, const float* __restrict__ a,
+    const float* __restrict__ s, float divisor, float* __restrict__ out, int64_t ntiles) {
+    const int64_t nq = P >> 2;
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+        const int64_t q0 = bid * (kBlock * C) + threadIdx.x;
+        if (q0 + (int64_t)(C - 1) * kBlock < nq) {
+            fold_quads_rows<U, C, SCORED>(xi, q0, N, a, s, divisor, O4 + q0);
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int64_t q = q0 + (int64_t)c * kBlock;
+                if (q < nq) fold_quads_rows<U, 1, SCORED>(xi, q, N, a, s, divisor, O4 + q);
+            }
+            const int64_t tb = nq / (kBlock * C), tl = (nq % (kBlock * C)) % kBlock;
+            if ((P & 3) && bid == tb && (int64_t)threadIdx.x == tl) {
+                for (int64_t col = nq * 4; col < P; ++col) {
+                    float acc = term1<SCORED>(xi[0][col], a[0], SCORED ? s[0] : 1.0f);
+                    for (int64_t i = 1; i < N; ++i) acc = acc + term1<SCORED>(xi[i][col], a[i], SCORED ? s[i] : 1.0f);
+                    out[col] = acc / divisor;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // bf16: 8 columns per lane (one 16-byte load per row), exact upcast, f32 fold.
 // ---------------------------------------------------------------------------
@@ -1224,6 +1293,33 @@ int fa_fedavg_f32_splitn(const float* X, int64_t N, int64_t P, int64_t ldx, cons
         hipLaunchKernelGGL((k_fold_f32_splitn<NW, false>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, X, N, P,
                            ldx, a, s, divisor, out);
     return check_launch("k_fold_f32_splitn");
+}
+
+int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                               float divisor, float* out, void* stream) {
+    int rc = check_common(N, P, P, xi, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(out)) return fail(FA_ERR_ARG, "fa_fedavg_f32_ptrs_aligned needs a 16-B aligned out");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
+#define FA_R(U, C, GRIDCAP)                                                                                    \
+    {                                                                                                          \
+        const int64_t tiles = (units + (int64_t)kBlock * (C) - 1) / ((int64_t)kBlock * (C));                   \
+        const int64_t g = (GRIDCAP) > 0 && tiles > (GRIDCAP) ? (GRIDCAP) : tiles;                              \
+        if (s)                                                                                                 \
+            hipLaunchKernelGGL((k_fold_f32_rows_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, xi, N, \
+                               P, a, s, divisor, out, tiles);                                                  \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_fold_f32_rows_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, xi,  \
+                               N, P, a, s, divisor, out, tiles);                                               \
+    }
+    // large models: ~one block per CU walking 16 KiB tiles (as the stacked
+    // default); narrow ones: one block per 4 KiB tile
+    if ((P >> 2) >= (int64_t)kBlock * 4 * cu_count()) FA_R(8, 4, (int64_t)cu_count())
+    else FA_R(8, 1, 0)
+#undef FA_R
+    return check_launch("k_fold_f32_rows_gs");
 }
 
 int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,

@@ -163,10 +163,12 @@ def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[
         return fold_stacked(torch.stack([r.reshape(-1) for r in rows]), weights, scores, out=out, total=total)
     f = Factors(weights, scores, np.dtype(np.float32), total=total)
     a, s = f.to(dev)
-    ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).to(dev)
+    host_ptrs = np.fromiter((r.data_ptr() for r in rows), dtype=np.int64, count=N)
+    ptrs = torch.from_numpy(host_ptrs).to(dev)
     out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
-    _lib.call("fa_fedavg_f32_ptrs", ptrs.data_ptr(), N, P, a.data_ptr(), _ptr(s), float(f.div),
-              out.data_ptr(), stream_ptr(dev))
+    aligned = not (host_ptrs % 16).any() and out.data_ptr() % 16 == 0
+    _lib.call("fa_fedavg_f32_ptrs_aligned" if aligned else "fa_fedavg_f32_ptrs", ptrs.data_ptr(), N, P,
+              a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), stream_ptr(dev))
     # `ptrs` may be freed on return: the caching allocator reuses it only in
     # stream order, i.e. after this kernel has read it.
     return out

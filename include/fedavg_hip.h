@@ -74,6 +74,11 @@ int fa_fedavg_f32_splitn(const float* X, int64_t N, int64_t P, int64_t ldx,
 int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P,
                        const float* a, const float* s, float divisor,
                        float* out, void* stream);
+/* The same with every row promised 16-B aligned by the caller (and out 16-B
+ * aligned): the tiled, grid-stride schedule of the stacked fold. */
+int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P,
+                               const float* a, const float* s, float divisor,
+                               float* out, void* stream);
 
 /* Chunked fold, the building block of streaming ingest
  * (StreamFedAvgAggregator.aggregate, fed_avg_aggregator.py:111-153):

@@ -224,6 +224,24 @@ def test_ptr_rows_equal_stacked(dev):
         assert _bits_equal(got, exp)
 
 
+@pytest.mark.parametrize("N,P", [(1, 1), (3, 5), (23, 4099), (9, 1024 * 256 + 6), (5, 4 * 1024 * 256 + 3),
+                                 (17, 4 * 1024 * 256 * 2 + 1)])
+@pytest.mark.parametrize("scored", [False, True])
+def test_aligned_ptr_rows(dev, N, P, scored):
+    """fa_fedavg_f32_ptrs_aligned (every row 16-B aligned): both launch shapes
+    (one block per 4 KiB tile, grid-stride 16 KiB tiles) and the column tail."""
+    from fedlesscan_amd import engine
+    X = synth.clients_f32(61 + N, N, 0, P)
+    w = synth.cardinalities(61 + P, N)
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]
+    assert all(r.data_ptr() % 16 == 0 for r in rows)
+    sc = [(r + 1) / 11 for r in synth.round_ids(61, N, 10, 2)] if scored else None
+    got = engine.fold_rows(rows, w, sc, out=_sentinel(P, dev)).cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    assert _bits_equal(got, exp)
+
+
 @pytest.mark.parametrize("N,P", [(1, 8), (5, 9), (64, 8 * 1000 + 3), (256, 65536)])
 @pytest.mark.parametrize("scored", [False, True])
 def test_bf16_matches_definition(dev, N, P, scored):

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Pointer-list fold (fa_fedavg_f32_ptrs: N separately allocated client rows)
+against the stacked fold on the same values.
+
+    python tools/ptrs_bench.py [--clients N] [--params P]   (GPU box) -> one JSON line
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedlesscan_amd import _lib, engine, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--clients", type=int, default=1024)
+ap.add_argument("--params", type=int, default=1_000_000)
+ap.add_argument("--reps", type=int, default=20)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+N, P = args.clients, args.params
+L = _lib.load()
+st = torch.cuda.current_stream(dev).cuda_stream
+X = torch.empty((N, P), dtype=torch.float32, device=dev)
+_lib.check(L.fa_synth_f32(X.data_ptr(), N, P, P, 9, 0, 0, st), "synth")
+rows = [X[i].clone() for i in range(N)]  # separate allocations
+w = synth.cardinalities(9, N)
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(args.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return sorted(ts)[len(ts) // 2]
+
+
+t_rows = timed(lambda: engine.fold_rows(rows, w))
+# the kernel alone: pointer table and factors built once, as a caller that
+# keeps its client tensors would
+import numpy as np  # noqa: E402
+ptr_tab = torch.from_numpy(np.array([r.data_ptr() for r in rows], dtype=np.int64)).to(dev)
+a_dev = torch.tensor([float(np.float32(x)) for x in w], dtype=torch.float32, device=dev)
+out = torch.empty(P, dtype=torch.float32, device=dev)
+div = float(np.float32(sum(w)))
+t_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), None,
+                                                               div, out.data_ptr(), st), "ptrs"))
+t_stack = timed(lambda: engine.fold_stacked(X, w))
+same = torch.equal(engine.fold_rows(rows, w).view(torch.int32), engine.fold_stacked(X, w).view(torch.int32))
+gb = (N * P * 4 + P * 4) / 1e9
+print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_GBps": round(gb / t_rows * 1e3, 1),
+                  "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
+                  "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
+                  "bit_identical": bool(same)}))
