@@ -73,7 +73,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=100)
     ap.add_argument("--params", type=int, default=1_000_000)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--bson", action="store_true", help="start from BSON documents in the result store")
