@@ -640,3 +640,28 @@ def test_splitn_rejects_unaligned(dev, lib):
     big[:, 1:65] = torch.from_numpy(Xh).to(dev)
     got = engine.fold_stacked(big[:, 1:65], [1, 2, 3, 4], exact=False).cpu().numpy()
     assert _bits_equal(got, OL.fedavg_f32(Xh, np.array([1, 2, 3, 4], np.float32), np.float32(10)))
+
+
+@pytest.mark.parametrize("scored", [False, True])
+def test_empty_and_scalar_layers(dev, scored):
+    """Layers with zero elements and 0-d layers next to ordinary ones, through
+    the drop-in classes, against the oracle's literal numpy fold."""
+    from oracle import fedavg_oracle as O
+    from fedlesscan_amd import FedAvgAggregator, StallAwareAggregator
+    from fedlesscan_amd.common.models import AggregationHyperParams
+    N = 5
+    rng = np.random.default_rng(3)
+    params = [[rng.standard_normal((3, 4)).astype(np.float32), np.zeros((0, 5), np.float32),
+               np.float32(rng.standard_normal()).reshape(()), rng.standard_normal(7).astype(np.float32)]
+              for _ in range(N)]
+    w = [3, 1, 4, 1, 5]
+    if scored:
+        feats = [{"round_id": r} for r in (8, 9, 10, 10, 9)]
+        got = StallAwareAggregator(10, AggregationHyperParams(tolerance=2))._aggregate(feats, params, w)
+        exp = O.stall_aware_literal(feats, 10, params, w)
+    else:
+        got = FedAvgAggregator()._aggregate(params, w)
+        exp = O.fedavg_literal(params, w)
+    assert [g.shape for g in got] == [e.shape for e in exp]
+    for g, e in zip(got, exp):
+        assert g.dtype == e.dtype and _bits_equal(g, e)
