@@ -665,3 +665,27 @@ def test_empty_and_scalar_layers(dev, scored):
     assert [g.shape for g in got] == [e.shape for e in exp]
     for g, e in zip(got, exp):
         assert g.dtype == e.dtype and _bits_equal(g, e)
+
+
+@pytest.mark.parametrize("N,P", [(64, 4099), (300, 300_001)])
+def test_fold_captures_into_hip_graph(dev, lib, N, P):
+    """The C-ABI enqueues only (no allocation, no synchronisation), so a fold
+    captures into a HIP graph and replays bit-exactly on new inputs."""
+    L = lib.load()
+    X = torch.from_numpy(synth.clients_f32(71, N, 0, P)).to(dev)
+    w = synth.cardinalities(71, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    out = _sentinel(P, dev)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rc = L.fa_fedavg_f32(X.data_ptr(), N, P, P, a.data_ptr(), None, div, out.data_ptr(), s.cuda_stream)
+    assert rc == 0, lib.last_error()
+    for seed in (72, 73):
+        X.copy_(torch.from_numpy(synth.clients_f32(seed, N, 0, P)))
+        g.replay()
+        torch.cuda.synchronize()
+        exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
+        assert _bits_equal(out.cpu().numpy(), exp)
