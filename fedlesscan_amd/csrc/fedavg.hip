@@ -91,7 +91,7 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 // lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
 // multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
 // ---------------------------------------------------------------------------
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock>
 __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
                                            const float* __restrict__ a, const float* __restrict__ s,
                                            const f32x4* acc_in, float divisor, f32x4* out) {
@@ -99,11 +99,11 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
     int64_t i = 0;
     if constexpr (ACC) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = acc_in[c * kBlock];
+        for (int c = 0; c < C; ++c) acc[c] = acc_in[c * B];
     } else {
         const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(ld4<NT>(p + c * kBlock), a0, s0);
+        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(ld4<NT>(p + c * B), a0, s0);
         i = 1;
     }
     for (; i + U <= N; i += U) {
@@ -111,7 +111,7 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int c = 0; c < C; ++c) v[u][c] = ld4<NT>(p + (i + u) * ldq + c * kBlock);
+            for (int c = 0; c < C; ++c) v[u][c] = ld4<NT>(p + (i + u) * ldq + c * B);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
@@ -122,13 +122,13 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
     for (; i < N; ++i) {
         const float ai = a[i], si = SCORED ? s[i] : 1.0f;
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * kBlock), ai, si));
+        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * B), ai, si));
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
-        if constexpr (NTS) __builtin_nontemporal_store(r, out + c * kBlock);
-        else out[c * kBlock] = r;
+        if constexpr (NTS) __builtin_nontemporal_store(r, out + c * B);
+        else out[c * B] = r;
     }
 }
 
@@ -141,31 +141,31 @@ __device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t n) {
 }
 
 // One tile: C*kBlock quads of every client row (tile index bid).
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
 __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           const float* acc_in, float divisor, float* out) {
     const int64_t nq = P >> 2;
     const int64_t ldq = ldx >> 2;
-    const int64_t q0 = bid * (kBlock * C) + threadIdx.x;
+    const int64_t q0 = bid * (B * C) + threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
     const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
     f32x4* O4 = reinterpret_cast<f32x4*>(out);
-    if (q0 + (int64_t)(C - 1) * kBlock < nq) {
+    if (q0 + (int64_t)(C - 1) * B < nq) {
         // every quad of this lane is in range (all blocks but the last)
-        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
+        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS, B>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
                                                     O4 + q0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        const int64_t q = q0 + (int64_t)c * kBlock;
+        const int64_t q = q0 + (int64_t)c * B;
         if (q < nq)
-            fold_quads<U, 1, NT, SCORED, ACC, FIN>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
+            fold_quads<U, 1, NT, SCORED, ACC, FIN, false, B>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
     }
     // column tail: at most 3 columns, folded by the lane that would own quad
     // index nq under the C-quads-per-lane mapping (scalar loads, same order)
-    const int64_t tb = nq / (kBlock * C), tl = (nq % (kBlock * C)) % kBlock;
+    const int64_t tb = nq / (B * C), tl = (nq % (B * C)) % B;
     if ((P & 3) && bid == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = nq * 4; col < P; ++col) {
             float acc;
@@ -198,13 +198,13 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
 // rows visited in near lock-step) and each block streams many rows per tile.
 // On MI355X this reads HBM faster than one block per tile with several
 // resident per CU.
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
-__global__ __launch_bounds__(kBlock) void k_fold_f32_gs(
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
+__global__ __launch_bounds__(B) void k_fold_f32_gs(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
     const float* acc_in, float divisor, float* out, int64_t ntiles) {  // acc_in may alias out
     for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
-        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
 
 // Balanced persistent form: the grid is the resident capacity (occupancy x
@@ -951,6 +951,9 @@ constexpr F32Variant kVariants[] = {
     {"gs1_u2c8nt_nts", 2, 8, true}, {"gs1_u4c8nt_nts", 4, 8, true}, {"gs1_u2c16nt_nts", 2, 16, true},
     {"gs1_u1c16nt_nts", 1, 16, true}, {"v4_pickq_nts", 0, 0, true},
     {"gs1_u16c4nt_nts", 16, 4, true}, {"gs1_u16c2nt_nts", 16, 2, true}, {"gs1_u12c4nt_nts", 12, 4, true},
+    // grid-stride with 512- / 1024-thread blocks (b512 / b1024)
+    {"gs1b512_u8c2nt_nts", 8, 2, true}, {"gs1b512_u4c4nt_nts", 4, 4, true}, {"gs1b512_u8c4nt_nts", 8, 4, true},
+    {"gs1b1024_u8c1nt_nts", 8, 1, true}, {"gs1b1024_u4c2nt_nts", 4, 2, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1039,21 +1042,21 @@ int cu_count() {
 }
 
 // Grid-stride fold: grid = min(tiles, per_cu x CUs).
-template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool NTS>
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool NTS, int B>
 void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
-    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t per_block = (int64_t)B * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
     const int64_t tiles = (units + per_block - 1) / per_block;  // incl. the column-tail lane
     int64_t grid = (int64_t)per_cu * cu_count();
     if (grid > tiles) grid = tiles;
-    hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS>), dim3((unsigned)grid), dim3(kBlock), 0, st, X,
+    hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS, B>), dim3((unsigned)grid), dim3(B), 0, st, X,
                        N, P, ldx, a, s, acc_in, d, out, tiles);
 }
 
-template <int U, int C, bool NTS>
+template <int U, int C, bool NTS, int B = kBlock>
 void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
-#define FA_G(SC, ACC, FIN) launch_gs<U, C, true, SC, ACC, FIN, NTS>(st, per_cu, X, N, P, ldx, a, s, acc_in, d, out)
+#define FA_G(SC, ACC, FIN) launch_gs<U, C, true, SC, ACC, FIN, NTS, B>(st, per_cu, X, N, P, ldx, a, s, acc_in, d, out)
     if (sc) {
         if (acc) { if (fin) FA_G(true, true, true); else FA_G(true, true, false); }
         else     { if (fin) FA_G(true, false, true); else FA_G(true, false, false); }
@@ -1155,6 +1158,8 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     launch_v4_flags<U, C, true, false, XR, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VG(K, U, C, NTS) \
     launch_gs_flags<U, C, NTS>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VGB(K, U, C, B) \
+    launch_gs_flags<U, C, true, B>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VL(NW, R, TQ) \
     launch_lds_flags<NW, R, TQ>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     int rc = FA_OK;
@@ -1215,6 +1220,11 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 48: FA_VG(1, 16, 4, true); break;
         case 49: FA_VG(1, 16, 2, true); break;
         case 50: FA_VG(1, 12, 4, true); break;
+        case 51: FA_VGB(1, 8, 2, 512); break;
+        case 52: FA_VGB(1, 4, 4, 512); break;
+        case 53: FA_VGB(1, 8, 4, 512); break;
+        case 54: FA_VGB(1, 8, 1, 1024); break;
+        case 55: FA_VGB(1, 4, 2, 1024); break;
         case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
@@ -1230,6 +1240,7 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #undef FA_VS
 #undef FA_VL
 #undef FA_VG
+#undef FA_VGB
     if (rc) return rc;
     return check_launch("fold_f32");
 }
