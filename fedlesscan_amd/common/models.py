@@ -77,9 +77,14 @@ class AggregatorFunctionResult(BaseModel):
 
 
 class AggregatorFunctionParams(BaseModel):
-    """aggregation_models.py:25-34 (database config replaced by the in-memory store)."""
+    """aggregation_models.py:25-34.  `database` (the MongoDB connection) is
+    accepted so the reference controller's requests parse, but results and
+    parameters come from the in-memory stores; `test_data` (Keras global
+    evaluation) is out of scope and the handler refuses a non-null one."""
     session_id: str
     round_id: int
+    database: Optional[Dict] = None
+    test_data: Optional[Dict] = None
     serializer: WeightsSerializerConfig = Field(
         default_factory=lambda: WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig()))
     aggregation_hyper_params: AggregationHyperParams = Field(default_factory=AggregationHyperParams)

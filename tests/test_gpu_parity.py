@@ -689,3 +689,22 @@ def test_fold_captures_into_hip_graph(dev, lib, N, P):
         torch.cuda.synchronize()
         exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
         assert _bits_equal(out.cpu().numpy(), exp)
+
+
+def test_openfaas_entry_point_on_gpu(dev):
+    """The FaaS entry point end to end on the HIP fold: request JSON in,
+    response JSON out, the saved round+1 model bit-exact vs the oracle."""
+    import json
+    from oracle import fedavg_oracle as O
+    from test_host import REF_REQUEST, _stores_with_round
+    from fedlesscan_amd.common.serialization import NpzWeightsSerializer
+    from fedlesscan_amd.functions import Event, make_openfaas_handler
+    st, ps = _stores_with_round()
+    ins = [(NpzWeightsSerializer().deserialize(r.parameters.blob), r.cardinality)
+           for r in st.load_results_for_round("s", 3)[1]]
+    resp = make_openfaas_handler(st, ps)(Event(json.dumps(REF_REQUEST)))
+    assert resp["statusCode"] == 200, resp["body"]
+    assert json.loads(resp["body"])["num_clients"] == 4
+    got = NpzWeightsSerializer().deserialize(ps.load("s", 4).blob)
+    exp = O.fedavg_literal([p for p, _ in ins], [c for _, c in ins])
+    assert all(_bits_equal(g, e) for g, e in zip(got, exp))

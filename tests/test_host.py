@@ -446,3 +446,74 @@ def test_aggregator_settings_from_yaml(tmp_path):
     assert hp.tolerance == 2 and hp.aggregate_online is True and hp.test_batch_size == 10
     strategy, hp = aggregator_settings({}, "fedavg")
     assert strategy == AggregationStrategy.PER_ROUND and hp.tolerance == 0
+
+
+# ---------------------------------------------------------------------------
+# FaaS entry points (functions/aggregator_functions/*, providers.py)
+# ---------------------------------------------------------------------------
+def _stores_with_round(n=4, round_id=3, session="s"):
+    st, ps = InMemoryClientResultStore(), InMemoryParameterStore()
+    rng = np.random.default_rng(5)
+    for i in range(n):
+        p = [rng.standard_normal((2, 3)).astype(np.float32), rng.standard_normal(4).astype(np.float32)]
+        st.save(session, round_id, f"c{i}", ClientResult(parameters=SerializedParameters(
+            blob=NpzWeightsSerializer().serialize(p),
+            serializer=WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())),
+            cardinality=i + 1))
+    return st, ps
+
+
+REF_REQUEST = {  # what the reference controller sends (aggregation_models.py:25-34)
+    "session_id": "s", "round_id": 3,
+    "database": {"host": "mongo", "port": 27017, "username": "u", "password": "p"},
+    "serializer": {"type": "npz", "params": {"type": "npz", "compressed": False}},
+    "test_data": None,
+    "aggregation_hyper_params": {"tolerance": 0, "aggregate_online": False, "test_batch_size": 10},
+    "aggregation_strategy": "per_round",
+}
+
+
+def test_openfaas_entry_point(oracle_fold):
+    import json
+    from fedlesscan_amd.functions import Event, make_openfaas_handler
+    st, ps = _stores_with_round()
+    handle = make_openfaas_handler(st, ps)
+    resp = handle(Event(json.dumps(REF_REQUEST)), None)
+    assert resp["statusCode"] == 200 and resp["headers"]["Content-Type"] == "application/json"
+    body = json.loads(resp["body"])
+    assert body == {"new_round_id": 4, "num_clients": 4, "test_results": None, "global_test_results": None}
+    assert ps.load("s", 4) is not None
+    # the round's results were deleted (delete_results_after_finish default): a second call finds none
+    resp = handle(Event(json.dumps(REF_REQUEST)), None)
+    err = json.loads(resp["body"])
+    assert resp["statusCode"] == 400 and err["errorType"] == "InsufficientClientResults"
+    assert set(err) == {"errorMessage", "errorType", "details"}
+    # malformed request -> pydantic ValidationError -> 400
+    bad = dict(REF_REQUEST)
+    del bad["round_id"]
+    resp = handle(Event(json.dumps(bad)), None)
+    assert resp["statusCode"] == 400 and json.loads(resp["body"])["errorType"] == "ValidationError"
+    # global evaluation is out of scope -> AggregationError -> 400
+    st, ps = _stores_with_round()
+    req = dict(REF_REQUEST, test_data={"type": "mnist", "params": {}})
+    resp = make_openfaas_handler(st, ps)(Event(json.dumps(req)))
+    assert resp["statusCode"] == 400 and json.loads(resp["body"])["errorType"] == "AggregationError"
+
+
+def test_openwhisk_entry_point(oracle_fold):
+    import base64
+    import json
+    from fedlesscan_amd.functions import make_openwhisk_main
+    st, ps = _stores_with_round()
+    main = make_openwhisk_main(st, ps)
+    resp = main(dict(REF_REQUEST))  # plain action: the params are the body
+    assert resp["statusCode"] == 200 and json.loads(resp["body"])["num_clients"] == 4
+    # web action: __ow_ keys, body base64-encoded JSON
+    st, ps = _stores_with_round()
+    main = make_openwhisk_main(st, ps)
+    enc = base64.b64encode(json.dumps(REF_REQUEST).encode()).decode()
+    resp = main({"__ow_body": enc, "__ow_method": "post", "__ow_headers": {}})
+    assert resp["statusCode"] == 200 and json.loads(resp["body"])["new_round_id"] == 4
+    # a body that is neither JSON nor base64 -> binascii.Error -> 400
+    resp = main({"__ow_body": "abc", "__ow_method": "post"})
+    assert resp["statusCode"] == 400 and json.loads(resp["body"])["errorType"] == "Error"
