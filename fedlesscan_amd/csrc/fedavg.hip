@@ -954,6 +954,12 @@ constexpr F32Variant kVariants[] = {
     // grid-stride with 512- / 1024-thread blocks (b512 / b1024)
     {"gs1b512_u8c2nt_nts", 8, 2, true}, {"gs1b512_u4c4nt_nts", 4, 4, true}, {"gs1b512_u8c4nt_nts", 8, 4, true},
     {"gs1b1024_u8c1nt_nts", 8, 1, true}, {"gs1b1024_u4c2nt_nts", 4, 2, true},
+    // grid-stride, balanced passes (grid = ceil(tiles / passes))
+    {"gsbal_u8c4nt_nts", 8, 4, true}, {"gsbal_u8c2nt_nts", 8, 2, true}, {"gsbal_u4c4nt_nts", 4, 4, true},
+    {"gsbal2_u8c4nt_nts", 8, 4, true},
+    // grid-stride, balanced passes over a fixed number of blocks (gsq<blocks>)
+    {"gsq128_u8c4nt_nts", 8, 4, true}, {"gsq160_u8c4nt_nts", 8, 4, true}, {"gsq192_u8c4nt_nts", 8, 4, true},
+    {"gsq224_u8c4nt_nts", 8, 4, true}, {"gsq192_u8c2nt_nts", 8, 2, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -967,18 +973,34 @@ inline int pick_quads(int64_t P) {
     return 1;
 }
 
+// Compute units of the current device (cached per device).
+int cu_count() {
+    static thread_local int cache[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cache[dev] > 0) return cache[dev];
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    cache[dev] = cus;
+    return cus;
+}
+
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
-// model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log):
-//   P < 256K params               LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
-//                                 (one lane per quad cannot fill the chip: 2-2.4x)
-//   N >= 256 and 2M <= P < 8M     LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
-//   otherwise (C2, C3, C5, ...)   grid-stride, 1 block per CU, 8 rows x 4 quads, nt stores
-enum class F32Pick { kLdsW4, kLdsW8, kGs1U8C4 };
+// model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
+// profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
+//   P < 256K params                    LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
+//   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
+//   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads
+// all with non-temporal output stores.
+enum class F32Pick { kLdsW4, kLdsW8, kGsBalC2, kGsBalC4 };
 inline F32Pick pick_f32(int64_t N, int64_t P) {
-    const int64_t nq = P >> 2;
+    const int64_t nq = P >> 2, cus = cu_count();
     if (nq < (1 << 16)) return F32Pick::kLdsW4;
-    if (N >= 256 && nq >= (1 << 19) && nq < (1 << 21)) return F32Pick::kLdsW8;
-    return F32Pick::kGs1U8C4;
+    const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
+    if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
+    if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
+    return F32Pick::kGsBalC4;
 }
 constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf16u4c2", "bf16u8c2",
                                          "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4",
@@ -1029,26 +1051,22 @@ void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
 }
 
-// Compute units of the current device (cached per device).
-int cu_count() {
-    static thread_local int cache[16] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-    if (cache[dev] > 0) return cache[dev];
-    int cus = 256;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    cache[dev] = cus;
-    return cus;
-}
-
-// Grid-stride fold: grid = min(tiles, per_cu x CUs).
+// Grid-stride fold: grid = min(tiles, per_cu x CUs); per_cu < 0 = balanced passes.
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool NTS, int B>
 void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
     const int64_t per_block = (int64_t)B * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
     const int64_t tiles = (units + per_block - 1) / per_block;  // incl. the column-tail lane
-    int64_t grid = (int64_t)per_cu * cu_count();
+    // per_cu >= 1000: a fixed block count (per_cu - 1000), balanced passes (sweeps only)
+    int64_t grid = per_cu >= 1000 ? per_cu - 1000 : (int64_t)(per_cu > 0 ? per_cu : -per_cu) * cu_count();
     if (grid > tiles) grid = tiles;
+    if (per_cu < 0 || per_cu >= 1000) {
+        // balanced passes: the fewest blocks that still finish in the same
+        // number of passes, so the last pass is (nearly) full instead of
+        // leaving up to a whole pass of CUs idle
+        const int64_t passes = (tiles + grid - 1) / grid;
+        grid = (tiles + passes - 1) / passes;
+    }
     hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS, B>), dim3((unsigned)grid), dim3(B), 0, st, X,
                        N, P, ldx, a, s, acc_in, d, out, tiles);
 }
@@ -1168,7 +1186,8 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
             switch (pick_f32(N, P)) {
                 case F32Pick::kLdsW4: rc = FA_VL(4, 64, 32); break;
                 case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
-                default: FA_VG(1, 8, 4, true); break;
+                case F32Pick::kGsBalC2: FA_VG(-1, 8, 2, true); break;
+                default: FA_VG(-1, 8, 4, true); break;
             }
             break;
         case 1: FA_VF(4, 4, true); break;
@@ -1225,6 +1244,15 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 53: FA_VGB(1, 8, 4, 512); break;
         case 54: FA_VGB(1, 8, 1, 1024); break;
         case 55: FA_VGB(1, 4, 2, 1024); break;
+        case 56: FA_VG(-1, 8, 4, true); break;
+        case 57: FA_VG(-1, 8, 2, true); break;
+        case 58: FA_VG(-1, 4, 4, true); break;
+        case 59: FA_VG(-2, 8, 4, true); break;
+        case 60: FA_VG(1128, 8, 4, true); break;
+        case 61: FA_VG(1160, 8, 4, true); break;
+        case 62: FA_VG(1192, 8, 4, true); break;
+        case 63: FA_VG(1224, 8, 4, true); break;
+        case 64: FA_VG(1192, 8, 2, true); break;
         case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
