@@ -1006,7 +1006,9 @@ constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf
                                          "bf16u1c8", "bf16u2c8", "bf16u1c4", "bf16u2c4",
                                          // grid-stride, gs<k> = k blocks per CU
                                          "bf16gs1u8c4", "bf16gs1u8c2", "bf16gs1u4c4", "bf16gs2u8c2",
-                                         "bf16gs1u16c2", "bf16gs2u4c4"};
+                                         "bf16gs1u16c2", "bf16gs2u4c4",
+                                         // balanced passes (grid = ceil(tiles / passes))
+                                         "bf16gsbalu8c2", "bf16gsbalu4c4", "bf16gsbalu2c8", "bf16gsbalu4c8"};
 
 // bf16 "auto": octets per lane from the client count.  Sweeps on MI355X
 //  put the optimum near 8 MB per block (rows x C x 4 KiB):
@@ -1401,8 +1403,9 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
     {                                                                                                      \
         const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);           \
         const int64_t tiles = (units + per_block - 1) / per_block;                                         \
-        int64_t g = (int64_t)(K) * cu_count();                                                             \
+        int64_t g = (int64_t)((K) > 0 ? (K) : -(K)) * cu_count();                                         \
         if (g > tiles) g = tiles;                                                                          \
+        if ((K) < 0) g = (tiles + (tiles + g - 1) / g - 1) / ((tiles + g - 1) / g);                        \
         if (s)                                                                                             \
             hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, X,  \
                                N, P, ldx, a, s, divisor, out_f32, out_bf16, tiles);                        \
@@ -1416,6 +1419,12 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                 // over the row-streaming pick; the full 100M model: pick_octets
                 if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
                     FA_BG(1, 8, 2);
+                    break;
+                }
+                // whole large models (C4's 100M on one GPU): balanced passes over
+                // 32 KiB tiles -- fewer tile switches per block, +3 %
+                if ((P >> 3) >= ((int64_t)1 << 22)) {
+                    FA_BG(-1, 2, 8);
                     break;
                 }
                 switch (pick_octets(N, P)) {
@@ -1438,7 +1447,11 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             case 11: FA_BG(1, 4, 4); break;
             case 12: FA_BG(2, 8, 2); break;
             case 13: FA_BG(1, 16, 2); break;
-            default: FA_BG(2, 4, 4); break;
+            case 14: FA_BG(2, 4, 4); break;
+            case 15: FA_BG(-1, 8, 2); break;
+            case 16: FA_BG(-1, 4, 4); break;
+            case 17: FA_BG(-1, 2, 8); break;
+            default: FA_BG(-1, 4, 8); break;
         }
 #undef FA_BF
 #undef FA_BG
