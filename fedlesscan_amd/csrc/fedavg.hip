@@ -960,6 +960,9 @@ constexpr F32Variant kVariants[] = {
     // grid-stride, balanced passes over a fixed number of blocks (gsq<blocks>)
     {"gsq128_u8c4nt_nts", 8, 4, true}, {"gsq160_u8c4nt_nts", 8, 4, true}, {"gsq192_u8c4nt_nts", 8, 4, true},
     {"gsq224_u8c4nt_nts", 8, 4, true}, {"gsq192_u8c2nt_nts", 8, 2, true},
+    // balanced grid-stride launches over column bands of <k> passes x CUs tiles (gsband<k>)
+    {"gsband2_u8c4nt_nts", 8, 4, true}, {"gsband3_u8c4nt_nts", 8, 4, true}, {"gsband4_u8c4nt_nts", 8, 4, true},
+    {"gsband3_u4c4nt_nts", 4, 4, true}, {"gsband6_u8c4nt_nts", 8, 4, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -991,7 +994,8 @@ int cu_count() {
 //   P < 256K params                    LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
-//   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads
+//   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
+//                                      in column bands of <= 4 passes x CUs tiles
 // all with non-temporal output stores.
 enum class F32Pick { kLdsW4, kLdsW8, kGsBalC2, kGsBalC4 };
 inline F32Pick pick_f32(int64_t N, int64_t P) {
@@ -1087,6 +1091,31 @@ void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, co
 #undef FA_G
 }
 
+// Column bands: the fold as several back-to-back balanced grid-stride
+// launches over contiguous column bands of about `passes` x CUs tiles each.
+// Columns are independent, so this is the same arithmetic; the kernel
+// boundaries re-align the blocks, which otherwise drift apart over many
+// passes (C3: 4 bands of 611 tiles, 5.80 ms, against 5.91 ms as one launch,
+// DESIGN.md 5).
+template <int U, int C, bool NTS>
+void launch_gs_bands(hipStream_t st, int passes, bool sc, bool acc, bool fin, const float* X, int64_t N,
+                     int64_t P, int64_t ldx, const float* a, const float* s, const float* acc_in, float d,
+                     float* out) {
+    const int64_t tq = (int64_t)kBlock * C;  // quads per tile
+    const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + tq - 1) / tq;
+    const int64_t per_band = (int64_t)passes * cu_count();
+    const int64_t nb = (tiles + per_band - 1) / per_band;
+    const int64_t band_tiles = (tiles + nb - 1) / nb;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t c0 = b * band_tiles * tq * 4;  // first column of the band (a multiple of 4 KiB x C)
+        if (c0 >= P) break;
+        const int64_t pb = (P - c0) < band_tiles * tq * 4 ? (P - c0) : band_tiles * tq * 4;
+        launch_gs_flags<U, C, NTS>(st, -1, sc, acc, fin, N == 0 ? X : X + c0, N, pb, ldx, a, s,
+                                   acc_in ? acc_in + c0 : nullptr, d, out + c0);
+    }
+}
+
 template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false, bool NTS = false>
 void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
                const float* s, const float* acc_in, float d, float* out) {
@@ -1180,6 +1209,8 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     launch_gs_flags<U, C, NTS>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VGB(K, U, C, B) \
     launch_gs_flags<U, C, true, B>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VBAND(K, U, C) \
+    launch_gs_bands<U, C, true>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VL(NW, R, TQ) \
     launch_lds_flags<NW, R, TQ>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     int rc = FA_OK;
@@ -1189,7 +1220,7 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
                 case F32Pick::kLdsW4: rc = FA_VL(4, 64, 32); break;
                 case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
                 case F32Pick::kGsBalC2: FA_VG(-1, 8, 2, true); break;
-                default: FA_VG(-1, 8, 4, true); break;
+                default: FA_VBAND(4, 8, 4); break;  // one band below 4 x CUs tiles
             }
             break;
         case 1: FA_VF(4, 4, true); break;
@@ -1255,6 +1286,11 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 62: FA_VG(1192, 8, 4, true); break;
         case 63: FA_VG(1224, 8, 4, true); break;
         case 64: FA_VG(1192, 8, 2, true); break;
+        case 65: FA_VBAND(2, 8, 4); break;
+        case 66: FA_VBAND(3, 8, 4); break;
+        case 67: FA_VBAND(4, 8, 4); break;
+        case 68: FA_VBAND(3, 4, 4); break;
+        case 69: FA_VBAND(6, 8, 4); break;
         case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
@@ -1271,6 +1307,7 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #undef FA_VL
 #undef FA_VG
 #undef FA_VGB
+#undef FA_VBAND
     if (rc) return rc;
     return check_launch("fold_f32");
 }

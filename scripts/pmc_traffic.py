@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into HBM bytes per launch.
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into HBM bytes per fold call.
 
     python scripts/pmc_traffic.py --fetch DIR_A --write DIR_B --kernel k_fold_f32_v4 \
         --bytes 41000000000 --out profiles/pmc_c3.json
@@ -41,26 +41,33 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--kernel", required=True)
-    ap.add_argument("--bytes", type=float, required=True, help="algorithmic bytes per launch")
+    ap.add_argument("--bytes", type=float, required=True, help="algorithmic bytes per fold call")
+    ap.add_argument("--dispatches-per-call", type=int, default=1,
+                    help="kernel dispatches one fa_fedavg_f32 call makes (column bands); bytes are summed per call")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = per_dispatch(counter_rows(a.fetch), "FETCH_SIZE", a.kernel)
     write = per_dispatch(counter_rows(a.write), "WRITE_SIZE", a.kernel)
     if not fetch or not write:
         raise SystemExit(f"no counter rows for {a.kernel}: fetch={len(fetch)} write={len(write)}")
-    f_kib = statistics.median(fetch)
-    w_kib = statistics.median(write)
+    k = a.dispatches_per_call
+    if len(fetch) % k or len(write) % k:
+        raise SystemExit(f"{len(fetch)}/{len(write)} dispatches are not whole calls of {k}")
+    # per call: the sum over its k consecutive band dispatches, median over calls
+    f_kib = statistics.median(sum(fetch[i:i + k]) for i in range(0, len(fetch), k))
+    w_kib = statistics.median(sum(write[i:i + k]) for i in range(0, len(write), k))
     read_bytes = 2.0 * f_kib * 1024.0   # gfx950: FETCH_SIZE = 1/2 of a wide streaming read
     write_bytes = w_kib * 1024.0
     res = {
         "kernel": a.kernel,
         "dispatches": {"fetch": len(fetch), "write": len(write)},
+        "dispatches_per_call": k,
         "FETCH_SIZE_KiB_median": f_kib,
         "WRITE_SIZE_KiB_median": w_kib,
-        "hbm_read_bytes_per_launch": read_bytes,
-        "hbm_write_bytes_per_launch": write_bytes,
-        "hbm_bytes_per_launch": read_bytes + write_bytes,
-        "algorithmic_bytes_per_launch": a.bytes,
+        "hbm_read_bytes_per_call": read_bytes,
+        "hbm_write_bytes_per_call": write_bytes,
+        "hbm_bytes_per_launch": read_bytes + write_bytes,  # per fold call (bench.py reads this key)
+        "algorithmic_bytes_per_call": a.bytes,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / a.bytes,
         "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads); "
                       "write = WRITE_SIZE x 1024",

@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_c3
     python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
 cd "$ROOT"
 python3 scripts/pmc_traffic.py --fetch "$OUT/pmc_c3_fetch" --write "$OUT/pmc_c3_write" \
-    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --out profiles/pmc_c3.json
+    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --dispatches-per-call 3 --out profiles/pmc_c3.json

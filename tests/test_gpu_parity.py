@@ -708,3 +708,35 @@ def test_openfaas_entry_point_on_gpu(dev):
     got = NpzWeightsSerializer().deserialize(ps.load("s", 4).blob)
     exp = O.fedavg_literal([p for p, _ in ins], [c for _, c in ins])
     assert all(_bits_equal(g, e) for g, e in zip(got, exp))
+
+
+@pytest.mark.parametrize("P", [4 * 1024 * 256 * 2 + 4096 * 3 + 3, 5_000_003])
+def test_band_variants_multi_band(dev, lib, P):
+    """Column-band launches (several kernels over contiguous column bands):
+    every band boundary and the tail, plain, stall-aware and as a chunked
+    continuation, bit-exact vs the oracle."""
+    L = lib.load()
+    N = 3
+    X = torch.from_numpy(synth.clients_f32(81, N, 0, P)).to(dev)
+    w = synth.cardinalities(81, N)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    sc = [(r + 1) / 11 for r in synth.round_ids(81, N, 10, 2)]
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Xh = X.cpu().numpy()
+    exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    bands = [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"gsband")]
+    assert bands
+    for v in bands + [0]:
+        for sp, e in ((None, exp), (s, exp_s)):
+            o = _sentinel(P, dev)
+            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+                                              None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v), "v")
+            assert _bits_equal(o.cpu().numpy(), e), (L.fa_variant_name(v), sp is not None)
+    acc = _sentinel(P, dev)  # auto policy as a two-chunk continuation
+    lib.check(L.fa_fold_f32(X.data_ptr(), 2, P, P, a.data_ptr(), None, None, div, 0, acc.data_ptr(), st), "f")
+    lib.check(L.fa_fold_f32(X[2].data_ptr(), 1, P, P, a[2:].data_ptr(), None, acc.data_ptr(), div, 1,
+                            acc.data_ptr(), st), "f")
+    assert _bits_equal(acc.cpu().numpy(), exp)
