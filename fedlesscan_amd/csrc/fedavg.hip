@@ -1012,7 +1012,9 @@ constexpr const char* kBf16Variants[] = {"bf16auto", "bf16u8c1", "bf16u4c4", "bf
                                          "bf16gs1u8c4", "bf16gs1u8c2", "bf16gs1u4c4", "bf16gs2u8c2",
                                          "bf16gs1u16c2", "bf16gs2u4c4",
                                          // balanced passes (grid = ceil(tiles / passes))
-                                         "bf16gsbalu8c2", "bf16gsbalu4c4", "bf16gsbalu2c8", "bf16gsbalu4c8"};
+                                         "bf16gsbalu8c2", "bf16gsbalu4c4", "bf16gsbalu2c8", "bf16gsbalu4c8",
+                                         // column bands of <k> passes (balanced grid-stride launches)
+                                         "bf16band4u2c8", "bf16band2u2c8", "bf16band4u8c2", "bf16band4u4c4"};
 
 // bf16 "auto": octets per lane from the client count.  Sweeps on MI355X
 //  put the optimum near 8 MB per block (rows x C x 4 KiB):
@@ -1312,6 +1314,43 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     return check_launch("fold_f32");
 }
 
+// bf16 grid-stride launch (per_cu < 0: balanced passes) and its column-band form
+template <int U, int C>
+void launch_bf16_gs(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                    const float* a, const float* s, float d, float* out, uint16_t* outb) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 3) + ((P & 7) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    int64_t g = (int64_t)(per_cu > 0 ? per_cu : -per_cu) * cu_count();
+    if (g > tiles) g = tiles;
+    if (per_cu < 0) {
+        const int64_t passes = (tiles + g - 1) / g;
+        g = (tiles + passes - 1) / passes;
+    }
+    if (s)
+        hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, X, N, P, ldx, a,
+                           s, d, out, outb, tiles);
+    else
+        hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, X, N, P, ldx,
+                           a, s, d, out, outb, tiles);
+}
+
+template <int U, int C>
+void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                       const float* a, const float* s, float d, float* out, uint16_t* outb) {
+    const int64_t to = (int64_t)kBlock * C;  // octets per tile
+    const int64_t units = (P >> 3) + ((P & 7) ? 1 : 0);
+    const int64_t tiles = (units + to - 1) / to;
+    const int64_t per_band = (int64_t)passes * cu_count();
+    const int64_t nb = (tiles + per_band - 1) / per_band;
+    const int64_t band_tiles = (tiles + nb - 1) / nb;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t c0 = b * band_tiles * to * 8;
+        if (c0 >= P) break;
+        const int64_t pb = (P - c0) < band_tiles * to * 8 ? (P - c0) : band_tiles * to * 8;
+        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
+    }
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1458,10 +1497,11 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                     FA_BG(1, 8, 2);
                     break;
                 }
-                // whole large models (C4's 100M on one GPU): balanced passes over
-                // 32 KiB tiles -- fewer tile switches per block, +3 %
+                // whole large models (C4's 100M on one GPU): balanced grid-stride
+                // launches over 32 KiB tiles (fewer tile switches per block), in
+                // column bands of 2 passes: +4 % over one launch
                 if ((P >> 3) >= ((int64_t)1 << 22)) {
-                    FA_BG(-1, 2, 8);
+                    launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
                     break;
                 }
                 switch (pick_octets(N, P)) {
@@ -1488,7 +1528,11 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
             case 15: FA_BG(-1, 8, 2); break;
             case 16: FA_BG(-1, 4, 4); break;
             case 17: FA_BG(-1, 2, 8); break;
-            default: FA_BG(-1, 4, 8); break;
+            case 18: FA_BG(-1, 4, 8); break;
+            case 19: launch_bf16_bands<2, 8>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+            case 20: launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+            case 21: launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+            default: launch_bf16_bands<4, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         }
 #undef FA_BF
 #undef FA_BG
