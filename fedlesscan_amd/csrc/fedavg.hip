@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_balanced(
 //   every other fold.  The partial quad of the P%4 tail columns is staged
 //   like a full one (element loads, zero-filled) and only its real columns
 //   are stored.  Per-chunk factors a[], s[] are staged in LDS too.
-template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN>
+template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1>
 __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
@@ -275,51 +275,55 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const int64_t ldq = ldx >> 2;
     const int t = threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
-    f32x4 v[LQ];
-    float fv = 0.f, sv = 0.f;
+    // one chunk in registers: its LQ quads per lane and (lanes < R) its factors
+    struct Stage {
+        f32x4 v[LQ];
+        float fv, sv;
+    };
+    Stage A, B;
     // Interior blocks (TQ full quads) stream their full chunks through a loop
     // whose loads carry no checks and no control flow: a branch between a
     // load and its use (the tail-quad loop, or a join with a checked path)
     // makes the compiler wait for the load right after issuing it, which
     // would serialise the chunk loads with the fold.  The last block and the
     // last partial chunk take the checked path, outside that loop.
-    auto load_full = [&](int64_t c) {  // chunk c: rows [c*R, c*R + R), every quad in range
+    auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
 #pragma unroll
         for (int j = 0; j < LQ; ++j) {
             const int e = t + j * NT;
-            v[j] = __builtin_nontemporal_load(X4 + (c * R + e / TQ) * ldq + q0 + e % TQ);
+            g.v[j] = __builtin_nontemporal_load(X4 + (c * R + e / TQ) * ldq + q0 + e % TQ);
         }
         if (t < R) {
-            fv = a[c * R + t];
-            if constexpr (SCORED) sv = s[c * R + t];
+            g.fv = a[c * R + t];
+            if constexpr (SCORED) g.sv = s[c * R + t];
         }
     };
-    auto load_checked = [&](int64_t c) {
+    auto load_checked = [&](int64_t c, Stage& g) {
 #pragma unroll
         for (int j = 0; j < LQ; ++j) {
             const int e = t + j * NT, r = e / TQ, qq = e % TQ;
             const int64_t row = c * R + r, q = q0 + qq;
             if (row < N && qq < tq) {
                 if (q < nq) {
-                    v[j] = __builtin_nontemporal_load(X4 + row * ldq + q);
+                    g.v[j] = __builtin_nontemporal_load(X4 + row * ldq + q);
                 } else {  // partial tail quad: P%4 real columns
                     f32x4 x = {0.f, 0.f, 0.f, 0.f};
                     for (int k = 0; k < (int)(P & 3); ++k) x[k] = X[row * ldx + q * 4 + k];
-                    v[j] = x;
+                    g.v[j] = x;
                 }
             }
         }
         if (t < R && c * R + t < N) {
-            fv = a[c * R + t];
-            if constexpr (SCORED) sv = s[c * R + t];
+            g.fv = a[c * R + t];
+            if constexpr (SCORED) g.sv = s[c * R + t];
         }
     };
-    auto stash = [&]() {
+    auto stash = [&](const Stage& g) {
 #pragma unroll
-        for (int j = 0; j < LQ; ++j) tile[t + j * NT] = v[j];
+        for (int j = 0; j < LQ; ++j) tile[t + j * NT] = g.v[j];
         if (t < R) {
-            fa[t] = fv;
-            if constexpr (SCORED) fs[t] = sv;
+            fa[t] = g.fv;
+            if constexpr (SCORED) fs[t] = g.sv;
         }
     };
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -360,23 +364,58 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     };
     const bool interior = q0 + TQ <= nq;
     const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
-    if (nfull > 0) {
-        load_full(0);
-        stash();
+    int64_t c = 0;  // next chunk to fold
+    if (DEPTH == 2 && nfull >= 4) {
+        // two chunks in flight: LDS holds chunk c, A = c+1 and B = c+2 are loading.
+        // The loop is peeled so that no load in it is conditional.
+        load_full(0, A);
+        stash(A);
         __syncthreads();
-        for (int64_t c = 0; c + 1 < nfull; ++c) {
-            load_full(c + 1);  // in flight while wave 0 folds chunk c
+        load_full(1, A);
+        load_full(2, B);
+        for (; c + 4 < nfull; c += 2) {
             fold(c, R);
             __syncthreads();  // chunk c consumed
-            stash();
+            stash(A);         // waits for A only; B stays in flight
+            __syncthreads();  // chunk c+1 staged
+            load_full(c + 3, A);
+            fold(c + 1, R);
+            __syncthreads();
+            stash(B);
+            __syncthreads();  // chunk c+2 staged
+            load_full(c + 4, B);
+        }
+        // LDS = c, A = c+1, B = c+2 (c + 2 < nfull <= c + 4)
+        fold(c, R);
+        __syncthreads();
+        stash(A);
+        __syncthreads();
+        fold(c + 1, R);
+        __syncthreads();
+        stash(B);
+        __syncthreads();
+        fold(c + 2, R);
+        __syncthreads();
+        c += 3;
+    } else if (nfull > 0) {
+        load_full(0, A);
+        stash(A);
+        __syncthreads();
+        for (; c + 1 < nfull; ++c) {
+            load_full(c + 1, A);  // in flight while wave 0 folds chunk c
+            fold(c, R);
+            __syncthreads();  // chunk c consumed
+            stash(A);
             __syncthreads();  // chunk c+1 staged
         }
-        fold(nfull - 1, R);
+        fold(c, R);
         __syncthreads();
+        ++c;
     }
-    for (int64_t c = nfull; c * R < N; ++c) {  // the rest, checked (no overlap)
-        load_checked(c);
-        stash();
+    for (; c * R < N; ++c) {  // the rest, checked (no overlap)
+        if (c < nfull) load_full(c, A);
+        else load_checked(c, A);
+        stash(A);
         __syncthreads();
         fold(c, (N - c * R) < R ? (int)(N - c * R) : R);
         __syncthreads();
@@ -963,6 +1002,10 @@ constexpr F32Variant kVariants[] = {
     // balanced grid-stride launches over column bands of <k> passes x CUs tiles (gsband<k>)
     {"gsband2_u8c4nt_nts", 8, 4, true}, {"gsband3_u8c4nt_nts", 8, 4, true}, {"gsband4_u8c4nt_nts", 8, 4, true},
     {"gsband3_u4c4nt_nts", 4, 4, true}, {"gsband6_u8c4nt_nts", 8, 4, true},
+    // LDS-staged with two chunks in flight per block (lds2_...)
+    {"lds2_w4r64t32", 0, 0, true}, {"lds2_w8r64t32", 0, 0, true}, {"lds2_w4r32t32", 0, 0, true},
+    {"lds2_w8r32t64", 0, 0, true}, {"lds2_w4r32t16", 0, 0, true}, {"lds2_w4r16t64", 0, 0, true},
+    {"lds2_w8r32t32", 0, 0, true}, {"lds2_w2r32t32", 0, 0, true}, {"lds2_w4r16t32", 0, 0, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -991,7 +1034,8 @@ int cu_count() {
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
-//   P < 256K params                    LDS-staged, 4 waves, 64-row chunks, 32-quad tiles
+//   P < 256K params                    LDS-staged, 4 waves, 32-row chunks, 16-quad tiles,
+//                                      two chunks in flight per block
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
@@ -1153,7 +1197,7 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 }
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
-template <int NW, int R, int TQ>
+template <int NW, int R, int TQ, int DEPTH = 1>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
     const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
@@ -1161,7 +1205,7 @@ int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
         return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
     const dim3 grid((unsigned)blocks), block(NW * 64);
 #define FA_L(SC, ACC, FIN)                                                                                   \
-    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN>), grid, block, 0, st, X, N, P, ldx, a, s, \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH>), grid, block, 0, st, X, N, P, ldx, a, s, \
                        acc_in, d, out)
     if (sc) {
         if (acc) { if (fin) FA_L(true, true, true); else FA_L(true, true, false); }
@@ -1213,13 +1257,15 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
     launch_gs_flags<U, C, true, B>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VBAND(K, U, C) \
     launch_gs_bands<U, C, true>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VL2(NW, R, TQ) \
+    launch_lds_flags<NW, R, TQ, 2>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
 #define FA_VL(NW, R, TQ) \
     launch_lds_flags<NW, R, TQ>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     int rc = FA_OK;
     switch (variant) {  // must match kVariants[]
         case 0:  // auto (pick_f32)
             switch (pick_f32(N, P)) {
-                case F32Pick::kLdsW4: rc = FA_VL(4, 64, 32); break;
+                case F32Pick::kLdsW4: rc = FA_VL2(4, 32, 16); break;
                 case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
                 case F32Pick::kGsBalC2: FA_VG(-1, 8, 2, true); break;
                 default: FA_VBAND(4, 8, 4); break;  // one band below 4 x CUs tiles
@@ -1293,6 +1339,15 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 67: FA_VBAND(4, 8, 4); break;
         case 68: FA_VBAND(3, 4, 4); break;
         case 69: FA_VBAND(6, 8, 4); break;
+        case 70: rc = FA_VL2(4, 64, 32); break;
+        case 71: rc = FA_VL2(8, 64, 32); break;
+        case 72: rc = FA_VL2(4, 32, 32); break;
+        case 73: rc = FA_VL2(8, 32, 64); break;
+        case 74: rc = FA_VL2(4, 32, 16); break;
+        case 75: rc = FA_VL2(4, 16, 64); break;
+        case 76: rc = FA_VL2(8, 32, 32); break;
+        case 77: rc = FA_VL2(2, 32, 32); break;
+        case 78: rc = FA_VL2(4, 16, 32); break;
         case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
@@ -1310,6 +1365,7 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #undef FA_VG
 #undef FA_VGB
 #undef FA_VBAND
+#undef FA_VL2
     if (rc) return rc;
     return check_launch("fold_f32");
 }

@@ -497,7 +497,7 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
 
 
 def _lds_variants(L):
-    return [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"lds_")]
+    return [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"lds")]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
