@@ -1123,11 +1123,16 @@ void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P,
                        N, P, ldx, a, s, acc_in, d, out, tiles);
 }
 
-template <int U, int C, bool NTS, int B = kBlock>
+// ALLF: instantiate every (scored, accumulate, finalize) combination -- only the
+// auto variant needs them (fa_fold_f32); tuning variants are always a plain
+// fold with the divide (acc == false, fin == true), so they instantiate two.
+template <int U, int C, bool NTS, int B = kBlock, bool ALLF = false>
 void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
 #define FA_G(SC, ACC, FIN) launch_gs<U, C, true, SC, ACC, FIN, NTS, B>(st, per_cu, X, N, P, ldx, a, s, acc_in, d, out)
-    if (sc) {
+    if constexpr (!ALLF) {
+        if (sc) FA_G(true, false, true); else FA_G(false, false, true);
+    } else if (sc) {
         if (acc) { if (fin) FA_G(true, true, true); else FA_G(true, true, false); }
         else     { if (fin) FA_G(true, false, true); else FA_G(true, false, false); }
     } else {
@@ -1143,7 +1148,7 @@ void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, co
 // boundaries re-align the blocks, which otherwise drift apart over many
 // passes (C3: 4 bands of 611 tiles, 5.80 ms, against 5.91 ms as one launch,
 // DESIGN.md 5).
-template <int U, int C, bool NTS>
+template <int U, int C, bool NTS, bool ALLF = false>
 void launch_gs_bands(hipStream_t st, int passes, bool sc, bool acc, bool fin, const float* X, int64_t N,
                      int64_t P, int64_t ldx, const float* a, const float* s, const float* acc_in, float d,
                      float* out) {
@@ -1157,7 +1162,7 @@ void launch_gs_bands(hipStream_t st, int passes, bool sc, bool acc, bool fin, co
         const int64_t c0 = b * band_tiles * tq * 4;  // first column of the band (a multiple of 4 KiB x C)
         if (c0 >= P) break;
         const int64_t pb = (P - c0) < band_tiles * tq * 4 ? (P - c0) : band_tiles * tq * 4;
-        launch_gs_flags<U, C, NTS>(st, -1, sc, acc, fin, N == 0 ? X : X + c0, N, pb, ldx, a, s,
+        launch_gs_flags<U, C, NTS, kBlock, ALLF>(st, -1, sc, acc, fin, N == 0 ? X : X + c0, N, pb, ldx, a, s,
                                    acc_in ? acc_in + c0 : nullptr, d, out + c0);
     }
 }
@@ -1179,13 +1184,10 @@ void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
         if constexpr (BAL) launch_balanced<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out); \
         else launch_v4<U, C, NT, SC, ACC, FIN, XR, NTS>(st, X, N, P, ldx, a, s, acc_in, d, out); \
     } while (0)
-    if (sc) {
-        if (acc) { if (fin) FA_V4(true, true, true); else FA_V4(true, true, false); }
-        else     { if (fin) FA_V4(true, false, true); else FA_V4(true, false, false); }
-    } else {
-        if (acc) { if (fin) FA_V4(false, true, true); else FA_V4(false, true, false); }
-        else     { if (fin) FA_V4(false, false, true); else FA_V4(false, false, false); }
-    }
+    // tuning variants only: a plain fold with the divide (see launch_gs_flags)
+    (void)acc;
+    (void)fin;
+    if (sc) FA_V4(true, false, true); else FA_V4(false, false, true);
 #undef FA_V4
 }
 
@@ -1197,7 +1199,7 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 }
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
-template <int NW, int R, int TQ, int DEPTH = 1>
+template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
     const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
@@ -1207,7 +1209,9 @@ int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
 #define FA_L(SC, ACC, FIN)                                                                                   \
     hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH>), grid, block, 0, st, X, N, P, ldx, a, s, \
                        acc_in, d, out)
-    if (sc) {
+    if constexpr (!ALLF) {
+        if (sc) FA_L(true, false, true); else FA_L(false, false, true);
+    } else if (sc) {
         if (acc) { if (fin) FA_L(true, true, true); else FA_L(true, true, false); }
         else     { if (fin) FA_L(true, false, true); else FA_L(true, false, false); }
     } else {
@@ -1262,13 +1266,26 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
 #define FA_VL(NW, R, TQ) \
     launch_lds_flags<NW, R, TQ>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
     int rc = FA_OK;
+    if (variant != 0 && (acc || !fin))
+        return fail(FA_ERR_ARG, "kernel variants are plain folds (no acc_in, finalize)");
     switch (variant) {  // must match kVariants[]
-        case 0:  // auto (pick_f32)
+        case 0:  // auto (pick_f32): every (scored, accumulate, finalize) combination
             switch (pick_f32(N, P)) {
-                case F32Pick::kLdsW4: rc = FA_VL2(4, 32, 16); break;
-                case F32Pick::kLdsW8: rc = FA_VL(8, 64, 32); break;
-                case F32Pick::kGsBalC2: FA_VG(-1, 8, 2, true); break;
-                default: FA_VBAND(4, 8, 4); break;  // one band below 4 x CUs tiles
+                case F32Pick::kLdsW4:
+                    rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor,
+                                                             out);
+                    break;
+                case F32Pick::kLdsW8:
+                    rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor,
+                                                             out);
+                    break;
+                case F32Pick::kGsBalC2:
+                    launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                              divisor, out);
+                    break;
+                default:  // one band below 4 x CUs tiles
+                    launch_gs_bands<8, 4, true, true>(st, 4, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+                    break;
             }
             break;
         case 1: FA_VF(4, 4, true); break;
