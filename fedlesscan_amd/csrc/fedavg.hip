@@ -1006,6 +1006,8 @@ constexpr F32Variant kVariants[] = {
     {"lds2_w4r64t32", 0, 0, true}, {"lds2_w8r64t32", 0, 0, true}, {"lds2_w4r32t32", 0, 0, true},
     {"lds2_w8r32t64", 0, 0, true}, {"lds2_w4r32t16", 0, 0, true}, {"lds2_w4r16t64", 0, 0, true},
     {"lds2_w8r32t32", 0, 0, true}, {"lds2_w2r32t32", 0, 0, true}, {"lds2_w4r16t32", 0, 0, true},
+    {"lds2_w4r64t16", 0, 0, true}, {"lds2_w8r64t16", 0, 0, true}, {"lds2_w2r32t16", 0, 0, true},
+    {"lds2_w4r32t8", 0, 0, true},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1034,17 +1036,18 @@ int cu_count() {
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
-//   P < 256K params                    LDS-staged, 4 waves, 32-row chunks, 16-quad tiles,
-//                                      two chunks in flight per block
+//   P < 256K params                    LDS-staged, 4 waves, two chunks in flight per block:
+//                                      32-row chunks of 16-quad tiles (16-row chunks of
+//                                      32-quad tiles for 32K-128K params)
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 4 passes x CUs tiles
 // all with non-temporal output stores.
-enum class F32Pick { kLdsW4, kLdsW8, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW4, kLdsW4T32, kLdsW8, kGsBalC2, kGsBalC4 };
 inline F32Pick pick_f32(int64_t N, int64_t P) {
     const int64_t nq = P >> 2, cus = cu_count();
-    if (nq < (1 << 16)) return F32Pick::kLdsW4;
+    if (nq < (1 << 16)) return nq >= (1 << 13) && nq < (1 << 15) ? F32Pick::kLdsW4T32 : F32Pick::kLdsW4;
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
     if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
@@ -1275,6 +1278,10 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
                     rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor,
                                                              out);
                     break;
+                case F32Pick::kLdsW4T32:
+                    rc = launch_lds_flags<4, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor,
+                                                             out);
+                    break;
                 case F32Pick::kLdsW8:
                     rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor,
                                                              out);
@@ -1365,6 +1372,10 @@ int fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, 
         case 76: rc = FA_VL2(8, 32, 32); break;
         case 77: rc = FA_VL2(2, 32, 32); break;
         case 78: rc = FA_VL2(4, 16, 32); break;
+        case 79: rc = FA_VL2(4, 64, 16); break;
+        case 80: rc = FA_VL2(8, 64, 16); break;
+        case 81: rc = FA_VL2(2, 32, 16); break;
+        case 82: rc = FA_VL2(4, 32, 8); break;
         case 47:  // v4_pickq_nts: the round-1 policy
             switch (pick_quads(P)) {
                 case 4: FA_VS(8, 4, false); break;
