@@ -99,3 +99,40 @@ def test_gpu_fold_properties(N, P, seed):
     for _ in range(N - 1):
         s = s + acc
     assert _bits(got, (s / np.float32(7 * N)).astype(np.float32))
+
+
+@pytest.mark.gpu
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(N=st.integers(60, 700), P=st.integers(1, 150_000), pad4=st.integers(0, 20), seed=st.integers(0, 2**32 - 1),
+       scored=st.booleans(), cut=st.floats(0.0, 1.0))
+def test_gpu_fold_many_clients(N, P, pad4, seed, scored, cut):
+    """Many clients on 16-B aligned rows: the LDS-staged folds' multi-chunk,
+    two-chunks-in-flight paths and their partial last chunk, as one fold and
+    as a two-part chunked continuation (fa_fold_f32), against the C oracle."""
+    from fedlesscan_amd import _lib
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    ldx = P + (-P) % 4 + 4 * pad4
+    X = synth.clients_f32(seed, N, 0, P)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
+    big = torch.zeros((N, ldx), dtype=torch.float32, device=dev)
+    big[:, :P] = torch.from_numpy(X).to(dev)
+    a = torch.tensor([float(np.float32(x)) for x in w], dtype=torch.float32, device=dev)
+    s = None if sc is None else torch.tensor([float(np.float32(x)) for x in sc], dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    out = torch.full((P,), float("nan"), device=dev)
+    _lib.check(L.fa_fedavg_f32(big.data_ptr(), N, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(), div,
+                               out.data_ptr(), stream), "fold")
+    assert _bits(out.cpu().numpy(), exp)
+    k = max(1, min(N - 1, int(cut * N)))  # rows [0, k) then [k, N), accumulator carried
+    acc = torch.full((P,), float("nan"), device=dev)
+    _lib.check(L.fa_fold_f32(big.data_ptr(), k, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(), None,
+                             div, 0, acc.data_ptr(), stream), "part 1")
+    _lib.check(L.fa_fold_f32(big[k].data_ptr(), N - k, P, ldx, a[k:].data_ptr(),
+                             None if s is None else s[k:].data_ptr(), acc.data_ptr(), div, 1, acc.data_ptr(),
+                             stream), "part 2")
+    assert _bits(acc.cpu().numpy(), exp)
