@@ -11,13 +11,19 @@
 // Bit-exactness contract: every output column is owned by
 // ONE lane, which folds clients 0..N-1 strictly in order with a separate
 // multiply and add (no FMA: this TU is compiled with fp-contract off) and
-// finishes with an IEEE divide.  No split-N, tree or atomic reassociation.
+// finishes with an IEEE divide.  No split-N, tree or atomic reassociation on
+// any default path (the opt-in fa_fedavg_f32_splitn is the one exception).
 //
 // Parallelism comes from the columns: lane = 4 consecutive fp32 columns
-// (one 16-byte global_load_dwordx4 per client row), a 64-lane wave reads
-// 1 KiB contiguous per row, a 256-thread block 4 KiB per row.  Memory-level
-// parallelism comes from unrolling U independent client-row loads ahead of
+// (one 16-byte global_load_dwordx4 per client row).  Memory-level
+// parallelism comes from U independent client-row loads in flight ahead of
 // the in-order adds (the loads are independent, only the adds are ordered).
+// Kernel families (the "auto" variant picks one by shape, pick_f32):
+//   k_fold_f32_gs    grid-stride over 16 KiB column tiles, ~1 block per CU,
+//                    balanced passes, launched per column band (large models)
+//   k_fold_f32_lds   LDS-staged: all waves stream client-row chunks of a
+//                    narrow column tile into LDS, wave 0 folds (narrow models)
+//   k_fold_f32_v4    one block per tile (the round-1 kernel; tuning variants)
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdint.h>
