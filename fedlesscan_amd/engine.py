@@ -148,7 +148,26 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
     return out
 
 
-def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[Sequence] = None, *,
+def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Tensor]:
+    """[N, P] view when the fp32 rows sit in ONE storage at a constant forward pitch.
+
+    A device-resident simulation usually hands over `X[i]` rows of one stacked
+    tensor (or equal-size slices of one buffer): then the stacked fold reads
+    them with ldx = pitch, with no pointer table to build and upload and with
+    the narrow-model (LDS-staged) kernels the pointer-list fold lacks."""
+    N = len(rows)
+    if N < 2 or P == 0:
+        return None
+    step = int(host_ptrs[1] - host_ptrs[0])
+    if step < P * 4 or step % 4:
+        return None
+    if (np.diff(host_ptrs) != step).any():
+        return None
+    base = rows[0]
+    sp = base.untyped_storage().data_ptr()
+    if any(r.untyped_storage().data_ptr() != sp for r in rows):
+        return None
+    return base.as_strided((N, P), (step // 4, 1))
               out: Optional[torch.Tensor] = None, total=None) -> torch.Tensor:
     """Same fold over separately allocated 1-D CUDA rows (no stacking copy for fp32)."""
     N = len(rows)
@@ -164,6 +183,9 @@ def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[
     f = Factors(weights, scores, np.dtype(np.float32), total=total)
     a, s = f.to(dev)
     host_ptrs = np.fromiter((r.data_ptr() for r in rows), dtype=np.int64, count=N)
+    view = _equal_stride_view(rows, host_ptrs, P)
+    if view is not None:  # rows of one allocation at a fixed pitch: the stacked fold, no pointer table
+        return fold_stacked(view, weights, scores, out=out, total=total)
     ptrs = torch.from_numpy(host_ptrs).to(dev)
     out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
     aligned = not (host_ptrs % 16).any() and out.data_ptr() % 16 == 0

@@ -224,6 +224,32 @@ def test_ptr_rows_equal_stacked(dev):
         assert _bits_equal(got, exp)
 
 
+@pytest.mark.parametrize("N,P,pitch", [(2, 1, 1), (23, 7001, 7001), (23, 7001, 7003), (300, 67267, 67328),
+                                       (64, 300_001, 300_001)])
+@pytest.mark.parametrize("scored", [False, True])
+@pytest.mark.parametrize("order", ["forward", "reversed"])
+def test_view_rows_of_one_buffer(dev, N, P, pitch, scored, order):
+    """Rows that are views of one buffer at a fixed pitch take the stacked fold
+    (engine._equal_stride_view); reversed rows take the pointer-list fold.
+    Both bit-equal to the oracle on the rows in the order given."""
+    from fedlesscan_amd import engine
+    X = synth.clients_f32(71 + N, N, 0, P)
+    w = synth.cardinalities(71 + N, N)
+    buf = torch.zeros(N * pitch + 3, dtype=torch.float32, device=dev)
+    B = buf[3:].as_strided((N, P), (pitch, 1))  # odd storage offset when pitch is odd: unaligned rows
+    B.copy_(torch.from_numpy(X))
+    idx = list(range(N)) if order == "forward" else list(range(N))[::-1]
+    rows = [B[i] for i in idx]
+    assert (engine._equal_stride_view(rows, np.array([r.data_ptr() for r in rows]), P) is not None) == \
+        (order == "forward")
+    sc = [(r + 1) / 11 for r in synth.round_ids(72, N, 10, 2)] if scored else None
+    got = engine.fold_rows(rows, [w[i] for i in idx], None if sc is None else [sc[i] for i in idx],
+                           out=_sentinel(P, dev)).cpu().numpy()
+    exp = OL.fedavg_f32(np.ascontiguousarray(X[idx]), np.array([w[i] for i in idx], np.float32),
+                        np.float32(sum(w)), s=None if sc is None else np.array([sc[i] for i in idx], np.float32))
+    assert _bits_equal(got, exp)
+
+
 @pytest.mark.parametrize("N,P", [(1, 1), (3, 5), (23, 4099), (9, 1024 * 256 + 6), (5, 4 * 1024 * 256 + 3),
                                  (17, 4 * 1024 * 256 * 2 + 1)])
 @pytest.mark.parametrize("scored", [False, True])
