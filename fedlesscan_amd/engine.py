@@ -168,6 +168,9 @@ def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Te
     if any(r.untyped_storage().data_ptr() != sp for r in rows):
         return None
     return base.as_strided((N, P), (step // 4, 1))
+
+
+def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[Sequence] = None, *,
               out: Optional[torch.Tensor] = None, total=None) -> torch.Tensor:
     """Same fold over separately allocated 1-D CUDA rows (no stacking copy for fp32)."""
     N = len(rows)
