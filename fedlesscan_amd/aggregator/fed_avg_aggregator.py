@@ -91,7 +91,11 @@ class FedAvgAggregator(ParameterAggregator):
 
     def select_aggregation_candidates(self, store, session_id, round_id):
         dicts, candidates = store.load_results_for_round(session_id=session_id, round_id=round_id)
-        if not dicts:
+        # The reference tests `if not round_candidates` (:51-54), and round_candidates
+        # is the generator _retrieve_result_files returns (client_daos.py:125,161):
+        # always truthy, so InsufficientClientResults is never raised here.  An empty
+        # round aggregates to [] and is saved as round R+1 with num_clients=0.
+        if not candidates:
             raise InsufficientClientResults(
                 f"Found no client results for session {session_id} and round {round_id}")
         return dicts, candidates

@@ -44,7 +44,8 @@ class StallAwareAggregator(ParameterAggregator):
     def select_aggregation_candidates(self, store, session_id, round_id):
         dicts, candidates = store.load_results_for_session(session_id=session_id, round_id=round_id,
                                                            tolerance=self.tolerance)
-        if not dicts:
+        # always-truthy generator, as in the reference (:76-79): see FedAvgAggregator
+        if not candidates:
             raise InsufficientClientResults(
                 f"Found no client results for session {session_id} and round {round_id}")
         return dicts, candidates

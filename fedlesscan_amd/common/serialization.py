@@ -51,12 +51,11 @@ class NpzWeightsSerializer:
         return WeightsSerializerConfig(type=p.type, params=p)
 
     def serialize(self, weights: List[np.ndarray]) -> bytes:
-        try:
-            with io.BytesIO() as f:
-                (np.savez_compressed if self.compressed else np.savez)(f, *weights)
-                return f.getvalue()
-        except (ValueError, IOError) as e:
-            raise SerializationError(e) from e
+        # not wrapped: only deserialize carries wrap_exceptions_as_serialization_error
+        # (serialization.py:292-306), so e.g. serialize(None) raises TypeError
+        with io.BytesIO() as f:
+            (np.savez_compressed if self.compressed else np.savez)(f, *weights)
+            return f.getvalue()
 
     def deserialize(self, blob: bytes) -> List[np.ndarray]:
         try:

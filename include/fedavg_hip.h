@@ -41,7 +41,9 @@ extern "C" {
 enum fa_status {
     FA_OK = 0,
     FA_ERR_ARG = 1,        /* bad size/pointer/stride -> ValueError                          */
-    FA_ERR_NO_CLIENTS = 2, /* N == 0 -> InsufficientClientResults (fed_avg_aggregator.py:51-54) */
+    FA_ERR_NO_CLIENTS = 2, /* N == 0 -> InsufficientClientResults.  ABI guard only: the strategies never
+                              fold zero rows (an empty round aggregates to [] on the host, as the
+                              reference's _aggregate does: fed_avg_aggregator.py:31-42) */
     FA_ERR_SHAPE = 3,      /* -> InvalidParameterShapeError (exceptions.py:13)                  */
     FA_ERR_HIP = 4,        /* launch / runtime failure -> AggregationError (exceptions.py:1)    */
 };

@@ -306,7 +306,193 @@ def case_edges():
     record_outputs(case, "fedavg", fa.FedAvgAggregator()._aggregate([[X[i]] for i in range(9)], cards))
 
 
+# ---------------------------------------------------------------------------
+# 6. the reference's whole default_aggregation_handler (aggregation.py:45-167)
+#    over an in-memory stand-in for MongoDB + GridFS: selection order, the
+#    `$gte R-tol` filter, counts, delete-after, the saved round R+1 model, and
+#    the empty round (the `if not round_candidates` check never fires, because
+#    round_candidates is a generator: fed_avg_aggregator.py:51, client_daos.py:125)
+# ---------------------------------------------------------------------------
+def _match(doc, flt):
+    for k, v in (flt or {}).items():
+        if isinstance(v, dict):
+            if set(v) != {"$gte"}:
+                raise NotImplementedError(v)
+            if not (k in doc and doc[k] >= v["$gte"]):
+                return False
+        elif doc.get(k) != v:
+            return False
+    return True
+
+
+class _FakeCollection:
+    """The pymongo Collection calls client_daos.py makes, in insertion order."""
+
+    def __init__(self):
+        self.docs = []
+
+    def find(self, filter=None, **kw):
+        return iter([dict(d) for d in self.docs if _match(d, filter)])
+
+    def find_one(self, filter=None, **kw):
+        return next(self.find(filter), None)
+
+    def replace_one(self, flt, doc, upsert=False):
+        for i, d in enumerate(self.docs):
+            if _match(d, flt):
+                self.docs[i] = dict(doc)
+                return
+        if upsert:
+            self.docs.append(dict(doc))
+
+    def delete_many(self, filter):
+        self.docs = [d for d in self.docs if not _match(d, filter)]
+
+    def count_documents(self, filter):
+        return sum(1 for d in self.docs if _match(d, filter))
+
+
+class _FakeDb(dict):
+    def __init__(self):
+        super().__init__()
+        self.files = {}
+
+    def __missing__(self, name):
+        c = self[name] = _FakeCollection()
+        return c
+
+
+class _FakeClient:
+    def __init__(self):
+        self.dbs = {}
+
+    def __getitem__(self, name):
+        return self.dbs.setdefault(name, _FakeDb())
+
+    def close(self):
+        pass
+
+
+class _FakeFile:
+    def __init__(self, data):
+        self.data = data
+
+    def read(self):
+        return self.data
+
+    def close(self):
+        pass
+
+
+class _FakeGridFS:
+    def __init__(self, db):
+        self.files = db.files
+
+    def put(self, data, **kw):
+        fid = f"f{len(self.files)}"
+        self.files[fid] = bytes(data)
+        return fid
+
+    def find_one(self, q):
+        d = self.files.get(q["_id"])
+        return None if d is None else _FakeFile(d)
+
+    def delete(self, file_id):
+        self.files.pop(file_id, None)
+
+
+def _import_handler():
+    from unittest import mock
+    # benchmark_configurator pulls in tf.keras model builders; the handler uses it
+    # only for global evaluation (test_data), which these cases leave at None
+    sys.modules.setdefault("fedless.datasets.benchmark_configurator", mock.MagicMock(name="benchmark_configurator"))
+    import fedless.aggregator.aggregation as agg
+    import fedless.common.persistence.client_daos as cd
+    return agg, cd
+
+
+HANDLER_SHAPES = [(4, 6), (6,), (3, 1, 2)]
+
+
+def case_handler():
+    """Scenarios run through the unmodified reference handler.  Manifest entry per
+    scenario: the stored documents (session, round, client, synth row, cardinality,
+    optional metrics), the handler arguments and everything the handler returned or
+    left behind."""
+    from unittest import mock
+    agg, cd = _import_handler()
+    seed, rows = 31, 40
+    P = sum(int(np.prod(s)) for s in HANDLER_SHAPES)
+    X = synth.clients_f32(seed, rows, 0, P)
+    cards = synth.cardinalities(seed, rows, 1, 600)
+    docs_round = ([("s", 3, f"c{i}", i, cards[i]) for i in range(6)] +
+                  [("s", 2, f"old{i}", 6 + i, cards[6 + i]) for i in range(2)] +
+                  [("other", 3, "x0", 8, cards[8])])
+    docs_session = ([("s", 7, "stale", 9, cards[9])] +
+                    [("s", 8 + (i % 3), f"c{i}", 10 + i, cards[10 + i]) for i in range(7)] +
+                    [("other", 10, "x0", 17, cards[17])])
+    docs_online = [("s", 10 - (i % 3), f"c{i}", i, cards[i]) for i in range(30)]
+    docs_metrics = [("s", 5, f"c{i}", 20 + i, cards[20 + i], (100 + i, {"loss": 0.5 + i, "accuracy": 0.25 * i}))
+                    for i in range(3)] + [("s", 5, "c3", 23, cards[23])]
+    scenarios = [
+        ("per_round", docs_round, 3, "per_round", {}, True),
+        ("per_round_keep", docs_round, 3, "per_round", {}, False),
+        ("per_session_tol2", docs_session, 10, "per_session", {"tolerance": 2}, True),
+        ("per_session_tol0", docs_session, 10, "per_session", {"tolerance": 0}, True),
+        ("online_per_round", docs_online, 10, "per_round", {"aggregate_online": True}, True),
+        ("online_per_session", docs_online, 10, "per_session", {"tolerance": 2, "aggregate_online": True}, True),
+        ("metrics", docs_metrics, 5, "per_round", {}, True),
+        ("empty_per_round", docs_round, 4, "per_round", {}, True),
+        ("empty_per_session", [], 4, "per_session", {"tolerance": 2}, True),
+        ("empty_online", [], 4, "per_round", {"aggregate_online": True}, True),
+    ]
+    case = "handler"
+    MANIFEST[case] = {"kind": "handler", "seed": seed, "rows": rows, "P": P,
+                      "shapes": [list(s) for s in HANDLER_SHAPES], "X_sha256": sha(X), "scenarios": {},
+                      "source": "reference fedless/aggregator/aggregation.py:45-167 over an in-memory Mongo/GridFS"}
+    ser_cfg = models.WeightsSerializerConfig(type="npz", params=models.NpzWeightsSerializerConfig())
+    for name, docs, R, strategy, hp_kw, delete in scenarios:
+        client = _FakeClient()
+        with mock.patch.object(cd, "GridFS", _FakeGridFS):
+            dao = cd.ClientResultDao(client)
+            for d in docs:
+                sess, rnd, cid, row, card = d[:5]
+                tm = None if len(d) < 6 else models.TestMetrics(cardinality=d[5][0], metrics=d[5][1])
+                blob = ser.NpzWeightsSerializer().serialize(split_layers(X[row], HANDLER_SHAPES))
+                cr = models.ClientResult(parameters=models.SerializedParameters(blob=blob, serializer=ser_cfg),
+                                         cardinality=card, test_metrics=tm)
+                dao.save(session_id=sess, round_id=rnd, client_id=cid, result=cr)
+            entry = {"docs": [list(d[:5]) + ([list(d[5])] if len(d) > 5 else []) for d in docs],
+                     "round_id": R, "strategy": strategy, "hyperparams": hp_kw, "delete": delete}
+            with mock.patch.object(agg.pymongo, "MongoClient", return_value=client):
+                try:
+                    res = agg.default_aggregation_handler(
+                        "s", R, models.MongodbConnectionConfig(host="h", port=1, username="u", password="p"),
+                        ser_cfg, None, delete, models.AggregationStrategy(strategy),
+                        models.AggregationHyperParams(**hp_kw))
+                except Exception as e:  # the reference's own failure, recorded as the expected outcome
+                    entry["raises"] = type(e).__name__
+                    MANIFEST[case]["scenarios"][name] = entry
+                    continue
+            saved = cd.ParameterDao(client).load(session_id="s", round_id=R + 1)
+        outs = ser.NpzWeightsSerializer().deserialize(saved.blob)
+        entry.update({
+            "new_round_id": res.new_round_id, "num_clients": res.num_clients,
+            "test_results": None if res.test_results is None else [t.dict() for t in res.test_results],
+            "global_test_results": res.global_test_results,
+            "saved_round_ids": sorted(d["round_id"] for d in client["fedless"]["parameters"].docs),
+            "saved_blob_len": len(saved.blob),
+            "saved_blob_sha256": hashlib.sha256(saved.blob).hexdigest() if not outs else None,
+            "remaining_results": sorted([d["session_id"], d["round_id"], d["client_id"]]
+                                        for d in client["fedless"]["results"].docs),
+            "remaining_files": len(client["fedless"].files) - 1,  # minus the saved model
+        })
+        MANIFEST[case]["scenarios"][name] = entry
+        record_outputs(case, name, outs)
+
+
 def main():
+    case_handler()
     case_ref_fixture()
     case_f32_small()
     case_stacked("f32_n60", 12, 60, 4096, streams=True)

@@ -62,7 +62,7 @@ def parameters(case: str):
 
 def stacked(case: str) -> np.ndarray:
     m = manifest()[case]
-    return synth.clients_f32(m["seed"], m["n_clients"], 0, m["P"])
+    return synth.clients_f32(m["seed"], m.get("n_clients", m.get("rows")), 0, m["P"])
 
 
 def expected(case: str, prefix: str):

@@ -239,12 +239,16 @@ def test_handler_per_session_tolerance(oracle_fold):
     assert st.count_results_for_session("s") == 0
 
 
-def test_handler_no_results_raises(oracle_fold):
-    from fedlesscan_amd import InsufficientClientResults
+def test_handler_no_results_saves_empty_model(oracle_fold):
+    # the reference never raises InsufficientClientResults at selection (it tests a
+    # generator's truthiness, fed_avg_aggregator.py:51-54): an empty round saves []
+    # at R+1 and reports num_clients=0 (pinned in test_handler_golden.py)
     from fedlesscan_amd.handler import default_aggregation_handler
     cfg = WeightsSerializerConfig(type="npz", params=NpzWeightsSerializerConfig())
-    with pytest.raises(InsufficientClientResults):
-        default_aggregation_handler("s", 1, InMemoryClientResultStore(), InMemoryParameterStore(), cfg)
+    ps = InMemoryParameterStore()
+    res = default_aggregation_handler("s", 1, InMemoryClientResultStore(), ps, cfg)
+    assert res.new_round_id == 2 and res.num_clients == 0 and res.test_results is None
+    assert NpzWeightsSerializer().deserialize(ps.load("s", 2).blob) == []
 
 
 def test_handler_online_uses_stream_variant(oracle_fold):
@@ -483,11 +487,16 @@ def test_openfaas_entry_point(oracle_fold):
     body = json.loads(resp["body"])
     assert body == {"new_round_id": 4, "num_clients": 4, "test_results": None, "global_test_results": None}
     assert ps.load("s", 4) is not None
-    # the round's results were deleted (delete_results_after_finish default): a second call finds none
+    # the round's results were deleted (delete_results_after_finish default): a second
+    # call finds none and, as in the reference, saves an empty model with num_clients 0
     resp = handle(Event(json.dumps(REF_REQUEST)), None)
+    assert resp["statusCode"] == 200
+    assert json.loads(resp["body"]) == {"new_round_id": 4, "num_clients": 0, "test_results": None,
+                                        "global_test_results": None}
+    # an error -> 400 {errorMessage, errorType, details} (providers.py:25-40)
+    resp = handle(Event(json.dumps(dict(REF_REQUEST, aggregation_strategy="bogus"))), None)
     err = json.loads(resp["body"])
-    assert resp["statusCode"] == 400 and err["errorType"] == "InsufficientClientResults"
-    assert set(err) == {"errorMessage", "errorType", "details"}
+    assert resp["statusCode"] == 400 and set(err) == {"errorMessage", "errorType", "details"}
     # malformed request -> pydantic ValidationError -> 400
     bad = dict(REF_REQUEST)
     del bad["round_id"]
