@@ -112,17 +112,17 @@ class Workload:
         self.slots = self.layout.slots(rank)
         self.P = sum(hi - lo for lo, hi in self.slots)  # real columns this rank folds
         self.rank, self.world, self.dev = rank, world, dev
-        L = _lib.load()
+        B = _lib.load_bench()  # input generator (bench / test support library)
         st = torch.cuda.current_stream(dev).cuda_stream
         tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
         sub, W = self.layout.sub, self.layout.local_width
         self.X = torch.zeros((self.N, W), dtype=tdt, device=dev)
-        gen = L.fa_synth_f32 if self.dtype == "f32" else L.fa_synth_bf16
+        gen = B.fa_synth_f32 if self.dtype == "f32" else B.fa_synth_bf16
         esz = self.X.element_size()
         for k, (lo, hi) in enumerate(self.slots):
             if hi > lo:
                 _lib.check(gen(self.X.data_ptr() + k * sub * esz, self.N, hi - lo, W, self.seed, 0, lo, st),
-                           "synth")
+                           "synth", bench=True)
         self.col0 = self.slots[0][0]
         self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
         self.scores = ([(r + 1) / 11 for r in synth.round_ids(self.seed, self.N, 10, 2)]
@@ -131,28 +131,40 @@ class Workload:
         self.a, self.s = f.to(dev)
         self.div = float(f.div)
         self.out = torch.empty(W, dtype=torch.float32, device=dev)  # this rank's slots, side by side
+        # bf16 models also write the RNE bf16 copy of the result (the form the
+        # multi-GPU gather moves: half the xGMI bytes of the fp32 result)
+        self.out_bf16 = torch.empty(W, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else None
         elt = 4 if self.dtype == "f32" else 2
         # algorithmic bytes per step on this rank: every real input element once + the fp32 output once
         self.bytes = self.N * self.P * elt + self.P * 4
         torch.cuda.synchronize()
 
     def launch(self, variant=0, k=0):
-        """Fold round k's slot (all of X when rounds == 1)."""
+        """Fold round k's slot (all of X when rounds == 1).  variant 0 is the
+        product entry point (fa_fedavg_f32 / fa_fedavg_bf16 of libfedavg_hip.so);
+        others come from the tuning library."""
         L = _lib.load()
         st = torch.cuda.current_stream(self.dev).cuda_stream
         s = None if self.s is None else self.s.data_ptr()
         sub, W = self.layout.sub, self.layout.local_width
         x = self.X.data_ptr() + k * sub * self.X.element_size()
         o = self.out.data_ptr() + k * sub * 4
+        ob = None if self.out_bf16 is None else self.out_bf16.data_ptr() + k * sub * 2
+        bench = variant > 0
         if self.dtype == "f32" and variant < 0:  # opt-in split-client fold
             rc = L.fa_fedavg_f32_splitn(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st)
+        elif self.dtype == "f32" and variant == 0:
+            rc = L.fa_fedavg_f32(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st)
         elif self.dtype == "f32":
-            rc = L.fa_fedavg_f32_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st, variant)
+            rc = _lib.load_bench().fa_fedavg_f32_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st,
+                                                         variant)
+        elif variant == 0:
+            rc = L.fa_fedavg_bf16(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, ob, st)
         else:
-            rc = L.fa_fedavg_bf16_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, None, st,
-                                          variant)
+            rc = _lib.load_bench().fa_fedavg_bf16_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o,
+                                                          ob, st, variant)
         if rc:
-            _lib.check(rc, "fold")
+            _lib.check(rc, "fold", bench=bench)
 
 
 def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
@@ -226,15 +238,15 @@ def main():
     if args.splitn:
         args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds)
-    L = _lib.load()
+    B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32, device=dev) if world > 1 else None
     gloo = world > 1 and dist.get_backend() == "gloo"
     stream = torch.cuda.current_stream(dev)
 
     if args.sweep and rank == 0:
-        nvar = L.fa_num_variants() if wl.dtype == "f32" else L.fa_num_bf16_variants()
-        vname = L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name
+        nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()
+        vname = B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name
         res = {v: [] for v in range(nvar)}
         for _ in range(2):
             for v in range(nvar):
@@ -321,8 +333,8 @@ def main():
     for k in range(max(3, min(args.steps, 10)) + 2):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        _lib.check(L.fa_read_sweep_f32(wl.X.data_ptr(), nfl - nfl % 4, sink.data_ptr(), 8192,
-                                       stream.cuda_stream), "read_sweep")
+        _lib.check(B.fa_read_sweep_f32(wl.X.data_ptr(), nfl - nfl % 4, sink.data_ptr(), 8192,
+                                       stream.cuda_stream), "read_sweep", bench=True)
         e1.record(stream)
         e1.synchronize()
         if k >= 2:
@@ -368,7 +380,7 @@ def main():
                     f" + RCCL all_gather in {rounds} rounds overlapped with the fold" if world > 1 else ""),
                 "rounds": rounds,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
-                (L.fa_variant_name if wl.dtype == "f32" else L.fa_bf16_variant_name)(args.variant).decode(),
+                (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
             },
             "roofline": {
                 "bound": "hbm",

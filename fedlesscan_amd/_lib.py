@@ -1,4 +1,6 @@
-"""ctypes binding of libfedavg_hip.so (declarations: include/fedavg_hip.h).
+"""ctypes binding of libfedavg_hip.so (declarations: include/fedavg_hip.h)
+and of the bench / tuning library libfedavg_hip_bench.so
+(include/fedavg_hip_bench.h), which only bench.py and the tests load.
 
 No fallback: if the library is missing or a call fails, this raises.  The
 product path never computes an aggregate on the CPU.
@@ -19,8 +21,10 @@ from .aggregator.exceptions import (
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip.so")
+BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
-ABI_VERSION = 1
+BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
+ABI_VERSION = 2
 
 FA_OK, FA_ERR_ARG, FA_ERR_NO_CLIENTS, FA_ERR_SHAPE, FA_ERR_HIP = range(5)
 
@@ -45,15 +49,6 @@ _PROTOS = {
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i64": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
-    "fa_synth_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _vp]),
-    "fa_synth_bf16": (_int, [_vp, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _vp]),
-    "fa_read_sweep_f32": (_int, [_vp, _i64, _vp, _i64, _vp]),
-    "fa_fedavg_f32_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
-    "fa_num_variants": (_int, []),
-    "fa_variant_name": (ctypes.c_char_p, [_int]),
-    "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
-    "fa_num_bf16_variants": (_int, []),
-    "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
     "fa_npz_index": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int]),
     "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
     "fa_bson_elements": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
@@ -64,33 +59,52 @@ _PROTOS = {
     "fa_copy_h2d": (_int, [_vp, _vp, _i64, _vp]),
 }
 
+# libfedavg_hip_bench.so (include/fedavg_hip_bench.h)
+_BENCH_PROTOS = {
+    "fa_bench_last_error": (ctypes.c_char_p, []),
+    "fa_synth_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _vp]),
+    "fa_synth_bf16": (_int, [_vp, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _vp]),
+    "fa_read_sweep_f32": (_int, [_vp, _i64, _vp, _i64, _vp]),
+    "fa_fedavg_f32_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
+    "fa_num_variants": (_int, []),
+    "fa_variant_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
+    "fa_num_bf16_variants": (_int, []),
+    "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
+}
+
 _lock = threading.Lock()
 _lib = None
+_bench = None
 
 
-def header_functions() -> list[str]:
-    """Every `fa_*(` function declared in include/fedavg_hip.h."""
-    with open(HEADER) as f:
+def header_functions(header: str = HEADER) -> list[str]:
+    """Every `fa_*(` function declared in a header (default include/fedavg_hip.h)."""
+    with open(header) as f:
         text = f.read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", text)))
 
 
+def _open(p: str, protos: dict):
+    if not os.path.exists(p):
+        raise AggregationError(
+            f"HIP extension not built: {p} missing (run `python -m fedlesscan_amd.native_build`)")
+    L = ctypes.CDLL(p)
+    for name, (res, args) in protos.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def load(path: str | None = None):
-    """Load and type the library (idempotent).  Raises if it is absent."""
+    """Load and type the product library (idempotent).  Raises if it is absent."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
-        if not os.path.exists(p):
-            raise AggregationError(
-                f"HIP extension not built: {p} missing (run `python -m fedlesscan_amd.native_build`)")
-        L = ctypes.CDLL(p)
-        for name, (res, args) in _PROTOS.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
+        L = _open(path or LIB_PATH, _PROTOS)
         v = L.fa_abi_version()
         if v != ABI_VERSION:
             raise AggregationError(f"libfedavg_hip ABI {v} != expected {ABI_VERSION}")
@@ -98,15 +112,26 @@ def load(path: str | None = None):
         return L
 
 
+def load_bench(path: str | None = None):
+    """Load and type the bench / tuning library (bench.py and tests only)."""
+    global _bench
+    with _lock:
+        if _bench is None:
+            _bench = _open(path or BENCH_LIB_PATH, _BENCH_PROTOS)
+        return _bench
+
+
 def last_error() -> str:
     return load().fa_last_error().decode(errors="replace")
 
 
-def check(rc: int, what: str) -> None:
-    """Map a C-ABI status onto the reference's exception classes."""
+def check(rc: int, what: str, bench: bool = False) -> None:
+    """Map a C-ABI status onto the reference's exception classes.  bench=True:
+    the status came from libfedavg_hip_bench.so (its own error string)."""
     if rc == FA_OK:
         return
-    msg = f"{what}: {last_error()}"
+    err = load_bench().fa_bench_last_error().decode(errors="replace") if bench else last_error()
+    msg = f"{what}: {err}"
     if rc == FA_ERR_NO_CLIENTS:
         raise InsufficientClientResults(msg)
     if rc == FA_ERR_SHAPE:

@@ -1,0 +1,381 @@
+// libfedavg_hip_bench.so — bench and tuning support, NOT the product ABI
+// (include/fedavg_hip_bench.h): the integer-exact synthetic generator that
+// fills HBM for bench.py and the GPU tests, the streaming-read calibration
+// kernel, and the kernel-variant sweep entry points (variant 0 = the product's
+// auto fold, the rest = alternatives kept for `bench.py --sweep`).  Shares the
+// kernels of fold_kernels.hpp with libfedavg_hip.so.
+#include "fold_kernels.hpp"
+#include "fedavg_hip_bench.h"
+
+namespace {
+
+// Bijective blockIdx remap that gives each of the 8 XCDs (blocks b and b+8
+// share one under round-robin dispatch) a contiguous range of column tiles.
+// Placement is a speed hint only; any placement gives the same result.
+__device__ __forceinline__ int64_t xcd_contiguous(int64_t b, int64_t n) {
+    const int64_t q = n / 8, r = n % 8, x = b % 8, k = b / 8;
+    return x * q + (x < r ? x : r) + k;
+}
+
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool XR = false, bool NTS = false>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_v4(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    const int64_t bid = XR ? xcd_contiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    fold_tile<U, C, NT, SCORED, ACC, FIN, NTS>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+}
+
+// Balanced persistent form: the grid is the resident capacity (occupancy x
+// CUs) and block b owns the contiguous quad range [b*per, (b+1)*per), per =
+// ceil(nq / grid): every CU streams the same number of bytes, so there is no
+// partly-filled last wave of blocks.  Inside its range a block walks tiles of
+// C*kBlock quads; the same fold_quads body does the work.
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_balanced(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t per) {  // acc_in may alias out
+    const int64_t nq = P >> 2;
+    const int64_t ldq = ldx >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < nq ? lo + per : nq;
+    int64_t q0 = lo + threadIdx.x;
+    for (; q0 + (int64_t)(C - 1) * kBlock < hi; q0 += (int64_t)C * kBlock)
+        fold_quads<U, C, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+    for (; q0 < hi; q0 += kBlock)
+        fold_quads<U, 1, NT, SCORED, ACC, FIN>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor, O4 + q0);
+    if ((P & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) {
+        for (int64_t col = nq * 4; col < P; ++col) {
+            float acc;
+            int64_t i = 0;
+            if constexpr (ACC) {
+                acc = acc_in[col];
+            } else {
+                acc = term1<SCORED>(X[col], a[0], SCORED ? s[0] : 1.0f);
+                i = 1;
+            }
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
+            if constexpr (FIN) acc = acc / divisor;
+            out[col] = acc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic generator (bit-identical to fedlesscan_amd/synth.py)
+// ---------------------------------------------------------------------------
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float synth_value(uint64_t key, int64_t col) {
+    uint64_t h = mix64(key + (uint64_t)(col + 1) * kGolden);
+    int64_t v = (int64_t)(h & 0x1FFFFF) + (int64_t)((h >> 21) & 0x1FFFFF) +
+                (int64_t)((h >> 42) & 0x1FFFFF) - 3 * (1 << 20);
+    return (float)v * 0x1p-24f;
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(kBlock) void k_synth(OutT* __restrict__ X, int64_t nrows, int64_t ncols,
+                                                   int64_t ldx, uint64_t seed, int64_t row0, int64_t col0) {
+    const int64_t total = nrows * ncols;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = e / ncols;
+        const int64_t c = e - r * ncols;
+        const uint64_t key = mix64((seed * kGolden) ^ mix64((uint64_t)(row0 + r) + 1));
+        const float v = synth_value(key, col0 + c);
+        if constexpr (sizeof(OutT) == 4) X[r * ldx + c] = v;
+        else X[r * ldx + c] = f2bf_rne(v);
+    }
+}
+
+// Contiguous streaming read (calibration ceiling for the fold): block b reads
+// its own contiguous 64 KiB chunk (16 independent 16-byte non-temporal loads
+// per lane, all issued before the first use), the fastest pure-read pattern
+// measured on MI355X (tools/hbm_probe.hip "chunk nt 64 KiB/block").
+constexpr int kSweepQuads = 16 * kBlock;  // 64 KiB per block
+__global__ __launch_bounds__(kBlock) void k_read_sweep(const f32x4* __restrict__ X, int64_t nq,
+                                                        float* __restrict__ sink, int64_t sink_len) {
+    const int64_t q0 = (int64_t)blockIdx.x * kSweepQuads + threadIdx.x;
+    f32x4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int64_t q = q0 + (int64_t)k * kBlock;
+        v[k] = q < nq ? __builtin_nontemporal_load(X + q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    f32x4 acc = v[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) acc = add4(acc, v[k]);
+    float t = acc.x + acc.y + acc.z + acc.w;
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    __shared__ float red[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) sink[blockIdx.x % sink_len] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Variant 0 is the product's auto fold (fold_f32_auto); the others are the
+// alternatives whose sweeps chose it (profiles/r01_sweep_*.log).
+// Names: u<rows ahead>c<quads per lane>, nt = non-temporal loads, _nts =
+// non-temporal output stores; gs<k> grid-stride with k blocks per CU, gsbal
+// balanced passes, gsq<n> n blocks, gsband<k> column bands of k passes;
+// lds[2]_w<waves>r<rows per chunk>t<quads per block> LDS-staged (2 = two chunks
+// in flight); bal_ balanced persistent grid; xcd_ XCD-contiguous block order.
+constexpr const char* kVariants[] = {
+    "auto",
+    // one block per tile (the round-1 row-streaming kernel)
+    "u8c4nt", "u4c1nt", "xcd_u8c4nt", "v4_pickq_nts", "bal_u4c4nt",
+    // grid-stride over 16 KiB tiles
+    "gs1_u8c4nt_nts", "gs2_u8c4nt_nts", "gs1_u4c8nt_nts", "gs1b512_u8c2nt_nts",
+    "gsbal_u8c4nt_nts", "gsbal_u8c2nt_nts", "gsq192_u8c4nt_nts",
+    "gsband2_u8c4nt_nts", "gsband3_u8c4nt_nts", "gsband4_u8c4nt_nts", "gsband6_u8c4nt_nts",
+    // LDS-staged narrow folds
+    "lds_w8r64t32", "lds_w4r64t64", "lds_w16r128t64",
+    "lds2_w4r32t16", "lds2_w4r16t32", "lds2_w4r64t32", "lds2_w8r32t32", "lds2_w4r32t8", "lds2_w2r32t16",
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// Quads per lane of the round-1 row-streaming policy (variant "v4_pickq_nts"):
+// the widest per-block row run (C * 4 KiB) that still leaves >= ~1000 blocks.
+inline int pick_quads(int64_t P) {
+    const int64_t nq = P >> 2;
+    if (nq / (4 * kBlock) >= 1000) return 4;
+    if (nq / (2 * kBlock) >= 1000) return 2;
+    return 1;
+}
+
+constexpr const char* kBf16Variants[] = {
+    "bf16auto",
+    // one block per tile, u<rows ahead>c<octets per lane>
+    "bf16u8c1", "bf16u8c2", "bf16u2c8",
+    // grid-stride (gs1: one block per CU; gsbal: balanced passes)
+    "bf16gs1u8c2", "bf16gs1u8c4", "bf16gsbalu8c2", "bf16gsbalu2c8",
+    // column bands of <k> passes
+    "bf16band2u2c8", "bf16band4u2c8", "bf16band4u8c2",
+};
+constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
+
+
+// Resident blocks of one balanced-kernel instantiation on the current device
+// (occupancy API x CU count), cached per (instantiation, device).  The guide
+// notes the API can over-report by one block per CU for SGPR-heavy 256-thread
+// kernels; for a plain (non-cooperative) launch that only costs balance.
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
+int resident_blocks() {
+    static thread_local int cache[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cache[dev] > 0) return cache[dev];
+    int cus = 256, per_cu = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fold_f32_balanced<U, C, NT, SC, ACC, FIN>, kBlock,
+                                                     0) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 4;
+    cache[dev] = cus * per_cu;
+    return cache[dev];
+}
+
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN>
+void launch_balanced(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                     const float* s, const float* acc_in, float d, float* out) {
+    auto kern = k_fold_f32_balanced<U, C, NT, SC, ACC, FIN>;
+    const int64_t nq = P >> 2;
+    int64_t grid = resident_blocks<U, C, NT, SC, ACC, FIN>();
+    const int64_t tiles = (nq + kBlock - 1) / kBlock;  // never more blocks than 256-quad tiles
+    if (grid > tiles) grid = tiles > 0 ? tiles : 1;
+    const int64_t per = grid > 0 ? (nq + grid - 1) / grid : 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, ldx, a, s, acc_in, d, out, per);
+}
+
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool XR = false, bool NTS = false>
+void launch_v4(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+               const float* s, const float* acc_in, float d, float* out) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const dim3 grid((unsigned)((units + per_block - 1) / per_block));  // incl. the column-tail lane
+    hipLaunchKernelGGL((k_fold_f32_v4<U, C, NT, SC, ACC, FIN, XR, NTS>), grid, dim3(kBlock), 0,
+                       st, X, N, P, ldx, a, s, acc_in, d, out);
+}
+
+template <int U, int C, bool NT, bool BAL = false, bool XR = false, bool NTS = false>
+void launch_v4_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+#define FA_V4(SC, ACC, FIN)                                                                   \
+    do {                                                                                      \
+        if constexpr (BAL) launch_balanced<U, C, NT, SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, d, out); \
+        else launch_v4<U, C, NT, SC, ACC, FIN, XR, NTS>(st, X, N, P, ldx, a, s, acc_in, d, out); \
+    } while (0)
+    // tuning variants only: a plain fold with the divide (see launch_gs_flags)
+    (void)acc;
+    (void)fin;
+    if (sc) FA_V4(true, false, true); else FA_V4(false, false, true);
+#undef FA_V4
+}
+
+int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                     float divisor, float* out, void* stream, int variant) {
+    if (variant < 0 || variant >= kNumVariants) return fail(FA_ERR_ARG, "unknown variant %d", variant);
+    if (variant == 0) return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream);
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(X) || (ldx % 4) || !aligned16(out))
+        return fail(FA_ERR_ARG, "kernel variants need 16-B aligned X and out and ldx %% 4 == 0");
+    hipStream_t st = (hipStream_t)stream;
+    const bool sc = s != nullptr, acc = false, fin = true;
+    const float* acc_in = nullptr;
+#define FA_VF(U, C) launch_v4_flags<U, C, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VB(U, C) launch_v4_flags<U, C, true, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VX(U, C) \
+    launch_v4_flags<U, C, true, false, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VS(U, C) \
+    launch_v4_flags<U, C, true, false, false, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VG(K, U, C) launch_gs_flags<U, C, true>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VGB(K, U, C, B) \
+    launch_gs_flags<U, C, true, B>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VBAND(K, U, C) launch_gs_bands<U, C, true>(st, K, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+#define FA_VL(NW, R, TQ, D) \
+    launch_lds_flags<NW, R, TQ, D>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+    switch (variant) {  // must match kVariants[]
+        case 1: FA_VF(8, 4); break;
+        case 2: FA_VF(4, 1); break;
+        case 3: FA_VX(8, 4); break;
+        case 4:  // v4_pickq_nts: the round-1 policy
+            switch (pick_quads(P)) {
+                case 4: FA_VS(8, 4); break;
+                case 2: FA_VS(4, 2); break;
+                default: FA_VS(4, 1); break;
+            }
+            break;
+        case 5: FA_VB(4, 4); break;
+        case 6: FA_VG(1, 8, 4); break;
+        case 7: FA_VG(2, 8, 4); break;
+        case 8: FA_VG(1, 4, 8); break;
+        case 9: FA_VGB(1, 8, 2, 512); break;
+        case 10: FA_VG(-1, 8, 4); break;
+        case 11: FA_VG(-1, 8, 2); break;
+        case 12: FA_VG(1192, 8, 4); break;
+        case 13: FA_VBAND(2, 8, 4); break;
+        case 14: FA_VBAND(3, 8, 4); break;
+        case 15: FA_VBAND(4, 8, 4); break;
+        case 16: FA_VBAND(6, 8, 4); break;
+        case 17: rc = FA_VL(8, 64, 32, 1); break;
+        case 18: rc = FA_VL(4, 64, 64, 1); break;
+        case 19: rc = FA_VL(16, 128, 64, 1); break;
+        case 20: rc = FA_VL(4, 32, 16, 2); break;
+        case 21: rc = FA_VL(4, 16, 32, 2); break;
+        case 22: rc = FA_VL(4, 64, 32, 2); break;
+        case 23: rc = FA_VL(8, 32, 32, 2); break;
+        case 24: rc = FA_VL(4, 32, 8, 2); break;
+        case 25: rc = FA_VL(2, 32, 16, 2); break;
+        default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
+    }
+#undef FA_VF
+#undef FA_VB
+#undef FA_VX
+#undef FA_VS
+#undef FA_VG
+#undef FA_VGB
+#undef FA_VBAND
+#undef FA_VL
+    if (rc) return rc;
+    return check_launch("fold_f32_variant");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fa_bench_last_error(void) { return g_err; }
+int fa_num_variants(void) { return kNumVariants; }
+const char* fa_variant_name(int variant) {
+    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant] : "";
+}
+
+int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                          const float* s, float divisor, float* out, void* stream, int variant) {
+    return fold_f32_variant(X, N, P, ldx, a, s, divisor, out, stream, variant);
+}
+
+int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                           const float* s, float divisor, float* out_f32, uint16_t* out_bf16, void* stream,
+                           int variant) {
+    if (variant < 0 || variant >= kNumBf16Variants) return fail(FA_ERR_ARG, "unknown bf16 variant %d", variant);
+    if (variant == 0) return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
+    int rc = check_common(N, P, ldx, X, a, out_f32);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(X) || (ldx % 8) || !aligned16(out_f32) || (out_bf16 && !aligned16(out_bf16)))
+        return fail(FA_ERR_ARG, "bf16 variants need 16-B aligned X and outputs and ldx %% 8 == 0");
+    hipStream_t st = (hipStream_t)stream;
+#define FA_BF(U, C)                                                                                         \
+    {                                                                                                       \
+        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);            \
+        const dim3 grid((unsigned)((units + per_block - 1) / per_block));                                   \
+        if (s)                                                                                              \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a, s, \
+                               divisor, out_f32, out_bf16);                                                 \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a,  \
+                               s, divisor, out_f32, out_bf16);                                              \
+    }
+    switch (variant) {  // must match kBf16Variants[]
+        case 1: FA_BF(8, 1); break;
+        case 2: FA_BF(8, 2); break;
+        case 3: FA_BF(2, 8); break;
+        case 4: launch_bf16_gs<8, 2>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 5: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 6: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 7: launch_bf16_gs<2, 8>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 8: launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 9: launch_bf16_bands<2, 8>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        default: launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+    }
+#undef FA_BF
+    return check_launch("fedavg_bf16_variant");
+}
+
+int fa_num_bf16_variants(void) { return kNumBf16Variants; }
+const char* fa_bf16_variant_name(int variant) {
+    return (variant >= 0 && variant < kNumBf16Variants) ? kBf16Variants[variant] : "";
+}
+
+int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed, int64_t row0,
+                 int64_t col0, void* stream) {
+    if (nrows < 0 || ncols < 0 || ldx < ncols) return fail(FA_ERR_ARG, "bad synth shape");
+    if (nrows == 0 || ncols == 0) { g_err[0] = 0; return FA_OK; }
+    if (!X) return fail(FA_ERR_ARG, "null X");
+    hipLaunchKernelGGL(k_synth<float>, dim3(8192), dim3(kBlock), 0, (hipStream_t)stream, X, nrows, ncols, ldx,
+                       seed, row0, col0);
+    return check_launch("k_synth<f32>");
+}
+
+int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed, int64_t row0,
+                  int64_t col0, void* stream) {
+    if (nrows < 0 || ncols < 0 || ldx < ncols) return fail(FA_ERR_ARG, "bad synth shape");
+    if (nrows == 0 || ncols == 0) { g_err[0] = 0; return FA_OK; }
+    if (!X) return fail(FA_ERR_ARG, "null X");
+    hipLaunchKernelGGL(k_synth<uint16_t>, dim3(8192), dim3(kBlock), 0, (hipStream_t)stream, X, nrows, ncols,
+                       ldx, seed, row0, col0);
+    return check_launch("k_synth<bf16>");
+}
+
+int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream) {
+    if (n < 0 || !X || !sink || sink_len <= 0 || !aligned16(X) || (n & 3))
+        return fail(FA_ERR_ARG, "read sweep needs 16-B aligned X, n %% 4 == 0, sink_len > 0");
+    const int64_t nq = n >> 2, grid = (nq + kSweepQuads - 1) / kSweepQuads;
+    if (grid > 0x7FFFFFFF) return fail(FA_ERR_ARG, "read sweep too large");
+    if (grid == 0) { g_err[0] = 0; return FA_OK; }
+    hipLaunchKernelGGL(k_read_sweep, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<const f32x4*>(X), nq, sink, sink_len);
+    return check_launch("k_read_sweep");
+}
+
+}  // extern "C"

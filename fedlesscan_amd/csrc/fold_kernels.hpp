@@ -1,0 +1,1116 @@
+// fold_kernels.hpp — device code shared by libfedavg_hip.so (the product,
+// fedavg.hip) and libfedavg_hip_bench.so (kernel variants, input generator and
+// read-sweep calibration for bench.py / the sweeps, fedavg_bench.hip).
+//
+// Hot path replaced (reference, all numpy on one CPU core):
+//   fedless/aggregator/fed_avg_aggregator.py:24-42        FedAvgAggregator._aggregate
+//   fedless/aggregator/stall_aware_aggregation.py:42-67   StallAwareAggregator._aggregate
+//
+// The op is a bandwidth-bound weighted column reduction over a row-stacked
+// [N clients][ldx] matrix: 2-3 FLOP per 4-byte element, far below any MFMA
+// ridge, so it runs on the VALU and the design goal is HBM read bandwidth.
+//
+// Bit-exactness contract: every output column is owned by
+// ONE lane, which folds clients 0..N-1 strictly in order with a separate
+// multiply and add (no FMA: these TUs are compiled with fp-contract off) and
+// finishes with an IEEE divide.  No split-N, tree or atomic reassociation on
+// any default path (the opt-in fa_fedavg_f32_splitn is the one exception).
+//
+// Parallelism comes from the columns: lane = 4 consecutive fp32 columns
+// (one 16-byte global_load_dwordx4 per client row).  Memory-level
+// parallelism comes from U independent client-row loads in flight ahead of
+// the in-order adds (the loads are independent, only the adds are ordered).
+// Kernel families (fold_f32_auto picks one by shape, pick_f32):
+//   k_fold_f32_gs    grid-stride over 16 KiB column tiles, ~1 block per CU,
+//                    balanced passes, launched per column band (large models)
+//   k_fold_f32_lds   LDS-staged: all waves stream client-row chunks of a
+//                    narrow column tile into LDS, wave 0 folds (narrow models)
+// Everything here sits in an anonymous namespace: each library gets its own
+// copy, and templates are instantiated only where a TU launches them.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "fedavg_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+constexpr int kBlock = 256;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const f32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+__device__ __forceinline__ f32x4 scale4(f32x4 x, float a) { return x * a; }
+__device__ __forceinline__ f32x4 add4(f32x4 x, f32x4 y) { return x + y; }
+__device__ __forceinline__ f32x4 div4(f32x4 x, float d) { return x / d; }
+
+// t_i = fl(fl(x*a) * s): two roundings, left-to-right like `layer * n * s`.
+template <bool SCORED>
+__device__ __forceinline__ f32x4 term4(f32x4 x, float a, float s) {
+    f32x4 t = scale4(x, a);
+    if constexpr (SCORED) t = scale4(t, s);
+    return t;
+}
+template <bool SCORED>
+__device__ __forceinline__ float term1(float x, float a, float s) {
+    float t = x * a;
+    if constexpr (SCORED) t = t * s;
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// fp32 fold over a stacked matrix, 16 B per lane per client row.
+//   X viewed as [N][ldq] f32x4 (ldq = ldx/4), 16-byte aligned rows.
+//   A lane owns C quads spaced kBlock apart (a block covers C*kBlock quads =
+//   C*4 KiB of every client row); nq = P/4 full quads, and the trailing P%4
+//   columns are folded by the lane whose first quad index == nq.
+// Template: U = client rows loaded ahead of the ordered adds; C = quads per
+// lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
+// multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
+// ---------------------------------------------------------------------------
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock>
+__device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
+                                           const float* __restrict__ a, const float* __restrict__ s,
+                                           const f32x4* acc_in, float divisor, f32x4* out) {
+    f32x4 acc[C];
+    int64_t i = 0;
+    if constexpr (ACC) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = acc_in[c * B];
+    } else {
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(ld4<NT>(p + c * B), a0, s0);
+        i = 1;
+    }
+    for (; i + U <= N; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = ld4<NT>(p + (i + u) * ldq + c * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(v[u][c], ai, si));
+        }
+    }
+    for (; i < N; ++i) {
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * B), ai, si));
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
+        if constexpr (NTS) __builtin_nontemporal_store(r, out + c * B);
+        else out[c * B] = r;
+    }
+}
+// One tile: C*kBlock quads of every client row (tile index bid).
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
+__device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__ X, int64_t N, int64_t P,
+                                          int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
+                                          const float* acc_in, float divisor, float* out) {
+    const int64_t nq = P >> 2;
+    const int64_t ldq = ldx >> 2;
+    const int64_t q0 = bid * (B * C) + threadIdx.x;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const f32x4* A4 = reinterpret_cast<const f32x4*>(acc_in);
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    if (q0 + (int64_t)(C - 1) * B < nq) {
+        // every quad of this lane is in range (all blocks but the last)
+        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS, B>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
+                                                    O4 + q0);
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int64_t q = q0 + (int64_t)c * B;
+        if (q < nq)
+            fold_quads<U, 1, NT, SCORED, ACC, FIN, false, B>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
+    }
+    // column tail: at most 3 columns, folded by the lane that would own quad
+    // index nq under the C-quads-per-lane mapping (scalar loads, same order)
+    const int64_t tb = nq / (B * C), tl = (nq % (B * C)) % B;
+    if ((P & 3) && bid == tb && (int64_t)threadIdx.x == tl) {
+        for (int64_t col = nq * 4; col < P; ++col) {
+            float acc;
+            int64_t i = 0;
+            if constexpr (ACC) {
+                acc = acc_in[col];
+            } else {
+                acc = term1<SCORED>(X[col], a[0], SCORED ? s[0] : 1.0f);
+                i = 1;
+            }
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
+            if constexpr (FIN) acc = acc / divisor;
+            out[col] = acc;
+        }
+    }
+}
+
+// Grid-stride form: a small grid (about one block per CU) walks the tiles in
+// order, tile = blockIdx.x + k*gridDim.x, so at any moment the running blocks
+// stream ADJACENT column tiles of the same client rows (one contiguous band,
+// rows visited in near lock-step) and each block streams many rows per tile.
+// On MI355X this reads HBM faster than one block per tile with several
+// resident per CU.
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
+__global__ __launch_bounds__(B) void k_fold_f32_gs(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t ntiles) {  // acc_in may alias out
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
+        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+}
+
+// Narrow models: LDS-staged client rows.
+//   When P is small (a few hundred thousand parameters: the MNIST CNN, the
+//   speech CNN, a 1M-param bucket), one lane per quad gives too few lanes to
+//   keep enough bytes in flight on 256 CUs.  Here a block owns only TQ quads
+//   (TQ*16 B of every client row) and ALL its NW waves load: each chunk of R
+//   client rows is read with R*TQ/(NW*64) independent 16-byte loads per lane
+//   and parked in LDS; wave 0 then folds the chunk from LDS in client order
+//   (lane = one quad) while the next chunk's loads are already in flight.  The
+//   adds stay one lane per column, strictly in row order: bit-identical to
+//   every other fold.  The partial quad of the P%4 tail columns is staged
+//   like a full one (element loads, zero-filled) and only its real columns
+//   are stored.  Per-chunk factors a[], s[] are staged in LDS too.
+template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1>
+__global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    constexpr int NT = NW * 64;
+    constexpr int LQ = R * TQ / NT;  // quads each thread loads per chunk
+    static_assert(TQ <= 64 && (R * TQ) % NT == 0 && R <= NT, "tile shape");
+    __shared__ f32x4 tile[R * TQ];
+    __shared__ float fa[R], fs[SCORED ? R : 1];
+    const int64_t nq = P >> 2;
+    const int64_t nqa = (P + 3) >> 2;  // quads incl. the partial tail quad
+    const int64_t q0 = (int64_t)blockIdx.x * TQ;
+    const int tq = (int)((nqa - q0) < TQ ? (nqa - q0) : TQ);
+    const int64_t ldq = ldx >> 2;
+    const int t = threadIdx.x;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    // one chunk in registers: its LQ quads per lane and (lanes < R) its factors
+    struct Stage {
+        f32x4 v[LQ];
+        float fv, sv;
+    };
+    Stage A, B;
+    // Interior blocks (TQ full quads) stream their full chunks through a loop
+    // whose loads carry no checks and no control flow: a branch between a
+    // load and its use (the tail-quad loop, or a join with a checked path)
+    // makes the compiler wait for the load right after issuing it, which
+    // would serialise the chunk loads with the fold.  The last block and the
+    // last partial chunk take the checked path, outside that loop.
+    auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int e = t + j * NT;
+            g.v[j] = __builtin_nontemporal_load(X4 + (c * R + e / TQ) * ldq + q0 + e % TQ);
+        }
+        if (t < R) {
+            g.fv = a[c * R + t];
+            if constexpr (SCORED) g.sv = s[c * R + t];
+        }
+    };
+    auto load_checked = [&](int64_t c, Stage& g) {
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int e = t + j * NT, r = e / TQ, qq = e % TQ;
+            const int64_t row = c * R + r, q = q0 + qq;
+            if (row < N && qq < tq) {
+                if (q < nq) {
+                    g.v[j] = __builtin_nontemporal_load(X4 + row * ldq + q);
+                } else {  // partial tail quad: P%4 real columns
+                    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+                    for (int k = 0; k < (int)(P & 3); ++k) x[k] = X[row * ldx + q * 4 + k];
+                    g.v[j] = x;
+                }
+            }
+        }
+        if (t < R && c * R + t < N) {
+            g.fv = a[c * R + t];
+            if constexpr (SCORED) g.sv = s[c * R + t];
+        }
+    };
+    auto stash = [&](const Stage& g) {
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) tile[t + j * NT] = g.v[j];
+        if (t < R) {
+            fa[t] = g.fv;
+            if constexpr (SCORED) fs[t] = g.sv;
+        }
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (ACC) {
+        if (t < tq) {
+            const int64_t q = q0 + t;
+            if (q < nq) {
+                acc = reinterpret_cast<const f32x4*>(acc_in)[q];
+            } else {
+                for (int k = 0; k < (int)(P & 3); ++k) acc[k] = acc_in[q * 4 + k];
+            }
+        }
+    }
+    // fold the staged chunk c (rows valid rows) in client order, lane = quad
+    auto fold = [&](int64_t c, int rows) {
+        if (t < tq) {
+            int r = 0;
+            if (!ACC && c == 0) {
+                acc = term4<SCORED>(tile[t], fa[0], SCORED ? fs[0] : 1.0f);
+                r = 1;
+            }
+            // 8 LDS reads in flight ahead of the ordered adds (the reads are
+            // independent, only the adds are ordered)
+            for (; r + 8 <= rows; r += 8) {
+                f32x4 x[8];
+                float f[8], g[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    x[k] = tile[(r + k) * TQ + t];
+                    f[k] = fa[r + k];
+                    g[k] = SCORED ? fs[r + k] : 1.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc = add4(acc, term4<SCORED>(x[k], f[k], g[k]));
+            }
+            for (; r < rows; ++r) acc = add4(acc, term4<SCORED>(tile[r * TQ + t], fa[r], SCORED ? fs[r] : 1.0f));
+        }
+    };
+    const bool interior = q0 + TQ <= nq;
+    const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
+    int64_t c = 0;  // next chunk to fold
+    if (DEPTH == 2 && nfull >= 4) {
+        // two chunks in flight: LDS holds chunk c, A = c+1 and B = c+2 are loading.
+        // The loop is peeled so that no load in it is conditional.
+        load_full(0, A);
+        stash(A);
+        __syncthreads();
+        load_full(1, A);
+        load_full(2, B);
+        for (; c + 4 < nfull; c += 2) {
+            fold(c, R);
+            __syncthreads();  // chunk c consumed
+            stash(A);         // waits for A only; B stays in flight
+            __syncthreads();  // chunk c+1 staged
+            load_full(c + 3, A);
+            fold(c + 1, R);
+            __syncthreads();
+            stash(B);
+            __syncthreads();  // chunk c+2 staged
+            load_full(c + 4, B);
+        }
+        // LDS = c, A = c+1, B = c+2 (c + 2 < nfull <= c + 4)
+        fold(c, R);
+        __syncthreads();
+        stash(A);
+        __syncthreads();
+        fold(c + 1, R);
+        __syncthreads();
+        stash(B);
+        __syncthreads();
+        fold(c + 2, R);
+        __syncthreads();
+        c += 3;
+    } else if (nfull > 0) {
+        load_full(0, A);
+        stash(A);
+        __syncthreads();
+        for (; c + 1 < nfull; ++c) {
+            load_full(c + 1, A);  // in flight while wave 0 folds chunk c
+            fold(c, R);
+            __syncthreads();  // chunk c consumed
+            stash(A);
+            __syncthreads();  // chunk c+1 staged
+        }
+        fold(c, R);
+        __syncthreads();
+        ++c;
+    }
+    for (; c * R < N; ++c) {  // the rest, checked (no overlap)
+        if (c < nfull) load_full(c, A);
+        else load_checked(c, A);
+        stash(A);
+        __syncthreads();
+        fold(c, (N - c * R) < R ? (int)(N - c * R) : R);
+        __syncthreads();
+    }
+    if (t < tq) {
+        const f32x4 res = FIN ? div4(acc, divisor) : acc;
+        const int64_t q = q0 + t;
+        if (q < nq) {
+            __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q);
+        } else {
+            for (int k = 0; k < (int)(P & 3); ++k) out[q * 4 + k] = res[k];
+        }
+    }
+}
+
+// Split-client fold (opt-in, NOT bit-exact; fa_fedavg_f32_splitn).
+//   For models too narrow to fill the chip even with LDS staging, the
+//   clients of every column are cut into S = 4*NW contiguous slices.  A block
+//   owns 16 quads (64 columns); lane l of wave w folds quad l%16 over slice
+//   4*w + l/16, in client order, 8 rows ahead.  The S partial sums are then
+//   combined in a FIXED pairwise tree -- two wavefront shuffles (slice pairs,
+//   then pairs of pairs), then the waves' partials through LDS -- so the
+//   result is deterministic run to run, but it is a different association
+//   than the reference's left fold: it differs in the last bits (normwise
+//   error measured in tests/test_gpu_parity.py and DESIGN.md 5).
+template <int NW, bool SCORED>
+__global__ __launch_bounds__(NW * 64) void k_fold_f32_splitn(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor, float* __restrict__ out) {
+    constexpr int S = 4 * NW;  // client slices
+    constexpr int U = 8;
+    __shared__ f32x4 part[NW][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qq = lane & 15, slice = 4 * w + (lane >> 4);
+    const int64_t nq = P >> 2, q = (int64_t)blockIdx.x * 16 + qq;
+    const int64_t ns = (N + S - 1) / S;
+    const int64_t r0 = slice * ns < N ? slice * ns : N, r1 = r0 + ns < N ? r0 + ns : N;
+    const int64_t ldq = ldx >> 2;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if ((int64_t)blockIdx.x * 16 + 16 <= nq) {  // block-uniform: 16 full quads, no checks in the loop
+        const f32x4* p = reinterpret_cast<const f32x4*>(X) + q;
+        int64_t i = r0;
+        if (i < r1) {
+            acc = term4<SCORED>(__builtin_nontemporal_load(p + i * ldq), a[i], SCORED ? s[i] : 1.0f);
+            ++i;
+        }
+        for (; i + U <= r1; i += U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldq);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
+        }
+        for (; i < r1; ++i)
+            acc = add4(acc, term4<SCORED>(__builtin_nontemporal_load(p + i * ldq), a[i], SCORED ? s[i] : 1.0f));
+    } else if (q * 4 < P) {  // last block: full and partial quads, element loads
+        const int w4 = (P - q * 4) < 4 ? (int)(P - q * 4) : 4;
+        for (int64_t i = r0; i < r1; ++i) {
+            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < w4; ++k) x[k] = X[i * ldx + q * 4 + k];
+            const f32x4 t = term4<SCORED>(x, a[i], SCORED ? s[i] : 1.0f);
+            acc = i == r0 ? t : add4(acc, t);
+        }
+    }
+    // fixed tree: slice pairs (xor 16), pairs of pairs (xor 32); fp add is
+    // commutative, so both lanes of a pair hold the same bits
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+        f32x4 o;
+        o.x = __shfl_xor(acc.x, off);
+        o.y = __shfl_xor(acc.y, off);
+        o.z = __shfl_xor(acc.z, off);
+        o.w = __shfl_xor(acc.w, off);
+        acc = add4(acc, o);
+    }
+    if (lane < 16) part[w][qq] = acc;
+    __syncthreads();
+    if (w == 0 && lane < 16 && q * 4 < P) {
+        f32x4 t[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) t[k] = part[k][qq];
+#pragma unroll
+        for (int stride = 1; stride < NW; stride <<= 1)  // ((p0+p1)+(p2+p3))+...
+#pragma unroll
+            for (int k = 0; k + stride < NW; k += 2 * stride) t[k] = add4(t[k], t[k + stride]);
+        const f32x4 r = div4(t[0], divisor);
+        if (q < nq) {
+            __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(out) + q);
+        } else {
+            for (int k = 0; k < (int)(P & 3); ++k) out[q * 4 + k] = r[k];
+        }
+    }
+}
+
+// One column per lane, any alignment / stride (fallback for unaligned input).
+template <bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    float acc;
+    int64_t i = 0;
+    if constexpr (ACC) {
+        acc = acc_in[c];
+    } else {
+        acc = term1<SCORED>(X[c], a[0], SCORED ? s[0] : 1.0f);
+        i = 1;
+    }
+#pragma unroll 8
+    for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + c], a[i], SCORED ? s[i] : 1.0f);
+    if constexpr (FIN) acc = acc / divisor;
+    out[c] = acc;
+}
+
+// List-of-rows form: xi[i] = device pointer to client i's P floats.  A lane
+// owns 4 columns; U rows are loaded ahead of the ordered adds.  The row
+// alignment test is wave-uniform (every lane reads the same pointer).
+__device__ __forceinline__ f32x4 load_row4(const float* row, int64_t c0, int w) {
+    if (w == 4 && aligned16(row)) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0));
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < w; ++k) x[k] = row[c0 + k];
+    return x;
+}
+
+template <int U, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f32_ptrs(
+    const float* const* __restrict__ xi, int64_t N, int64_t P,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out) {
+    const int64_t c0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (c0 >= P) return;
+    const int w = (P - c0) >= 4 ? 4 : (int)(P - c0);
+    f32x4 acc = term4<SCORED>(load_row4(xi[0], c0, w), a[0], SCORED ? s[0] : 1.0f);
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = load_row4(xi[i + u], c0, w);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = add4(acc, term4<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f));
+    }
+    for (; i < N; ++i) acc = add4(acc, term4<SCORED>(load_row4(xi[i], c0, w), a[i], SCORED ? s[i] : 1.0f));
+    acc = div4(acc, divisor);
+    if (w == 4 && aligned16(out + c0)) {
+        *reinterpret_cast<f32x4*>(out + c0) = acc;
+    } else {
+        for (int k = 0; k < w; ++k) out[c0 + k] = acc[k];
+    }
+}
+
+// List-of-rows form with every row 16-B aligned (fa_fedavg_f32_ptrs_aligned):
+// the tile structure of the stacked fold (C quads per lane, U rows ahead) with
+// row i's base read from xi[i] (a wave-uniform scalar load).  No branch sits
+// between the loads and their use.
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void fold_quads_rows(const float* const* __restrict__ xi, int64_t q0, int64_t N,
+                                                const float* __restrict__ a, const float* __restrict__ s,
+                                                float divisor, f32x4* __restrict__ out) {
+    f32x4 acc[C];
+    {
+        const f32x4* r = reinterpret_cast<const f32x4*>(xi[0]) + q0;
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(__builtin_nontemporal_load(r + c * kBlock), a0, s0);
+    }
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        f32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const f32x4* r = reinterpret_cast<const f32x4*>(xi[i + u]) + q0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(v[u][c], ai, si));
+        }
+    }
+    for (; i < N; ++i) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(xi[i]) + q0;
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(__builtin_nontemporal_load(r + c * kBlock), ai, si));
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) __builtin_nontemporal_store(div4(acc[c], divisor), out + c * kBlock);
+}
+
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_rows_gs(
+    const float* const* __restrict__ xi, int64_t N, int64_t P, const float* __restrict__ a,
+    const float* __restrict__ s, float divisor, float* __restrict__ out, int64_t ntiles) {
+    const int64_t nq = P >> 2;
+    f32x4* O4 = reinterpret_cast<f32x4*>(out);
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+        const int64_t q0 = bid * (kBlock * C) + threadIdx.x;
+        if (q0 + (int64_t)(C - 1) * kBlock < nq) {
+            fold_quads_rows<U, C, SCORED>(xi, q0, N, a, s, divisor, O4 + q0);
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int64_t q = q0 + (int64_t)c * kBlock;
+                if (q < nq) fold_quads_rows<U, 1, SCORED>(xi, q, N, a, s, divisor, O4 + q);
+            }
+            const int64_t tb = nq / (kBlock * C), tl = (nq % (kBlock * C)) % kBlock;
+            if ((P & 3) && bid == tb && (int64_t)threadIdx.x == tl) {
+                for (int64_t col = nq * 4; col < P; ++col) {
+                    float acc = term1<SCORED>(xi[0][col], a[0], SCORED ? s[0] : 1.0f);
+                    for (int64_t i = 1; i < N; ++i) acc = acc + term1<SCORED>(xi[i][col], a[i], SCORED ? s[i] : 1.0f);
+                    out[col] = acc / divisor;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bf16: 8 columns per lane (one 16-byte load per row), exact upcast, f32 fold.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f != f) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+// A 16-byte load holds 8 bf16 = 4 words; the low half of word k is column 2k,
+// the high half column 2k+1.  Exact upcast = the half moved to the top of an
+// f32, so the 8 columns fold as two f32x4 (even / odd columns).
+__device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) {
+    even = __builtin_bit_cast(f32x4, w << 16);
+    odd = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
+}
+
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
+                                            const float* __restrict__ a, const float* __restrict__ s,
+                                            float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
+                                            int64_t o0) {
+    f32x4 ev[C], od[C];
+    {
+        const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + c * kBlock), e, o);
+            ev[c] = term4<SCORED>(e, a0, s0);
+            od[c] = term4<SCORED>(o, a0, s0);
+        }
+    }
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        u32x4 v[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                f32x4 e, o;
+                unpack_bf16x8(v[u][c], e, o);
+                ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
+                od[c] = add4(od[c], term4<SCORED>(o, ai, si));
+            }
+        }
+    }
+    for (; i < N; ++i) {
+        const float ai = a[i], si = SCORED ? s[i] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + i * ldo + c * kBlock), e, o);
+            ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
+            od[c] = add4(od[c], term4<SCORED>(o, ai, si));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
+        const int64_t oc = o0 + (int64_t)c * kBlock;
+        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
+        __builtin_nontemporal_store(f32x4{e.x, o.x, e.y, o.y}, o4);
+        __builtin_nontemporal_store(f32x4{e.z, o.z, e.w, o.w}, o4 + 1);
+        if (outb) {
+            u32x4 b;
+            b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
+            b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
+            b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
+            b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
+            __builtin_nontemporal_store(b, reinterpret_cast<u32x4*>(outb) + oc);
+        }
+    }
+}
+
+// bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
+// spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
+                                          int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
+                                          float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
+    const int64_t no = P >> 3;  // full octets
+    const int64_t ldo = ldx >> 3;
+    const int64_t o0 = bid * (kBlock * C) + threadIdx.x;
+    const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
+    if (o0 + (int64_t)(C - 1) * kBlock < no) {
+        fold_octets<U, C, SCORED>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int64_t o = o0 + (int64_t)c * kBlock;
+        if (o < no) fold_octets<U, 1, SCORED>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+    }
+    const int64_t tb = no / (kBlock * C), tl = (no % (kBlock * C)) % kBlock;
+    if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
+        for (int64_t col = no * 8; col < P; ++col) {
+            float acc = term1<SCORED>(bf2f(X[col]), a[0], SCORED ? s[0] : 1.0f);
+            for (int64_t i = 1; i < N; ++i)
+                acc = acc + term1<SCORED>(bf2f(X[i * ldx + col]), a[i], SCORED ? s[i] : 1.0f);
+            acc = acc / divisor;
+            out[col] = acc;
+            if (outb) outb[col] = f2bf_rne(acc);
+        }
+    }
+}
+
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_v8(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb) {
+    bf16_tile<U, C, SCORED>(blockIdx.x, X, N, P, ldx, a, s, divisor, out, outb);
+}
+
+// grid-stride over octet tiles, as k_fold_f32_gs
+template <int U, int C, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_gs(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles) {
+    for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
+        bf16_tile<U, C, SCORED>(bid, X, N, P, ldx, a, s, divisor, out, outb);
+}
+
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_bf16_scalar(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    float acc = term1<SCORED>(bf2f(X[c]), a[0], SCORED ? s[0] : 1.0f);
+    for (int64_t i = 1; i < N; ++i)
+        acc = acc + term1<SCORED>(bf2f(X[i * ldx + c]), a[i], SCORED ? s[i] : 1.0f);
+    acc = acc / divisor;
+    out[c] = acc;
+    if (outb) outb[c] = f2bf_rne(acc);
+}
+
+// ---------------------------------------------------------------------------
+// float64 and integer folds: one column per lane, coalesced 8-byte loads.
+// ---------------------------------------------------------------------------
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// float64: a lane owns 2 columns (one 16-byte load per row), U rows ahead;
+// the odd last column (P % 2) goes to the lane with q == P/2.
+template <int U, bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f64_v2(
+    const double* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const double* __restrict__ a, const double* __restrict__ s, double divisor,
+    double* __restrict__ out) {
+    const int64_t nq = P >> 1, ldq = ldx >> 1;
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q < nq) {
+        const f64x2* p = reinterpret_cast<const f64x2*>(X) + q;
+        f64x2 acc = __builtin_nontemporal_load(p) * a[0];
+        if constexpr (SCORED) acc = acc * s[0];
+        int64_t i = 1;
+        for (; i + U <= N; i += U) {
+            f64x2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (i + u) * ldq);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                f64x2 t = v[u] * a[i + u];
+                if constexpr (SCORED) t = t * s[i + u];
+                acc = acc + t;
+            }
+        }
+        for (; i < N; ++i) {
+            f64x2 t = __builtin_nontemporal_load(p + i * ldq) * a[i];
+            if constexpr (SCORED) t = t * s[i];
+            acc = acc + t;
+        }
+        __builtin_nontemporal_store(acc / divisor, reinterpret_cast<f64x2*>(out) + q);
+    } else if (q == nq && (P & 1)) {
+        const int64_t c = P - 1;
+        double acc = X[c] * a[0];
+        if constexpr (SCORED) acc = acc * s[0];
+        for (int64_t i = 1; i < N; ++i) {
+            double t = X[i * ldx + c] * a[i];
+            if constexpr (SCORED) t = t * s[i];
+            acc = acc + t;
+        }
+        out[c] = acc / divisor;
+    }
+}
+
+// float64, one column per lane, any alignment / stride.
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fedavg_f64(
+    const double* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const double* __restrict__ a, const double* __restrict__ s, double divisor,
+    double* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    double acc = X[c] * a[0];
+    if constexpr (SCORED) acc = acc * s[0];
+#pragma unroll 8
+    for (int64_t i = 1; i < N; ++i) {
+        double t = X[i * ldx + c] * a[i];
+        if constexpr (SCORED) t = t * s[i];
+        acc = acc + t;
+    }
+    out[c] = acc / divisor;
+}
+
+// numpy integer semantics: product and fold in the input dtype with
+// two's-complement wrap (computed unsigned to avoid C++ UB), then
+// true_divide -> float64(acc) / float64(total).
+template <typename T, typename UT>
+__global__ __launch_bounds__(kBlock) void k_fedavg_int(
+    const T* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const int64_t* __restrict__ a, double divisor, double* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    UT acc = 0;
+    for (int64_t i = 0; i < N; ++i) {
+        UT t = (UT)X[i * ldx + c] * (UT)(T)a[i];
+        acc = (i == 0) ? t : (UT)(acc + t);
+    }
+    out[c] = (double)(T)acc / divisor;
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+inline dim3 grid_for(int64_t lanes) { return dim3((unsigned)((lanes + kBlock - 1) / kBlock)); }
+
+int check_common(int64_t N, int64_t P, int64_t ldx, const void* X, const void* a, const void* out) {
+    if (N < 0 || P < 0) return fail(FA_ERR_ARG, "negative size (N=%lld, P=%lld)", (long long)N, (long long)P);
+    if (N == 0) return fail(FA_ERR_NO_CLIENTS, "no client results to aggregate (N == 0)");
+    if (ldx < P) return fail(FA_ERR_SHAPE, "row pitch ldx=%lld < P=%lld", (long long)ldx, (long long)P);
+    if (P > 0 && (!X || !a || !out)) return fail(FA_ERR_ARG, "null X/a/out pointer");
+    if ((P + 4 * (int64_t)kBlock) / (4 * (int64_t)kBlock) > (int64_t)0x7FFFFFFF)
+        return fail(FA_ERR_ARG, "P too large for one launch");
+    return FA_OK;
+}
+
+// Compute units of the current device (cached per device).
+int cu_count() {
+    static thread_local int cache[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cache[dev] > 0) return cache[dev];
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    cache[dev] = cus;
+    return cus;
+}
+
+// The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
+// model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
+// profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
+//   P < 256K params                    LDS-staged, 4 waves, two chunks in flight per block:
+//                                      32-row chunks of 16-quad tiles (16-row chunks of
+//                                      32-quad tiles for 32K-128K params)
+//   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
+//   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
+//                                      in column bands of <= 4 passes x CUs tiles
+// all with non-temporal output stores.
+enum class F32Pick { kLdsW4, kLdsW4T32, kLdsW8, kGsBalC2, kGsBalC4 };
+inline F32Pick pick_f32(int64_t N, int64_t P) {
+    const int64_t nq = P >> 2, cus = cu_count();
+    if (nq < (1 << 16)) return nq >= (1 << 13) && nq < (1 << 15) ? F32Pick::kLdsW4T32 : F32Pick::kLdsW4;
+    const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
+    if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
+    if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
+    return F32Pick::kGsBalC4;
+}
+
+// bf16 "auto": octets per lane from the client count.  Sweeps on MI355X
+//  put the optimum near 8 MB per block (rows x C x 4 KiB):
+// 256 rows -> C=8 (u2c8), 512 -> C=4, 1024 -> C=2 (u8c2); C shrinks further
+// while the launch would have fewer than ~1000 blocks.
+inline int pick_octets(int64_t N, int64_t P) {
+    int c = N <= 384 ? 8 : (N <= 768 ? 4 : 2);
+    while (c > 1 && (P >> 3) / ((int64_t)c * kBlock) < 1000) c >>= 1;
+    return c;
+}
+
+// Grid-stride fold: grid = min(tiles, per_cu x CUs); per_cu < 0 = balanced passes.
+template <int U, int C, bool NT, bool SC, bool ACC, bool FIN, bool NTS, int B>
+void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+               const float* s, const float* acc_in, float d, float* out) {
+    const int64_t per_block = (int64_t)B * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;  // incl. the column-tail lane
+    // per_cu >= 1000: a fixed block count (per_cu - 1000), balanced passes (sweeps only)
+    int64_t grid = per_cu >= 1000 ? per_cu - 1000 : (int64_t)(per_cu > 0 ? per_cu : -per_cu) * cu_count();
+    if (grid > tiles) grid = tiles;
+    if (per_cu < 0 || per_cu >= 1000) {
+        // balanced passes: the fewest blocks that still finish in the same
+        // number of passes, so the last pass is (nearly) full instead of
+        // leaving up to a whole pass of CUs idle
+        const int64_t passes = (tiles + grid - 1) / grid;
+        grid = (tiles + passes - 1) / passes;
+    }
+    hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS, B>), dim3((unsigned)grid), dim3(B), 0, st, X,
+                       N, P, ldx, a, s, acc_in, d, out, tiles);
+}
+
+// ALLF: instantiate every (scored, accumulate, finalize) combination -- only the
+// auto variant needs them (fa_fold_f32); tuning variants are always a plain
+// fold with the divide (acc == false, fin == true), so they instantiate two.
+template <int U, int C, bool NTS, int B = kBlock, bool ALLF = false>
+void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+#define FA_G(SC, ACC, FIN) launch_gs<U, C, true, SC, ACC, FIN, NTS, B>(st, per_cu, X, N, P, ldx, a, s, acc_in, d, out)
+    if constexpr (!ALLF) {
+        if (sc) FA_G(true, false, true); else FA_G(false, false, true);
+    } else if (sc) {
+        if (acc) { if (fin) FA_G(true, true, true); else FA_G(true, true, false); }
+        else     { if (fin) FA_G(true, false, true); else FA_G(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_G(false, true, true); else FA_G(false, true, false); }
+        else     { if (fin) FA_G(false, false, true); else FA_G(false, false, false); }
+    }
+#undef FA_G
+}
+
+// Column bands: the fold as several back-to-back balanced grid-stride
+// launches over contiguous column bands of about `passes` x CUs tiles each.
+// Columns are independent, so this is the same arithmetic; the kernel
+// boundaries re-align the blocks, which otherwise drift apart over many
+// passes (C3: 4 bands of 611 tiles, 5.80 ms, against 5.91 ms as one launch,
+// DESIGN.md 5).
+template <int U, int C, bool NTS, bool ALLF = false>
+void launch_gs_bands(hipStream_t st, int passes, bool sc, bool acc, bool fin, const float* X, int64_t N,
+                     int64_t P, int64_t ldx, const float* a, const float* s, const float* acc_in, float d,
+                     float* out) {
+    const int64_t tq = (int64_t)kBlock * C;  // quads per tile
+    const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + tq - 1) / tq;
+    const int64_t per_band = (int64_t)passes * cu_count();
+    const int64_t nb = (tiles + per_band - 1) / per_band;
+    const int64_t band_tiles = (tiles + nb - 1) / nb;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t c0 = b * band_tiles * tq * 4;  // first column of the band (a multiple of 4 KiB x C)
+        if (c0 >= P) break;
+        const int64_t pb = (P - c0) < band_tiles * tq * 4 ? (P - c0) : band_tiles * tq * 4;
+        launch_gs_flags<U, C, NTS, kBlock, ALLF>(st, -1, sc, acc, fin, N == 0 ? X : X + c0, N, pb, ldx, a, s,
+                                   acc_in ? acc_in + c0 : nullptr, d, out + c0);
+    }
+}
+
+template <bool SC, bool ACC, bool FIN>
+void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+                   const float* s, const float* acc_in, float d, float* out) {
+    hipLaunchKernelGGL((k_fold_f32_scalar<SC, ACC, FIN>), grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx,
+                       a, s, acc_in, d, out);
+}
+
+// LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
+template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false>
+int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                     int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
+    if (blocks * NW * 64 > (int64_t)0xFFFFFFFF)  // work-items per launch dimension
+        return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
+    const dim3 grid((unsigned)blocks), block(NW * 64);
+#define FA_L(SC, ACC, FIN)                                                                                   \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH>), grid, block, 0, st, X, N, P, ldx, a, s, \
+                       acc_in, d, out)
+    if constexpr (!ALLF) {
+        if (sc) FA_L(true, false, true); else FA_L(false, false, true);
+    } else if (sc) {
+        if (acc) { if (fin) FA_L(true, true, true); else FA_L(true, true, false); }
+        else     { if (fin) FA_L(true, false, true); else FA_L(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_L(false, true, true); else FA_L(false, true, false); }
+        else     { if (fin) FA_L(false, false, true); else FA_L(false, false, false); }
+    }
+#undef FA_L
+    return FA_OK;
+}
+
+// bf16 grid-stride launch (per_cu < 0: balanced passes) and its column-band form
+template <int U, int C>
+void launch_bf16_gs(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                    const float* a, const float* s, float d, float* out, uint16_t* outb) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 3) + ((P & 7) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    int64_t g = (int64_t)(per_cu > 0 ? per_cu : -per_cu) * cu_count();
+    if (g > tiles) g = tiles;
+    if (per_cu < 0) {
+        const int64_t passes = (tiles + g - 1) / g;
+        g = (tiles + passes - 1) / passes;
+    }
+    if (s)
+        hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, X, N, P, ldx, a,
+                           s, d, out, outb, tiles);
+    else
+        hipLaunchKernelGGL((k_fedavg_bf16_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, X, N, P, ldx,
+                           a, s, d, out, outb, tiles);
+}
+
+template <int U, int C>
+void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                       const float* a, const float* s, float d, float* out, uint16_t* outb) {
+    const int64_t to = (int64_t)kBlock * C;  // octets per tile
+    const int64_t units = (P >> 3) + ((P & 7) ? 1 : 0);
+    const int64_t tiles = (units + to - 1) / to;
+    const int64_t per_band = (int64_t)passes * cu_count();
+    const int64_t nb = (tiles + per_band - 1) / per_band;
+    const int64_t band_tiles = (tiles + nb - 1) / nb;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t c0 = b * band_tiles * to * 8;
+        if (c0 >= P) break;
+        const int64_t pb = (P - c0) < band_tiles * to * 8 ? (P - c0) : band_tiles * to * 8;
+        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
+    }
+}
+
+
+// The product fp32 fold: checks, then the scalar fallback for unaligned input
+// or the shape-picked vector fold (pick_f32).  acc_in continues a fold
+// (fa_fold_f32); with acc_in and N == 0 it only finalises.
+inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                         const float* acc_in, float divisor, int finalize, float* out, void* stream) {
+    if (!(acc_in && N == 0)) {
+        int rc = check_common(N, P, ldx, X, a, out);
+        if (rc) return rc;
+    } else if (P > 0 && !out) {
+        return fail(FA_ERR_ARG, "null out pointer");
+    }
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    const bool sc = s != nullptr, acc = acc_in != nullptr, fin = finalize != 0;
+    const bool vec = (N == 0 || aligned16(X)) && (ldx % 4 == 0) && aligned16(out) &&
+                     (!acc || aligned16(acc_in));
+    if (!vec) {
+#define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
+        if (sc) {
+            if (acc) { if (fin) FA_SC(true, true, true); else FA_SC(true, true, false); }
+            else     { if (fin) FA_SC(true, false, true); else FA_SC(true, false, false); }
+        } else {
+            if (acc) { if (fin) FA_SC(false, true, true); else FA_SC(false, true, false); }
+            else     { if (fin) FA_SC(false, false, true); else FA_SC(false, false, false); }
+        }
+#undef FA_SC
+        return check_launch("k_fold_f32_scalar");
+    }
+    int rc = FA_OK;
+    switch (pick_f32(N, P)) {  // every (scored, accumulate, finalize) combination
+        case F32Pick::kLdsW4:
+            rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW4T32:
+            rc = launch_lds_flags<4, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW8:
+            rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kGsBalC2:
+            launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        default:  // one band below 4 x CUs tiles
+            launch_gs_bands<8, 4, true, true>(st, 4, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+    }
+    if (rc) return rc;
+    return check_launch("fold_f32");
+}
+
+// The product bf16 fold (exact upcast, fp32 fold in order, optional RNE bf16 copy).
+inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                     float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+    int rc = check_common(N, P, ldx, X, a, out_f32);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    hipStream_t st = (hipStream_t)stream;
+    const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && (!out_bf16 || aligned16(out_bf16));
+    if (!vec) {
+        if (s)
+            hipLaunchKernelGGL(k_fedavg_bf16_scalar<true>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
+                               divisor, out_f32, out_bf16);
+        else
+            hipLaunchKernelGGL(k_fedavg_bf16_scalar<false>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
+                               divisor, out_f32, out_bf16);
+        return check_launch("k_fedavg_bf16_scalar");
+    }
+    if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
+        // per-GPU C4 buckets (256 x 12.5M): grid-stride, 8 rows x 2 octets,
+        // one block per CU: +7 % over the row-streaming pick
+        launch_bf16_gs<8, 2>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+    } else if ((P >> 3) >= ((int64_t)1 << 22)) {
+        // whole large models (C4's 100M on one GPU): balanced grid-stride
+        // launches over 32 KiB tiles (fewer tile switches per block), in
+        // column bands of 2 passes: +4 % over one launch
+        launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+    } else {
+        // smaller models: one block per tile, octets per lane from the client count
+#define FA_BF(U, C)                                                                                         \
+    {                                                                                                       \
+        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);            \
+        const dim3 grid((unsigned)((units + per_block - 1) / per_block));                                   \
+        if (s)                                                                                              \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a, s, \
+                               divisor, out_f32, out_bf16);                                                 \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a,  \
+                               s, divisor, out_f32, out_bf16);                                              \
+    }
+        switch (pick_octets(N, P)) {
+            case 8: FA_BF(2, 8); break;
+            case 4: FA_BF(4, 4); break;
+            case 2: FA_BF(8, 2); break;
+            default: FA_BF(8, 1); break;
+        }
+#undef FA_BF
+    }
+    return check_launch("fedavg_bf16");
+}
+
+}  // namespace

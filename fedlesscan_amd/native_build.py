@@ -1,9 +1,14 @@
-"""Build libfedavg_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+"""Build the native libraries in-tree for gfx950 (hipcc cross-compiles without a GPU).
 
     python -m fedlesscan_amd.native_build [--force] [--isa]
 
-The .so lands in fedlesscan_amd/_native/ (git-ignored, but shipped to the GPU
-box by gpurun with the rest of the tree).
+  libfedavg_hip.so        the product: fedavg.hip (+ fold_kernels.hpp) and the
+                          host ingest (NPZ index / pack, BSON walk)
+  libfedavg_hip_bench.so  bench / tuning support: fedavg_bench.hip (kernel
+                          variants, HBM input generator, read-sweep calibration)
+
+Both compile in parallel.  The .so files land in fedlesscan_amd/_native/
+(git-ignored, but shipped to the GPU box by gpurun with the rest of the tree).
 """
 from __future__ import annotations
 
@@ -14,11 +19,21 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
-SRC = os.path.join(PKG, "csrc", "fedavg.hip")
-HOST_SRCS = [os.path.join(PKG, "csrc", f) for f in ("ingest_host.cpp", "bson_host.cpp")]
+CSRC = os.path.join(PKG, "csrc")
+SRC = os.path.join(CSRC, "fedavg.hip")
+BENCH_SRC = os.path.join(CSRC, "fedavg_bench.hip")
+KERNELS = os.path.join(CSRC, "fold_kernels.hpp")
+HOST_SRCS = [os.path.join(CSRC, f) for f in ("ingest_host.cpp", "bson_host.cpp")]
 HDR = os.path.join(REPO, "include", "fedavg_hip.h")
+BENCH_HDR = os.path.join(REPO, "include", "fedavg_hip_bench.h")
 OUT_DIR = os.path.join(PKG, "_native")
 LIB = os.path.join(OUT_DIR, "libfedavg_hip.so")
+BENCH_LIB = os.path.join(OUT_DIR, "libfedavg_hip_bench.so")
+# library -> (sources compiled into it, files it depends on)
+TARGETS = {
+    LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, HDR, *HOST_SRCS]),
+    BENCH_LIB: ([BENCH_SRC], [BENCH_SRC, KERNELS, HDR, BENCH_HDR]),
+}
 ARCH = os.environ.get("FEDAVG_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: multiply and add must stay separate (numpy semantics);
@@ -34,26 +49,33 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, *HOST_SRCS, HDR))
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(p) > t for p in TARGETS[lib][1])
 
 
 def build(force: bool = False, isa_dir: str | None = None) -> str:
-    if not force and not _stale():
-        return LIB
+    """Compile every stale library (all of them with force); returns the product path."""
     os.makedirs(OUT_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, SRC, *HOST_SRCS]
-    if isa_dir:
-        os.makedirs(isa_dir, exist_ok=True)
-        cmd.insert(1, "-save-temps")
-        subprocess.check_call(cmd, cwd=isa_dir)
-    else:
-        subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
+    jobs = []
+    for lib, (srcs, _) in TARGETS.items():
+        if not force and not _stale(lib):
+            continue
+        tmp = lib + ".tmp"
+        cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, *srcs]
+        cwd = None
+        if isa_dir:
+            cwd = os.path.join(isa_dir, os.path.basename(lib).split(".")[0])
+            os.makedirs(cwd, exist_ok=True)
+            cmd.insert(1, "-save-temps")
+        jobs.append((lib, tmp, subprocess.Popen(cmd, cwd=cwd)))
+    failed = [lib for lib, _, p in jobs if p.wait() != 0]
+    if failed:
+        raise RuntimeError(f"hipcc failed for {', '.join(os.path.basename(f) for f in failed)}")
+    for lib, tmp, _ in jobs:
+        os.replace(tmp, lib)
     return LIB
 
 

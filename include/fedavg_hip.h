@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 1
+#define FA_ABI_VERSION 2
 
 enum fa_status {
     FA_OK = 0,
@@ -122,31 +122,6 @@ int fa_fedavg_i32(const int32_t* X, int64_t N, int64_t P, int64_t ldx,
                   const int64_t* a, double divisor, double* out, void* stream);
 int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx,
                   const int64_t* a, double divisor, double* out, void* stream);
-
-/* ---- support: synthetic workloads and calibration (not reference API) ----- */
-/* Deterministic generator, bit-identical to fedlesscan_amd/synth.py. */
-int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
-                 int64_t row0, int64_t col0, void* stream);
-int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
-                  int64_t row0, int64_t col0, void* stream);
-/* Contiguous read-only sweep of n floats, one 64 KiB chunk per block (16 B
- * per lane) -> one partial per block in sink[block % sink_len] (values are
- * meaningless): the streaming-read ceiling the fold is compared with. */
-int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
-/* Tuning entry: fa_fedavg_f32 with an explicit kernel variant;
- * variant 0 = the default.  Returns FA_ERR_ARG for an unknown variant. */
-int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
-                          const float* a, const float* s, float divisor,
-                          float* out, void* stream, int variant);
-int fa_num_variants(void);
-/* [host] short name of a variant, e.g. "u4c4nt". */
-const char* fa_variant_name(int variant);
-/* Same for the bf16 fold (variant 0 = fa_fedavg_bf16's default). */
-int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
-                           const float* a, const float* s, float divisor,
-                           float* out_f32, uint16_t* out_bf16, void* stream, int variant);
-int fa_num_bf16_variants(void);
-const char* fa_bf16_variant_name(int variant);
 
 /* ---- host staging: page-locked documents and direct DMA ---------------------
  * A result store that keeps documents in page-locked memory lets the ingest

@@ -1,0 +1,53 @@
+/*
+ * fedavg_hip_bench.h — C-ABI of libfedavg_hip_bench.so: bench and tuning
+ * support for the engine of fedavg_hip.h.  NOT part of the product ABI and
+ * not a reference interface: nothing in the drop-in path (fedlesscan_amd/)
+ * loads this library.  bench.py and the GPU tests use it to generate
+ * synthetic client matrices straight into HBM, to measure the streaming-read
+ * ceiling next to the fold, and to sweep the kernel variants the product's
+ * auto policy was chosen from.
+ *
+ * Same conventions as fedavg_hip.h (device pointers, hipStream_t, FA_* codes);
+ * fa_bench_last_error() describes this library's last failure.
+ */
+#ifndef FEDAVG_HIP_BENCH_H
+#define FEDAVG_HIP_BENCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* fa_bench_last_error(void);
+
+/* Deterministic generator, bit-identical to fedlesscan_amd/synth.py. */
+int fa_synth_f32(float* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
+                 int64_t row0, int64_t col0, void* stream);
+int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64_t seed,
+                  int64_t row0, int64_t col0, void* stream);
+/* Contiguous read-only sweep of n floats, one 64 KiB chunk per block (16 B
+ * per lane) -> one partial per block in sink[block % sink_len] (values are
+ * meaningless): the streaming-read ceiling the fold is compared with. */
+int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
+/* fa_fedavg_f32 with an explicit kernel variant; variant 0 = the product's
+ * auto fold.  Variants other than 0 need 16-B aligned X / out and ldx % 4 == 0.
+ * Returns FA_ERR_ARG for an unknown variant. */
+int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
+                          const float* a, const float* s, float divisor,
+                          float* out, void* stream, int variant);
+int fa_num_variants(void);
+/* [host] short name of a variant, e.g. "gsband4_u8c4nt_nts"; "" if out of range. */
+const char* fa_variant_name(int variant);
+/* Same for the bf16 fold (variant 0 = fa_fedavg_bf16). */
+int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                           const float* a, const float* s, float divisor,
+                           float* out_f32, uint16_t* out_bf16, void* stream, int variant);
+int fa_num_bf16_variants(void);
+const char* fa_bf16_variant_name(int variant);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAVG_HIP_BENCH_H */

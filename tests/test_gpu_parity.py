@@ -27,6 +27,12 @@ def lib():
     return _lib
 
 
+def _bcheck(rc, what):
+    """Status of a libfedavg_hip_bench.so call (variants, generator)."""
+    from fedlesscan_amd import _lib
+    _lib.check(rc, what, bench=True)
+
+
 def _bits_equal(a, b):
     return G.same_bits(np.asarray(a), np.asarray(b))
 
@@ -164,6 +170,7 @@ def test_fold_f32_pitch_and_misalignment(dev, offset, pad):
 
 def test_all_variants_bit_identical(dev, lib):
     L = lib.load()
+    B = lib.load_bench()
     N, P = 77, 50003
     X = torch.from_numpy(synth.clients_f32(8, N, 0, P)).to(dev)
     w = synth.cardinalities(8, N)
@@ -171,10 +178,10 @@ def test_all_variants_bit_identical(dev, lib):
     s = torch.tensor([(r + 1) / 11 for r in synth.round_ids(8, N, 10, 2)], dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     outs = []
-    for v in range(L.fa_num_variants()):
+    for v in range(B.fa_num_variants()):
         for sp in (None, s):
             o = _sentinel(P, dev)
-            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+            _bcheck(B.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
                                               None if sp is None else sp.data_ptr(),
                                               float(np.float32(sum(w))), o.data_ptr(), st, v), "variant")
             outs.append((v, sp is None, o.cpu().numpy()))
@@ -285,6 +292,7 @@ def test_bf16_matches_definition(dev, N, P, scored):
 
 def test_bf16_variants_bit_identical(dev, lib):
     L = lib.load()
+    B = lib.load_bench()
     N, P = 37, 8 * 3000 + 5
     Xb = synth.clients_bf16(71, N, 0, P)
     w = synth.cardinalities(71, N)
@@ -292,10 +300,10 @@ def test_bf16_variants_bit_identical(dev, lib):
     Xd = torch.from_numpy(Xb.view(np.int16)).to(dev)
     a = torch.tensor(w, dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
-    for v in range(L.fa_num_bf16_variants()):
+    for v in range(B.fa_num_bf16_variants()):
         o = _sentinel(P, dev)
         ob = torch.full((P,), -1, dtype=torch.int16, device=dev)
-        lib.check(L.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
+        _bcheck(B.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
                                            o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
         assert _bits_equal(o.cpu().numpy(), exp), v
         assert np.array_equal(ob.cpu().numpy().view(np.uint16), expb), v
@@ -318,14 +326,15 @@ def test_f64_and_int_paths(dev):
 
 def test_gpu_synth_matches_host(dev, lib):
     L = lib.load()
+    B = lib.load_bench()
     st = torch.cuda.current_stream(dev).cuda_stream
     X = torch.empty((5, 3000), dtype=torch.float32, device=dev)
-    lib.check(L.fa_synth_f32(X.data_ptr(), 5, 2999, 3000, 77, 10, 123, st), "synth")
+    _bcheck(B.fa_synth_f32(X.data_ptr(), 5, 2999, 3000, 77, 10, 123, st), "synth")
     exp = synth.clients_f32(77, 5, 123, 2999, row0=10)
     assert np.array_equal(X[:, :2999].cpu().numpy().view(np.uint32), exp.view(np.uint32))
-    B = torch.empty((3, 1000), dtype=torch.int16, device=dev)
-    lib.check(L.fa_synth_bf16(B.data_ptr(), 3, 1000, 1000, 78, 0, 5, st), "synth_bf16")
-    assert np.array_equal(B.cpu().numpy().view(np.uint16), synth.clients_bf16(78, 3, 5, 1000))
+    Xb = torch.empty((3, 1000), dtype=torch.int16, device=dev)
+    _bcheck(B.fa_synth_bf16(Xb.data_ptr(), 3, 1000, 1000, 78, 0, 5, st), "synth_bf16")
+    assert np.array_equal(Xb.cpu().numpy().view(np.uint16), synth.clients_bf16(78, 3, 5, 1000))
 
 
 def test_error_mapping(dev, lib):
@@ -353,10 +362,11 @@ def _full_size_check(dev, lib, N, P, seed, dtype, scored, card_hi=600, block=1 <
     the inputs block by block with the bit-identical host generator)."""
     from fedlesscan_amd import engine
     L = lib.load()
+    B = lib.load_bench()
     st = torch.cuda.current_stream(dev).cuda_stream
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
     X = torch.empty((N, P), dtype=tdt, device=dev)
-    fn = L.fa_synth_f32 if dtype == "f32" else L.fa_synth_bf16
+    fn = B.fa_synth_f32 if dtype == "f32" else B.fa_synth_bf16
     lib.check(fn(X.data_ptr(), N, P, P, seed, 0, 0, st), "synth")
     w = synth.cardinalities(seed, N, 1, card_hi)
     sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
@@ -437,6 +447,7 @@ def test_every_variant_writes_every_column(dev, lib, P):
     """Column tails (P % 4 != 0) and partial last blocks for every fp32 variant,
     folded from scratch and as a continued chunked fold."""
     L = lib.load()
+    B = lib.load_bench()
     N = 6
     X = torch.from_numpy(synth.clients_f32(300 + P, N, 0, P)).to(dev)
     w = synth.cardinalities(300 + P, N)
@@ -444,9 +455,9 @@ def test_every_variant_writes_every_column(dev, lib, P):
     div = float(np.float32(sum(w)))
     st = torch.cuda.current_stream(dev).cuda_stream
     exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)))
-    for v in range(L.fa_num_variants()):
+    for v in range(B.fa_num_variants()):
         o = _sentinel(P, dev)
-        lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(), None, div, o.data_ptr(), st, v),
+        _bcheck(B.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(), None, div, o.data_ptr(), st, v),
                   "variant")
         assert _bits_equal(o.cpu().numpy(), exp), (v, P)
     acc = _sentinel(P, dev)
@@ -459,6 +470,7 @@ def test_every_variant_writes_every_column(dev, lib, P):
 @pytest.mark.parametrize("P", [1, 7, 9, 15, 2049, 2055, 8 * 256 * 2 + 3, 8 * 256 * 4 + 7, 65541])
 def test_every_bf16_variant_writes_every_column(dev, lib, P):
     L = lib.load()
+    B = lib.load_bench()
     N = 5
     Xb = synth.clients_bf16(400 + P, N, 0, P)
     w = synth.cardinalities(400 + P, N)
@@ -466,10 +478,10 @@ def test_every_bf16_variant_writes_every_column(dev, lib, P):
     Xd = torch.from_numpy(Xb.view(np.int16)).to(dev)
     a = torch.tensor(w, dtype=torch.float32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
-    for v in range(L.fa_num_bf16_variants()):
+    for v in range(B.fa_num_bf16_variants()):
         o = _sentinel(P, dev)
         ob = torch.full((P,), -1, dtype=torch.int16, device=dev)
-        lib.check(L.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
+        _bcheck(B.fa_fedavg_bf16_variant(Xd.data_ptr(), N, P, P, a.data_ptr(), None, float(np.float32(sum(w))),
                                            o.data_ptr(), ob.data_ptr(), st, v), "bf16 variant")
         assert _bits_equal(o.cpu().numpy(), exp), (v, P)
         assert np.array_equal(ob.cpu().numpy().view(np.uint16), expb), (v, P)
@@ -522,8 +534,8 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
     assert _bits_equal(out.cpu().numpy(), exp)
 
 
-def _lds_variants(L):
-    return [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"lds")]
+def _lds_variants(B):
+    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith(b"lds")]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
@@ -533,6 +545,7 @@ def test_lds_variants_chunk_and_tile_edges(dev, lib, N, P):
     boundaries and the partial tail quad: plain, stall-aware, and a chunked
     continuation (acc carried, divide at the end), all bit-exact vs the oracle."""
     L = lib.load()
+    B = lib.load_bench()
     X = torch.from_numpy(synth.clients_f32(700 + N, N, 0, P)).to(dev)
     w = synth.cardinalities(700 + P, N)
     sc = [(r + 1) / 11 for r in synth.round_ids(700 + N, N, 10, 2)]
@@ -543,15 +556,15 @@ def test_lds_variants_chunk_and_tile_edges(dev, lib, N, P):
     Xh = X.cpu().numpy()
     exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
     exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
-    variants = _lds_variants(L)
+    variants = _lds_variants(B)
     assert len(variants) >= 4
     for v in variants:
         for sp, e in ((None, exp), (s, exp_s)):
             o = _sentinel(P, dev)
-            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+            _bcheck(B.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
                                               None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v),
                       "lds variant")
-            assert _bits_equal(o.cpu().numpy(), e), (L.fa_variant_name(v), N, P, sp is not None)
+            assert _bits_equal(o.cpu().numpy(), e), (B.fa_variant_name(v), N, P, sp is not None)
 
 
 @pytest.mark.parametrize("N,P,pad", [(9, 1030, 2), (300, 65537, 63), (5, 300001, 3), (257, 2_100_003, 61),
@@ -742,6 +755,7 @@ def test_band_variants_multi_band(dev, lib, P):
     every band boundary and the tail, plain, stall-aware and as a chunked
     continuation, bit-exact vs the oracle."""
     L = lib.load()
+    B = lib.load_bench()
     N = 3
     X = torch.from_numpy(synth.clients_f32(81, N, 0, P)).to(dev)
     w = synth.cardinalities(81, N)
@@ -753,14 +767,14 @@ def test_band_variants_multi_band(dev, lib, P):
     Xh = X.cpu().numpy()
     exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
     exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
-    bands = [v for v in range(L.fa_num_variants()) if L.fa_variant_name(v).startswith(b"gsband")]
+    bands = [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith(b"gsband")]
     assert bands
     for v in bands + [0]:
         for sp, e in ((None, exp), (s, exp_s)):
             o = _sentinel(P, dev)
-            lib.check(L.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
+            _bcheck(B.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(),
                                               None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v), "v")
-            assert _bits_equal(o.cpu().numpy(), e), (L.fa_variant_name(v), sp is not None)
+            assert _bits_equal(o.cpu().numpy(), e), (B.fa_variant_name(v), sp is not None)
     acc = _sentinel(P, dev)  # auto policy as a two-chunk continuation
     lib.check(L.fa_fold_f32(X.data_ptr(), 2, P, P, a.data_ptr(), None, None, div, 0, acc.data_ptr(), st), "f")
     lib.check(L.fa_fold_f32(X[2].data_ptr(), 1, P, P, a[2:].data_ptr(), None, acc.data_ptr(), div, 1,

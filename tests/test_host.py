@@ -31,10 +31,31 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     assert set(declared) == set(_lib._PROTOS), "ctypes prototypes out of sync with the header"
     assert L.fa_abi_version() == _lib.ABI_VERSION
+    # the bench / tuning library exports its own header, and the product does not carry it
+    B = _lib.load_bench()
+    bench = _lib.header_functions(_lib.BENCH_HEADER)
+    assert not [f for f in bench if not hasattr(B, f)]
+    assert set(bench) == set(_lib._BENCH_PROTOS)
+    assert not set(bench) & set(declared)
+    assert not [f for f in bench if hasattr(L, f)], "tuning entry points leaked into the product library"
+
+
+def test_product_library_exports_only_the_header():
+    """`nm -D`: every exported fa_* symbol of libfedavg_hip.so is declared in
+    include/fedavg_hip.h (no tuning scaffolding in the product ABI)."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or shutil.which("llvm-nm")
+    if nm is None:
+        pytest.skip("no nm")
+    out = subprocess.run([nm, "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("fa_")}
+    assert exported == set(_lib.header_functions())
 
 
 def test_library_variant_table():
-    L = _lib.load()
+    L = _lib.load_bench()
     n = L.fa_num_variants()
     assert n >= 1
     names = [L.fa_variant_name(i).decode() for i in range(n)]

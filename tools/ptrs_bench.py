@@ -24,7 +24,7 @@ N, P = args.clients, args.params
 L = _lib.load()
 st = torch.cuda.current_stream(dev).cuda_stream
 X = torch.empty((N, P), dtype=torch.float32, device=dev)
-_lib.check(L.fa_synth_f32(X.data_ptr(), N, P, P, 9, 0, 0, st), "synth")
+_lib.check(_lib.load_bench().fa_synth_f32(X.data_ptr(), N, P, P, 9, 0, 0, st), "synth", bench=True)
 rows = [X[i].clone() for i in range(N)]  # separate allocations
 w = synth.cardinalities(9, N)
 
