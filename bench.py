@@ -36,7 +36,7 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import SlotLayout  # noqa: E402
+from fedlesscan_amd.sharding import SlotLayout, _gather_into  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -136,7 +136,8 @@ class Workload:
         self.out_bf16 = torch.empty(W, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else None
         elt = 4 if self.dtype == "f32" else 2
         # algorithmic bytes per step on this rank: every real input element once + the fp32 output once
-        self.bytes = self.N * self.P * elt + self.P * 4
+        # (+ the bf16 copy of the output for bf16 models)
+        self.bytes = self.N * self.P * elt + self.P * 4 + (self.P * 2 if self.dtype == "bf16" else 0)
         torch.cuda.synchronize()
 
     def launch(self, variant=0, k=0):
@@ -240,8 +241,8 @@ def main():
     wl = Workload(cfg, rank, world, dev, rounds)
     B = _lib.load_bench()
     lay = wl.layout
-    full = torch.empty(lay.padded_total, dtype=torch.float32, device=dev) if world > 1 else None
-    gloo = world > 1 and dist.get_backend() == "gloo"
+    full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
+                       device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
     if args.sweep and rank == 0:
@@ -269,31 +270,33 @@ def main():
                 f"min {ts[0]:.3f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
 
     sub = lay.sub
+    # the exchanged model: fp32 result for fp32 updates, the RNE bf16 result
+    # for bf16 updates (2 B/param over xGMI: half the bytes of the fp32 result)
+    send = wl.out if wl.dtype == "f32" else wl.out_bf16
 
-    def step(events=None):
+    def step(ev=None):
+        """ev = (fold events per round, end event) for the timed steps."""
         works = []
         for k in range(rounds):
-            if events is not None:
-                events[k][0].record(stream)
+            if ev is not None:
+                ev[0][k][0].record(stream)
             wl.launch(args.variant, k)
-            if events is not None:
-                events[k][1].record(stream)
+            if ev is not None:
+                ev[0][k][1].record(stream)
             if world > 1:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
                 lo, hi = lay.round_range(k)
-                piece = wl.out[k * sub:(k + 1) * sub]
-                if gloo:  # rehearsal only: host-staged
-                    host = torch.empty(hi - lo, dtype=torch.float32)
-                    dist.all_gather_into_tensor(host, piece.cpu())
-                    full[lo:hi].copy_(host)
-                else:
-                    works.append(dist.all_gather_into_tensor(full[lo:hi], piece, async_op=True))
+                w = _gather_into(full[lo:hi], send[k * sub:(k + 1) * sub], None, async_op=True)
+                if w is not None:
+                    works.append(w)
         for w in works:
-            w.wait()
+            w.wait()  # the compute stream waits for the RCCL stream
+        if ev is not None:
+            ev[1].record(stream)
 
     for _ in range(args.warmup):
         step()
-    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(rounds)] for _ in range(args.steps)]
+    evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(rounds)], torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -311,19 +314,22 @@ def main():
     gather_ok = None
     if world > 1:  # my slots inside the reassembled model must be my fold output, bit for bit
         ok = True
+        iv = torch.int32 if wl.dtype == "f32" else torch.int16
         for k, (lo, hi) in enumerate(wl.slots):
             if hi > lo:
-                ok &= torch.equal(full[lo:hi].view(torch.int32),
-                                  wl.out[k * sub:k * sub + hi - lo].view(torch.int32))
+                ok &= torch.equal(full[lo:hi].view(iv), send[k * sub:k * sub + hi - lo].view(iv))
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
-    kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in ev) for ev in evs]
+    kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in folds) for folds, _ in evs]
+    # the exchange left exposed: from the last fold's end to the end of the step
+    exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
     kern_avg = float(np.mean(kern_ms))
+    exposed_avg = float(np.mean(exposed_ms))
     if world > 1:
-        t = torch.tensor([kern_avg], dtype=torch.float64, device=dev)
+        t = torch.tensor([kern_avg, exposed_avg], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        kern_avg = float(t.item())
+        kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
 
     # streaming-read ceiling over the same HBM bytes (contiguous, no fold)
     # byte-level sweep: bf16 input is read as the same bytes viewed as fp32 quads
@@ -397,6 +403,12 @@ def main():
             },
             "cpu_baseline": cpu,
             "gather_check": gather_ok,
+            # per-rank split of a step at N > 1 (max over ranks): the fold kernels,
+            # and the all-gather left exposed after the last fold of the step
+            "fold_ms": round(kern_avg, 4),
+            "gather_exposed_ms": round(exposed_avg, 4) if world > 1 else None,
+            "gather_bytes_per_rank": (lay.padded_total * (4 if wl.dtype == "f32" else 2)
+                                      * (world - 1) // world) if world > 1 else 0,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

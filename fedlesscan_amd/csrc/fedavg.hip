@@ -101,11 +101,25 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
                                N, P, a, s, divisor, out, tiles);                                               \
     }
     // large models: ~one block per CU walking 16 KiB tiles (as the stacked
-    // default); narrow ones: one block per 4 KiB tile
-    if ((P >> 2) >= (int64_t)kBlock * 4 * cu_count()) FA_R(8, 4, (int64_t)cu_count())
+    // default); mid-size: one block per 4 KiB tile; narrow models (the
+    // stacked fold's LDS-staged picks): the LDS-staged fold reading row bases
+    // from the table
+    const F32Pick pk = pick_f32(N, P);
+    rc = FA_OK;
+    if (pk == F32Pick::kLdsW4)
+        rc = launch_lds_flags<4, 32, 16, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
+    else if (pk == F32Pick::kLdsW4T32)
+        rc = launch_lds_flags<4, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
+    else if (pk == F32Pick::kLdsW8)
+        rc = launch_lds_flags<8, 64, 32, 1, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
+    else if ((P >> 2) >= (int64_t)kBlock * 4 * cu_count()) FA_R(8, 4, (int64_t)cu_count())
     else FA_R(8, 1, 0)
 #undef FA_R
-    return check_launch("k_fold_f32_rows_gs");
+    if (rc) return rc;
+    return check_launch("fa_fedavg_f32_ptrs_aligned");
 }
 
 int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,

@@ -226,8 +226,9 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
     int rc = check_common(N, P, ldx, X, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
+    // unaligned layouts take the product's scalar fold, whatever the variant
     if (!aligned16(X) || (ldx % 4) || !aligned16(out))
-        return fail(FA_ERR_ARG, "kernel variants need 16-B aligned X and out and ldx %% 4 == 0");
+        return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream);
     hipStream_t st = (hipStream_t)stream;
     const bool sc = s != nullptr, acc = false, fin = true;
     const float* acc_in = nullptr;
@@ -313,7 +314,7 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     if (!aligned16(X) || (ldx % 8) || !aligned16(out_f32) || (out_bf16 && !aligned16(out_bf16)))
-        return fail(FA_ERR_ARG, "bf16 variants need 16-B aligned X and outputs and ldx %% 8 == 0");
+        return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
     hipStream_t st = (hipStream_t)stream;
 #define FA_BF(U, C)                                                                                         \
     {                                                                                                       \

@@ -211,7 +211,11 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
 //   every other fold.  The partial quad of the P%4 tail columns is staged
 //   like a full one (element loads, zero-filled) and only its real columns
 //   are stored.  Per-chunk factors a[], s[] are staged in LDS too.
-template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1>
+//   ROWS: X is really `const float* const* xi`, a device table of N row
+//   pointers (separately allocated client rows, every row 16-B aligned;
+//   fa_fedavg_f32_ptrs_aligned); ldx is unused.  The table is read per lane
+//   (8 B, cache-resident: every block reads the same N entries).
+template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1, bool ROWS = false>
 __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
@@ -228,6 +232,15 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const int64_t ldq = ldx >> 2;
     const int t = threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const float* const* xi = reinterpret_cast<const float* const*>(X);
+    auto row4 = [&](int64_t row) -> const f32x4* {  // quad 0 of a client row
+        if constexpr (ROWS) return reinterpret_cast<const f32x4*>(xi[row]);
+        else return X4 + row * ldq;
+    };
+    auto rowf = [&](int64_t row) -> const float* {
+        if constexpr (ROWS) return xi[row];
+        else return X + row * ldx;
+    };
     // one chunk in registers: its LQ quads per lane and (lanes < R) its factors
     struct Stage {
         f32x4 v[LQ];
@@ -244,7 +257,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
 #pragma unroll
         for (int j = 0; j < LQ; ++j) {
             const int e = t + j * NT;
-            g.v[j] = __builtin_nontemporal_load(X4 + (c * R + e / TQ) * ldq + q0 + e % TQ);
+            g.v[j] = __builtin_nontemporal_load(row4(c * R + e / TQ) + q0 + e % TQ);
         }
         if (t < R) {
             g.fv = a[c * R + t];
@@ -258,10 +271,11 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
             const int64_t row = c * R + r, q = q0 + qq;
             if (row < N && qq < tq) {
                 if (q < nq) {
-                    g.v[j] = __builtin_nontemporal_load(X4 + row * ldq + q);
+                    g.v[j] = __builtin_nontemporal_load(row4(row) + q);
                 } else {  // partial tail quad: P%4 real columns
                     f32x4 x = {0.f, 0.f, 0.f, 0.f};
-                    for (int k = 0; k < (int)(P & 3); ++k) x[k] = X[row * ldx + q * 4 + k];
+                    const float* rp = rowf(row);
+                    for (int k = 0; k < (int)(P & 3); ++k) x[k] = rp[q * 4 + k];
                     g.v[j] = x;
                 }
             }
@@ -952,7 +966,7 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 }
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
-template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false>
+template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false, bool ROWS = false>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
     const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
@@ -960,7 +974,7 @@ int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
         return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
     const dim3 grid((unsigned)blocks), block(NW * 64);
 #define FA_L(SC, ACC, FIN)                                                                                   \
-    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH>), grid, block, 0, st, X, N, P, ldx, a, s, \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH, ROWS>), grid, block, 0, st, X, N, P, ldx, a, s, \
                        acc_in, d, out)
     if constexpr (!ALLF) {
         if (sc) FA_L(true, false, true); else FA_L(false, false, true);

@@ -2,7 +2,8 @@
 
 Layering
   engine.fold_stacked(X, weights, scores)   X: CUDA tensor [N, P] (row pitch = X.stride(0))
-  engine.fold_rows(rows, weights, scores)   N separately allocated CUDA rows (pointer list)
+  engine.fold_rows(rows, weights, scores)   N separately allocated CUDA rows (pointer list;
+                                            engine.RowSet prepares a reusable row set)
   engine.aggregate_layers(params, weights)  host or device per-client layer lists -> per-layer outputs
 
 The scalar factors are formed on the host exactly as numpy forms them in the
@@ -49,12 +50,89 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 def result_dtype(in_dtype: np.dtype, weights: Sequence, scores: Optional[Sequence] = None,
                  total=None) -> np.dtype:
     """dtype numpy gives `reduce(add, [x * n_i (* s_i)]) / sum(n)` (NEP 50 weak Python scalars)."""
+    in_dtype = np.dtype(in_dtype)
+    if in_dtype.kind == "f":
+        # Python bool / int / float scalars are weak: a float array keeps its dtype
+        kinds = set(map(type, weights))
+        if scores is not None:
+            kinds.update(map(type, scores))
+        if total is not None:
+            kinds.add(type(total))
+        if kinds <= {bool, int, float}:
+            return in_dtype
     if total is None:
         total = sum(weights)
     dt = np.result_type(in_dtype, *weights, *(scores or ()), total)
     if dt.kind in "iu" or dt.kind == "b":
         dt = np.result_type(dt, np.float64)  # true_divide of integers
     return dt
+
+
+_EXACT_F64 = float(2 ** 53)
+
+
+def round_scalars(values: Sequence, dt: np.dtype) -> np.ndarray:
+    """[dt(v) for v in values] -- numpy's rounding of Python (or numpy) scalars
+    to `dt`, vectorised.  Going through float64 first is exact whenever every
+    value is representable there (ints below 2**53, any float), so rounding the
+    float64 array once gives the same bits as rounding each scalar; anything
+    else takes the per-element loop."""
+    dt = np.dtype(dt)
+    try:
+        v = np.asarray(values, dtype=np.float64)
+    except (TypeError, ValueError, OverflowError):
+        v = None
+    if v is not None and v.ndim == 1 and dt.kind == "f" and not (v.size and np.abs(v).max() >= _EXACT_F64):
+        return v.astype(dt)
+    return np.array([dt.type(x) for x in values], dtype=dt)
+
+
+class _FactorRing:
+    """Page-locked staging slots for the per-client factors of one device: the
+    factors of a call travel in ONE async H2D on the caller's stream (instead
+    of synchronous pageable copies).  A slot is rewritten only after the copy
+    that last read it has completed (its event)."""
+
+    SLOTS, SLOT_BYTES = 8, 1 << 17
+
+    def __init__(self):
+        self.host = [torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True) for _ in range(self.SLOTS)]
+        self.done = [None] * self.SLOTS
+        self.k = 0
+
+    def stage(self, parts: List[np.ndarray], dev: torch.device) -> List[torch.Tensor]:
+        nbytes = sum(p.nbytes for p in parts)
+        if nbytes > self.SLOT_BYTES:  # very many clients: plain copies
+            return [torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in parts]
+        k = self.k
+        self.k = (k + 1) % self.SLOTS
+        if self.done[k] is not None:
+            self.done[k].synchronize()
+        hv = self.host[k].numpy()
+        off = 0
+        for p in parts:
+            hv[off:off + p.nbytes] = np.ascontiguousarray(p).view(np.uint8).reshape(-1)
+            off += p.nbytes
+        d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        d.copy_(self.host[k][:nbytes], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self.done[k] = ev
+        out, off = [], 0
+        for p in parts:
+            out.append(d[off:off + p.nbytes].view(_NP_TO_TORCH[p.dtype]))
+            off += p.nbytes
+        return out
+
+
+_rings: dict = {}
+
+
+def stage_factors(parts: List[np.ndarray], dev: torch.device) -> List[torch.Tensor]:
+    ring = _rings.get(dev)
+    if ring is None:
+        ring = _rings[dev] = _FactorRing()
+    return ring.stage(parts, dev)
 
 
 class Factors:
@@ -64,18 +142,17 @@ class Factors:
                  total=None):
         self.total = sum(weights) if total is None else total
         if int_weights:
-            self.a = np.array([int(w) for w in weights], dtype=np.int64)
+            self.a = np.asarray([int(w) for w in weights], dtype=np.int64)
             self.div = float(self.total)
         else:
-            t = dt.type
-            self.a = np.array([t(w) for w in weights], dtype=dt)
-            self.div = t(self.total)
-        self.s = None if scores is None else np.array([dt.type(x) for x in scores], dtype=dt)
+            self.a = round_scalars(weights, dt)
+            self.div = np.dtype(dt).type(self.total)
+        self.s = None if scores is None else round_scalars(scores, dt)
 
     def to(self, device):
-        a = torch.from_numpy(self.a).to(device, non_blocking=False)
-        s = None if self.s is None else torch.from_numpy(self.s).to(device, non_blocking=False)
-        return a, s
+        parts = [self.a] if self.s is None else [self.a, self.s]
+        staged = stage_factors(parts, device)
+        return staged[0], (staged[1] if self.s is not None else None)
 
 
 def _check_matrix(X: torch.Tensor) -> tuple[int, int, int]:
@@ -170,32 +247,67 @@ def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Te
     return base.as_strided((N, P), (step // 4, 1))
 
 
-def fold_rows(rows: Sequence[torch.Tensor], weights: Sequence, scores: Optional[Sequence] = None, *,
+class RowSet:
+    """N client rows already on the GPU, prepared once for repeated folds.
+
+    A device-resident simulation keeps each client's update in its own
+    persistent tensor and refolds the same rows every round.  Building a
+    RowSet validates the rows and looks at their placement ONCE:
+      - rows of one allocation at a constant forward pitch (X[i] of a stacked
+        tensor) become one [N, P] strided view: the stacked fold, no table;
+      - other fp32 rows get a device table of row pointers for
+        fa_fedavg_f32_ptrs_aligned (every row 16-B aligned) or
+        fa_fedavg_f32_ptrs (any alignment).
+    fold_rows(rowset, weights) then costs the factor upload and the kernel.
+    The RowSet keeps the tensors alive; their CONTENTS may change between
+    folds, their storage may not (re-create the RowSet after reallocating)."""
+
+    def __init__(self, rows: Sequence[torch.Tensor]):
+        N = len(rows)
+        if N == 0:
+            _lib.check(_lib.FA_ERR_NO_CLIENTS, "RowSet")
+        r0 = rows[0]
+        P, dev, dt = r0.numel(), r0.device, r0.dtype
+        if not r0.is_cuda:
+            raise ValueError("rows must be CUDA (HIP) tensors")
+        for r in rows:
+            if r.numel() != P or r.dtype != dt or not r.is_contiguous() or r.device != dev:
+                raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
+        self.rows = [r.reshape(-1) for r in rows]
+        self.N, self.P, self.device, self.dtype = N, P, dev, dt
+        self.view = None
+        self.ptrs = None
+        self.aligned = False
+        if dt == torch.float32 and P > 0:
+            host_ptrs = np.fromiter(map(torch.Tensor.data_ptr, self.rows), dtype=np.int64, count=N)
+            self.view = _equal_stride_view(self.rows, host_ptrs, P)
+            if self.view is None:
+                self.ptrs = torch.from_numpy(host_ptrs).to(dev)
+                self.aligned = not (host_ptrs % 16).any()
+
+
+def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
               out: Optional[torch.Tensor] = None, total=None) -> torch.Tensor:
-    """Same fold over separately allocated 1-D CUDA rows (no stacking copy for fp32)."""
-    N = len(rows)
-    if N == 0:
-        _lib.check(_lib.FA_ERR_NO_CLIENTS, "fold_rows")
-    P = rows[0].numel()
-    dev = rows[0].device
-    for r in rows:
-        if r.numel() != P or r.dtype != rows[0].dtype or not r.is_contiguous() or r.device != dev:
-            raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
-    if rows[0].dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32:
-        return fold_stacked(torch.stack([r.reshape(-1) for r in rows]), weights, scores, out=out, total=total)
+    """The fold over separately allocated 1-D CUDA rows (no stacking copy for
+    fp32).  `rows` is a RowSet (prepared once, reusable) or a sequence of
+    tensors (a RowSet is built for this call)."""
+    rs = rows if isinstance(rows, RowSet) else RowSet(rows)
+    if len(weights) != rs.N or (scores is not None and len(scores) != rs.N):
+        raise InvalidParameterShapeError(f"{rs.N} rows but {len(weights)} weights"
+                                         + ("" if scores is None else f" / {len(scores)} scores"))
+    if rs.dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32:
+        return fold_stacked(torch.stack(rs.rows), weights, scores, out=out, total=total)
+    if rs.view is not None or rs.P == 0:
+        # rows of one allocation at a fixed pitch: the stacked fold, no pointer table
+        X = rs.view if rs.view is not None else torch.stack(rs.rows)
+        return fold_stacked(X, weights, scores, out=out, total=total)
+    dev = rs.device
     f = Factors(weights, scores, np.dtype(np.float32), total=total)
     a, s = f.to(dev)
-    host_ptrs = np.fromiter((r.data_ptr() for r in rows), dtype=np.int64, count=N)
-    view = _equal_stride_view(rows, host_ptrs, P)
-    if view is not None:  # rows of one allocation at a fixed pitch: the stacked fold, no pointer table
-        return fold_stacked(view, weights, scores, out=out, total=total)
-    ptrs = torch.from_numpy(host_ptrs).to(dev)
-    out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
-    aligned = not (host_ptrs % 16).any() and out.data_ptr() % 16 == 0
-    _lib.call("fa_fedavg_f32_ptrs_aligned" if aligned else "fa_fedavg_f32_ptrs", ptrs.data_ptr(), N, P,
+    out = out if out is not None else torch.empty(rs.P, dtype=torch.float32, device=dev)
+    aligned = rs.aligned and out.data_ptr() % 16 == 0
+    _lib.call("fa_fedavg_f32_ptrs_aligned" if aligned else "fa_fedavg_f32_ptrs", rs.ptrs.data_ptr(), rs.N, rs.P,
               a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), stream_ptr(dev))
-    # `ptrs` may be freed on return: the caching allocator reuses it only in
-    # stream order, i.e. after this kernel has read it.
     return out
 
 

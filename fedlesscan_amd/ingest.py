@@ -31,6 +31,7 @@ import torch
 
 from . import _lib
 from .aggregator.exceptions import InvalidParameterShapeError
+from .engine import round_scalars
 
 
 class StreamingFold:
@@ -163,10 +164,10 @@ class StreamingFold:
                     self.devbuf[b][r:r1].copy_(self.host[b][r:r1], non_blocking=True)
                     r = r1
                 fh = self.fac_host[b].numpy()
-                fh[0, :n] = [np.float32(w) for w in self.chunk_a[b]]  # fl32(n_i), numpy's rounding
+                fh[0, :n] = round_scalars(self.chunk_a[b], np.float32)  # fl32(n_i), numpy's rounding
                 scored = self.chunk_s[b][0] is not None
                 if scored:
-                    fh[1, :n] = [np.float32(x) for x in self.chunk_s[b]]
+                    fh[1, :n] = round_scalars(self.chunk_s[b], np.float32)
                 self.fac_dev[b].copy_(self.fac_host[b], non_blocking=True)
                 self.h2d_done[b].record(self.copy_stream)
             self.compute.wait_event(self.h2d_done[b])

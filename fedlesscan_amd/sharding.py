@@ -71,11 +71,30 @@ class SlotLayout:
         return k * self.world * self.sub, (k + 1) * self.world * self.sub
 
 
+def _gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
+    """all_gather_into_tensor of `piece` into `full`.  16-bit payloads travel
+    as bytes (bit-identical; an all-gather moves bytes, and gloo takes neither
+    bfloat16 nor int16).  Under gloo a device piece is staged through host
+    memory (CPU rehearsals only); under nccl this is RCCL over xGMI."""
+    if piece.dtype in (torch.bfloat16, torch.float16):
+        full, piece = full.view(torch.uint8), piece.view(torch.uint8)
+    if piece.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(full.shape, dtype=full.dtype)
+        dist.all_gather_into_tensor(host, piece.cpu(), group=group)
+        full.copy_(host)
+        return None
+    return dist.all_gather_into_tensor(full, piece, group=group, async_op=async_op)
+
+
 class ShardedAggregator:
     """Fold this rank's parameter bucket, then all-gather the global model.
 
-    `fold` maps (X_local [N, P_r], weights, scores) -> [P_r]; it defaults to
-    the HIP engine.  Tests on CPU (gloo) pass the oracle instead.
+    `fold` maps (X_local [N, P_r], weights, scores, out=, total=, want_bf16=)
+    -> [P_r] (or (f32, bf16) with want_bf16 on bf16 input), the contract of
+    engine.fold_stacked, which is the default.  Tests on CPU (gloo) pass the
+    oracle instead.  `total` is the divisor sum over EVERY weight (the
+    reference divides by sum(weights) even where zip() truncated the rows,
+    fed_avg_aggregator.py:31-35).
     """
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None):
@@ -105,22 +124,16 @@ class ShardedAggregator:
         else:
             padded = local
         if out is not None:
-            if out.numel() < chunk * self.world or not out.is_contiguous():
-                raise ValueError(f"out needs {chunk * self.world} contiguous elements")
+            if out.numel() < chunk * self.world or not out.is_contiguous() or out.dtype != local.dtype:
+                raise ValueError(f"out needs {chunk * self.world} contiguous {local.dtype} elements")
             full = out[: chunk * self.world]
         else:
             full = torch.empty(chunk * self.world, dtype=local.dtype, device=local.device)
-        if padded.is_cuda and dist.get_backend(self.group) == "gloo":
-            # gloo has no device transport: stage through host memory (rehearsal / no-RCCL hosts)
-            host = torch.empty(full.shape, dtype=full.dtype)
-            dist.all_gather_into_tensor(host, padded.cpu(), group=self.group)
-            full.copy_(host)
-        else:
-            dist.all_gather_into_tensor(full, padded, group=self.group)
+        _gather_into(full, padded, self.group, async_op=False)
         return full[:P]
 
     def aggregate(self, X_local: torch.Tensor, weights: Sequence, scores: Optional[Sequence] = None,
-                  P: Optional[int] = None) -> torch.Tensor:
+                  P: Optional[int] = None, total=None) -> torch.Tensor:
         """X_local = this rank's columns [start, end) of the stacked updates, all N clients."""
         if P is None:
             t = torch.tensor([X_local.shape[1]], dtype=torch.int64, device=X_local.device)
@@ -131,72 +144,101 @@ class ShardedAggregator:
         if X_local.shape[1] != hi - lo:
             raise ValueError(f"rank {self.rank} holds {X_local.shape[1]} columns, bucket is [{lo}, {hi})")
         if hi > lo:
-            local = self.fold(X_local, weights, scores)
+            local = self.fold(X_local, weights, scores, total=total)
         else:
             local = torch.empty(0, dtype=torch.float32, device=X_local.device)
         return self.gather(local, P)
 
     def aggregate_slots(self, X_local: torch.Tensor, weights: Sequence, scores: Optional[Sequence],
-                        layout: "SlotLayout", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        layout: "SlotLayout", out: Optional[torch.Tensor] = None, total=None) -> torch.Tensor:
         """Fold round by round and all-gather each round asynchronously, so the
         exchange of round k overlaps the fold of round k+1.
 
         X_local: [N, layout.local_width], this rank's slots side by side (columns
-        past P may hold anything; their outputs are trimmed).  Returns [P].
-        `fold` must accept out= (engine.fold_stacked does)."""
+        past P may hold anything; their outputs are trimmed).  Returns [P]:
+        float32 for fp32 updates; for bf16 updates the RNE bf16 model (the fold
+        still accumulates in fp32), so the exchange moves 2 bytes per parameter,
+        half the xGMI bytes of the fp32 result.  `fold` must accept out= (and
+        want_bf16= for bf16 input), as engine.fold_stacked does."""
         if X_local.shape[1] != layout.local_width:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
         sub = layout.sub
-        full = out if out is not None else torch.empty(layout.padded_total, dtype=torch.float32,
-                                                       device=X_local.device)
+        bf16 = X_local.dtype == torch.bfloat16
+        odt = torch.bfloat16 if bf16 else torch.float32
+        full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
+        if full.dtype != odt or full.numel() < layout.padded_total:
+            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
         local = torch.empty(layout.local_width, dtype=torch.float32, device=X_local.device)
+        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=X_local.device) if bf16 else None
         works = []
-        gloo = self.world > 1 and dist.get_backend(self.group) == "gloo"
         for k in range(layout.rounds):
             piece = local[k * sub:(k + 1) * sub]
             if sub:
-                self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece)
+                if bf16:
+                    _, pb = self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece, total=total,
+                                      want_bf16=True)
+                    local_b[k * sub:(k + 1) * sub].copy_(pb)
+                else:
+                    self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece, total=total)
+            send = local_b[k * sub:(k + 1) * sub] if bf16 else piece
             lo, hi = layout.round_range(k)
             if self.world == 1:
-                full[lo:hi].copy_(piece)
-            elif gloo and piece.is_cuda:
-                host = torch.empty(hi - lo, dtype=piece.dtype)
-                dist.all_gather_into_tensor(host, piece.cpu(), group=self.group)
-                full[lo:hi].copy_(host)
-            else:
-                works.append(dist.all_gather_into_tensor(full[lo:hi], piece, group=self.group, async_op=True))
+                full[lo:hi].copy_(send)
+                continue
+            w = _gather_into(full[lo:hi], send, self.group, async_op=True)
+            if w is not None:
+                works.append(w)
         for w in works:
             w.wait()
         return full[: layout.P]
 
     def aggregate_layers(self, parameters: Sequence[Sequence], weights: Sequence,
                          scores: Optional[Sequence] = None, device=None) -> List:
-        """Reference-shaped entry: every rank sees the same per-client layer lists
-        (numpy) and H2D-copies only its own bucket of each client's row."""
+        """Reference-shaped entry (fed_avg_aggregator.py:24-42 over per-client
+        layer lists): every rank sees the same per-client float32 numpy layers
+        and copies only the pieces of each layer that fall in its own bucket
+        (no full-row concatenation).  zip() truncation is kept: rows beyond the
+        shorter of parameters / weights / scores are not folded, but the divisor
+        is the sum of every weight.  Other dtypes (float64, integer, mixed) are
+        rejected: engine.aggregate_layers handles them on one GPU."""
         import numpy as np
+
+        from .aggregator.exceptions import InvalidParameterShapeError
+        from .engine import result_dtype
         n = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
         if n == 0:
             return []
         L = min(len(p) for p in parameters[:n])
         shapes = [np.asarray(parameters[0][li]).shape for li in range(L)]
+        for i in range(n):
+            for li in range(L):
+                x = parameters[i][li]
+                if not isinstance(x, np.ndarray) or x.dtype != np.float32 or x.shape != shapes[li]:
+                    raise InvalidParameterShapeError(
+                        f"sharded aggregation takes float32 numpy layers shaped like client 0's; client {i} "
+                        f"layer {li} is {getattr(x, 'dtype', type(x))} {getattr(x, 'shape', None)}")
+        sc = None if scores is None else list(scores[:n])
+        total = sum(weights)
+        if result_dtype(np.dtype(np.float32), list(weights), sc, total) != np.float32:
+            raise InvalidParameterShapeError("weights/scores promote the float32 layers (numpy scalar types)")
         sizes = [int(np.prod(s)) if len(s) else 1 for s in shapes]
-        P = sum(sizes)
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        P = int(offs[-1])
         lo, hi = self.bounds(P)
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        dt = np.asarray(parameters[0][0]).dtype
-        host = np.empty((n, hi - lo), dtype=dt)
-        for i in range(n):
-            row = np.concatenate([np.asarray(parameters[i][li]).reshape(-1) for li in range(L)])
-            host[i] = row[lo:hi]
-        X = torch.from_numpy(host).to(dev)
-        full = self.aggregate(X, list(weights[:n]), None if scores is None else list(scores[:n]), P=P)
+        host = torch.empty((n, hi - lo), dtype=torch.float32, pin_memory=dev.type == "cuda")
+        hv = host.numpy()
+        for li in range(L):  # layers overlapping [lo, hi) only
+            a, b = max(lo, int(offs[li])), min(hi, int(offs[li + 1]))
+            if a >= b:
+                continue
+            for i in range(n):
+                hv[i, a - lo:b - lo] = parameters[i][li].reshape(-1)[a - offs[li]:b - offs[li]]
+        X = host.to(dev, non_blocking=True) if dev.type == "cuda" else host
+        full = self.aggregate(X, list(weights[:n]), sc, P=P, total=total)
         if full.is_cuda:
             from . import engine
             flat = engine.to_host(full)
         else:
             flat = full.numpy()
-        outs, off = [], 0
-        for shp, sz in zip(shapes, sizes):
-            outs.append(flat[off:off + sz].reshape(shp))
-            off += sz
-        return outs
+        return [flat[offs[li]:offs[li + 1]].reshape(shapes[li]) for li in range(L)]

@@ -31,7 +31,8 @@ int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64
  * meaningless): the streaming-read ceiling the fold is compared with. */
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
 /* fa_fedavg_f32 with an explicit kernel variant; variant 0 = the product's
- * auto fold.  Variants other than 0 need 16-B aligned X / out and ldx % 4 == 0.
+ * auto fold.  Layouts the vector kernels cannot take (X / out not 16-B
+ * aligned, ldx % 4 != 0) run the product's scalar fold whatever the variant.
  * Returns FA_ERR_ARG for an unknown variant. */
 int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
                           const float* a, const float* s, float divisor,

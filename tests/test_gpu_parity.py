@@ -275,6 +275,41 @@ def test_aligned_ptr_rows(dev, N, P, scored):
     assert _bits_equal(got, exp)
 
 
+@pytest.mark.parametrize("N,P", [(2, 3), (31, 16387), (33, 40003), (129, 67267), (300, 300_001), (1024, 4096)])
+@pytest.mark.parametrize("scored", [False, True])
+def test_rowset_lds_pointer_fold(dev, N, P, scored):
+    """Separately allocated narrow rows take the LDS-staged fold with row bases
+    read from the pointer table (every LDS pick: 16- and 32-quad tiles, the
+    8-wave form at N >= 256); a RowSet built once refolds bit-exactly after
+    its rows' contents change in place."""
+    from fedlesscan_amd import engine
+    X = synth.clients_f32(91 + N, N, 0, P)
+    w = synth.cardinalities(91 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(91, N, 10, 2)] if scored else None
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]
+    rs = engine.RowSet(rows)
+    assert rs.view is None and rs.aligned
+    s32 = None if sc is None else np.array(sc, np.float32)
+    for rnd in range(2):
+        got = engine.fold_rows(rs, w, sc, out=_sentinel(P, dev)).cpu().numpy()
+        exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=s32)
+        assert _bits_equal(got, exp), rnd
+        X = synth.clients_f32(191 + N, N, 0, P)  # next round: new contents, same tensors
+        for i in range(N):
+            rows[i].copy_(torch.from_numpy(X[i]))
+
+
+def test_rowset_rejects_mixed_rows(dev):
+    from fedlesscan_amd import InvalidParameterShapeError, engine
+    with pytest.raises(InvalidParameterShapeError):
+        engine.RowSet([torch.zeros(4, device=dev), torch.zeros(5, device=dev)])
+    with pytest.raises(InvalidParameterShapeError):
+        engine.RowSet([torch.zeros(4, device=dev), torch.zeros(4, device=dev, dtype=torch.float64)])
+    rs = engine.RowSet([torch.zeros(4, device=dev), torch.zeros(4, device=dev)])
+    with pytest.raises(InvalidParameterShapeError):
+        engine.fold_rows(rs, [1, 2, 3])
+
+
 @pytest.mark.parametrize("N,P", [(1, 8), (5, 9), (64, 8 * 1000 + 3), (256, 65536)])
 @pytest.mark.parametrize("scored", [False, True])
 def test_bf16_matches_definition(dev, N, P, scored):

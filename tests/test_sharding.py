@@ -62,13 +62,20 @@ def _free_port():
     return p
 
 
-def _oracle_fold(X, w, s=None, out=None, **_):
+def _oracle_fold(X, w, s=None, out=None, total=None, want_bf16=False):
+    """engine.fold_stacked's contract, computed by the oracle (CPU ranks)."""
     from oracle import fedavg_oracle as O
-    res = torch.from_numpy(O.fedavg_stacked(np.ascontiguousarray(X.numpy()), w, s))
+    if X.dtype == torch.bfloat16:
+        bits = np.ascontiguousarray(X.view(torch.int16).numpy()).view(np.uint16)
+        f, b = O.fedavg_stacked_bf16(bits, w, s, total)
+        res, resb = torch.from_numpy(f), torch.from_numpy(b.view(np.int16)).view(torch.bfloat16)
+    else:
+        res = torch.from_numpy(O.fedavg_stacked(np.ascontiguousarray(X.numpy()), w, s, total))
+        resb = None
     if out is not None:
         out.copy_(res)
-        return out
-    return res
+        res = out
+    return (res, resb) if want_bf16 else res
 
 
 def _worker(rank, world, port, N, P, seed, scored, q):
@@ -145,3 +152,115 @@ def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds):
     for r in range(world):
         out = np.frombuffer(got[r], dtype=np.float32)
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
+
+
+def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q):
+    """BASELINE config 4's layout in miniature: bf16 client rows in round-robin
+    slots, fp32 fold per slot, RNE-bf16 slot outputs all-gathered (2 B/param)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        agg = ShardedAggregator(fold=_oracle_fold)
+        lay = SlotLayout(P, world, rounds)
+        X = torch.zeros((N, lay.local_width), dtype=torch.int16)
+        for k, (lo, hi) in enumerate(lay.slots(rank)):
+            if hi > lo:
+                X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(
+                    synth.clients_bf16(seed, N, lo, hi - lo).view(np.int16))
+        w = synth.cardinalities(seed, N)
+        sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
+        full = agg.aggregate_slots(X.view(torch.bfloat16), w, sc, lay)
+        assert full.dtype == torch.bfloat16 and full.numel() == P
+        q.put((rank, full.view(torch.int16).numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P,rounds", [(2, 4099, 4), (3, 1000, 2)])
+def test_bf16_slot_gather_gloo_matches_oracle(world, P, rounds):
+    from oracle import fedavg_oracle as O
+    N, seed = 6, 29
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bf16_slot_worker, args=(r, world, port, N, P, rounds, seed, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
+    _, expb = O.fedavg_stacked_bf16(synth.clients_bf16(seed, N, 0, P), synth.cardinalities(seed, N), sc)
+    for r in range(world):
+        assert np.array_equal(np.frombuffer(got[r], dtype=np.uint16), expb), r
+
+
+SHAPES = [(3, 5, 7), (64,), (33, 17), (1,), (900,)]
+
+
+def _layers_worker(rank, world, port, N, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        agg = ShardedAggregator(fold=_oracle_fold)
+        P = sum(int(np.prod(s)) for s in SHAPES)
+        X = synth.clients_f32(seed, N, 0, P)
+        params = []
+        for i in range(N):
+            row, off = [], 0
+            for shp in SHAPES:
+                n = int(np.prod(shp))
+                row.append(X[i, off:off + n].reshape(shp).copy())
+                off += n
+            params.append(row)
+        w = synth.cardinalities(seed, N)
+        sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)][: N - 2]  # zip() truncates to N-2 rows
+        outs = agg.aggregate_layers(params, w, sc, device=torch.device("cpu"))
+        q.put((rank, [o.tobytes() for o in outs], [o.shape for o in outs]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_aggregate_layers_slices_per_layer(world):
+    """Reference-shaped per-layer lists through the sharded path: each rank
+    copies only the layer pieces inside its bucket; zip() truncation keeps the
+    divisor over every weight (stall_aware_aggregation.py:52-60)."""
+    from oracle import fedavg_oracle as O
+    N, seed = 7, 31
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_layers_worker, args=(r, world, port, N, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, outs, shapes = q.get(timeout=120)
+        got[r] = (outs, shapes)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    P = sum(int(np.prod(s)) for s in SHAPES)
+    X = synth.clients_f32(seed, N, 0, P)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)][: N - 2]
+    exp = O.fedavg_stacked(X[: N - 2], w[: N - 2], sc, total=sum(w))
+    for r in range(world):
+        outs, shapes = got[r]
+        assert [tuple(s) for s in shapes] == SHAPES
+        flat = np.concatenate([np.frombuffer(b, dtype=np.float32) for b in outs])
+        assert np.array_equal(flat.view(np.uint32), exp.view(np.uint32)), r
+
+
+def test_aggregate_layers_rejects_other_dtypes():
+    from fedlesscan_amd.aggregator.exceptions import InvalidParameterShapeError
+    agg = ShardedAggregator(fold=_oracle_fold)
+    with pytest.raises(InvalidParameterShapeError):
+        agg.aggregate_layers([[np.zeros(4, np.float64)], [np.zeros(4, np.float64)]], [1, 2],
+                             device=torch.device("cpu"))
+    with pytest.raises(InvalidParameterShapeError):
+        agg.aggregate_layers([[np.zeros(4, np.float32)], [np.zeros(4, np.float32)]], [np.float64(1), 2],
+                             device=torch.device("cpu"))

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Pointer-list fold (fa_fedavg_f32_ptrs: N separately allocated client rows)
-against the stacked fold on the same values.
+against the stacked fold on the same values.  All times are GPU-event spans
+around the Python call, so they include its host work whenever the GPU waits
+for it: ptrs_ms = a fresh list of rows per call, rowset_ms = an engine.RowSet
+built once, views_ms = X[i] rows of one stacked tensor (equal-stride view).
 
     python tools/ptrs_bench.py [--clients N] [--params P]   (GPU box) -> one JSON line
 """
@@ -43,7 +46,13 @@ def timed(fn):
     return sorted(ts)[len(ts) // 2]
 
 
-t_rows = timed(lambda: engine.fold_rows(rows, w))
+t_rows = timed(lambda: engine.fold_rows(rows, w))  # a fresh list each call: validation + pointer table
+rs = engine.RowSet(rows)  # prepared once, as a caller that keeps its client tensors would
+t_rowset = timed(lambda: engine.fold_rows(rs, w))
+views = [X[i] for i in range(N)]  # rows of one stacked tensor: the equal-stride view path
+t_views = timed(lambda: engine.fold_rows(views, w))
+rs_views = engine.RowSet(views)
+t_views_rs = timed(lambda: engine.fold_rows(rs_views, w))
 # the kernel alone: pointer table and factors built once, as a caller that
 # keeps its client tensors would
 import numpy as np  # noqa: E402
@@ -54,9 +63,12 @@ div = float(np.float32(sum(w)))
 t_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), None,
                                                                div, out.data_ptr(), st), "ptrs"))
 t_stack = timed(lambda: engine.fold_stacked(X, w))
-same = torch.equal(engine.fold_rows(rows, w).view(torch.int32), engine.fold_stacked(X, w).view(torch.int32))
+ref = engine.fold_stacked(X, w).view(torch.int32)
+same = all(torch.equal(engine.fold_rows(r, w).view(torch.int32), ref) for r in (rows, rs, views, rs_views))
 gb = (N * P * 4 + P * 4) / 1e9
 print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_GBps": round(gb / t_rows * 1e3, 1),
+                  "rowset_ms": round(t_rowset, 4), "views_ms": round(t_views, 4),
+                  "views_rowset_ms": round(t_views_rs, 4),
                   "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
                   "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
                   "bit_identical": bool(same)}))
