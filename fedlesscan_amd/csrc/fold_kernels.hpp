@@ -60,6 +60,9 @@ int check_launch(const char* what) {
 constexpr int kBlock = 256;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// f32x4 in the global address space: loads through pointers read from memory
+// (row tables) are global_load, not flat_load
+typedef __attribute__((address_space(1))) const f32x4 gf32x4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const int64_t ldq = ldx >> 2;
     const int t = threadIdx.x;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
-    const float* const* xi = reinterpret_cast<const float* const*>(X);
+    const float* const* __restrict__ xi = reinterpret_cast<const float* const*>(X);
     auto row4 = [&](int64_t row) -> const f32x4* {  // quad 0 of a client row
         if constexpr (ROWS) return reinterpret_cast<const f32x4*>(xi[row]);
         else return X4 + row * ldq;
@@ -254,10 +257,34 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     // would serialise the chunk loads with the fold.  The last block and the
     // last partial chunk take the checked path, outside that loop.
     auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
+        if constexpr (ROWS) {
+            // One wave-instruction covers RPW = 64/TQ whole rows, so its row
+            // pointers are wave-uniform: scalar loads of RPW consecutive table
+            // entries, then each lane picks its row's (no per-lane table load
+            // in front of the data load).
+            constexpr int RPW = 64 / TQ;
+            static_assert(64 % TQ == 0 && NT % 64 == 0, "rows per wave-instruction");
+            const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+            const int lane = t & 63;
 #pragma unroll
-        for (int j = 0; j < LQ; ++j) {
-            const int e = t + j * NT;
-            g.v[j] = __builtin_nontemporal_load(row4(c * R + e / TQ) + q0 + e % TQ);
+            for (int j = 0; j < LQ; ++j) {
+                const int64_t r0 = c * R + (j * NT + w * 64) / TQ;  // wave-uniform
+                const float* p[RPW];
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) p[k] = xi[r0 + k];  // scalar loads
+                const float* rp = p[0];
+#pragma unroll
+                for (int k = 1; k < RPW; ++k) rp = (lane / TQ == k) ? p[k] : rp;
+                // a global (not flat) load: the table holds device pointers
+                const gf32x4* g4 = (const gf32x4*)rp;
+                g.v[j] = __builtin_nontemporal_load(g4 + q0 + lane % TQ);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < LQ; ++j) {
+                const int e = t + j * NT;
+                g.v[j] = __builtin_nontemporal_load(row4(c * R + e / TQ) + q0 + e % TQ);
+            }
         }
         if (t < R) {
             g.fv = a[c * R + t];
