@@ -256,29 +256,39 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     // makes the compiler wait for the load right after issuing it, which
     // would serialise the chunk loads with the fold.  The last block and the
     // last partial chunk take the checked path, outside that loop.
+    const bool interior = q0 + TQ <= nq;
+    const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
+    // ROWS: one wave-instruction covers RPW = 64/TQ whole rows, so its row
+    // pointers are wave-uniform: scalar loads of RPW consecutive table
+    // entries, then each lane picks its row's.  The pointers of the NEXT chunk
+    // are fetched while this chunk's data loads go out (the pipelined loop
+    // loads chunks in increasing order), so no table load sits in front of a
+    // data load.
+    constexpr int RPW = 64 / TQ;
+    static_assert(!ROWS || (64 % TQ == 0 && NT % 64 == 0), "rows per wave-instruction");
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const float* nxt[ROWS ? LQ * RPW : 1];
+    auto fetch_ptrs = [&](int64_t c) {  // chunk c < nfull
+        if constexpr (ROWS) {
+#pragma unroll
+            for (int j = 0; j < LQ; ++j)
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) nxt[j * RPW + k] = xi[c * R + (j * NT + wv * 64) / TQ + k];
+        }
+    };
+    if (ROWS && nfull > 0) fetch_ptrs(0);
     auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
         if constexpr (ROWS) {
-            // One wave-instruction covers RPW = 64/TQ whole rows, so its row
-            // pointers are wave-uniform: scalar loads of RPW consecutive table
-            // entries, then each lane picks its row's (no per-lane table load
-            // in front of the data load).
-            constexpr int RPW = 64 / TQ;
-            static_assert(64 % TQ == 0 && NT % 64 == 0, "rows per wave-instruction");
-            const int w = __builtin_amdgcn_readfirstlane(t >> 6);
             const int lane = t & 63;
 #pragma unroll
             for (int j = 0; j < LQ; ++j) {
-                const int64_t r0 = c * R + (j * NT + w * 64) / TQ;  // wave-uniform
-                const float* p[RPW];
+                const float* rp = nxt[j * RPW];
 #pragma unroll
-                for (int k = 0; k < RPW; ++k) p[k] = xi[r0 + k];  // scalar loads
-                const float* rp = p[0];
-#pragma unroll
-                for (int k = 1; k < RPW; ++k) rp = (lane / TQ == k) ? p[k] : rp;
+                for (int k = 1; k < RPW; ++k) rp = (lane / TQ == k) ? nxt[j * RPW + k] : rp;
                 // a global (not flat) load: the table holds device pointers
-                const gf32x4* g4 = (const gf32x4*)rp;
-                g.v[j] = __builtin_nontemporal_load(g4 + q0 + lane % TQ);
+                g.v[j] = __builtin_nontemporal_load((const gf32x4*)rp + q0 + lane % TQ);
             }
+            if (c + 1 < nfull) fetch_ptrs(c + 1);
         } else {
 #pragma unroll
             for (int j = 0; j < LQ; ++j) {
@@ -356,8 +366,6 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
             for (; r < rows; ++r) acc = add4(acc, term4<SCORED>(tile[r * TQ + t], fa[r], SCORED ? fs[r] : 1.0f));
         }
     };
-    const bool interior = q0 + TQ <= nq;
-    const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
     int64_t c = 0;  // next chunk to fold
     if (DEPTH == 2 && nfull >= 4) {
         // two chunks in flight: LDS holds chunk c, A = c+1 and B = c+2 are loading.

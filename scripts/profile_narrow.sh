@@ -7,10 +7,9 @@
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/narrow
-mkdir -p "$OUT"
-for s in ${*:-"1024:67267 256:67267 100:582026 10:582026 100:1000000"}; do mkdir -p "$OUT/n${s%%:*}_p${s##*:}"; done
-cd /tmp && export TMPDIR=/tmp
 SHAPES=${*:-"1024:67267 256:67267 100:582026 10:582026 100:1000000"}
+for s in $SHAPES; do mkdir -p "$OUT/n${s%%:*}_p${s##*:}"; done
+cd /tmp && export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD"
 for s in $SHAPES; do
     n=${s%%:*}; p=${s##*:}
