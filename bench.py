@@ -209,7 +209,10 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
                   f"of fed_avg_aggregator.py:24-42 (1 core, numpy ufuncs single-threaded), median of {len(t_np_all)} runs {t_np:.2f} s "
                   f"(total {sum(t_np_all):.1f} s)",
         "omp": {"value": round(sample_bytes / min(t_omp) / 1e9, 3), "unit": "GB/s", "cores": threads,
-                "kind": "port", "impl": "oracle/fedavg_ref.c (bit-identical, OpenMP)"},
+                "kind": "port", "impl": "oracle/fedavg_ref.c (bit-identical, OpenMP)",
+                "cores_note": f"OpenMP threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS', 'unset')}), "
+                              "the host CPU share of one GPU on the GPU box; the other visible CPUs "
+                              "belong to the node's other GPUs"},
         "host_cpus_visible": len(os.sched_getaffinity(0)),
         "sample_bit_exact_vs_gpu": exact,
         "gen_s": round(gen_s, 2),
@@ -300,9 +303,16 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # One GPU: the folds run back to back and two events bracket the whole timed
+    # region (per-launch events would add their own few-microsecond gaps to
+    # every launch, which distorts the small models).  Several GPUs: events
+    # around every round's fold split a step into fold time and exposed gather.
+    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    region[0].record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step(evs[k] if world > 1 else None)
+    region[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -321,11 +331,15 @@ def main():
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
-    kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in folds) for folds, _ in evs]
-    # the exchange left exposed: from the last fold's end to the end of the step
-    exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
-    kern_avg = float(np.mean(kern_ms))
-    exposed_avg = float(np.mean(exposed_ms))
+    if world > 1:
+        kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in folds) for folds, _ in evs]
+        # the exchange left exposed: from the last fold's end to the end of the step
+        exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
+        kern_avg = float(np.mean(kern_ms))
+        exposed_avg = float(np.mean(exposed_ms))
+    else:
+        kern_avg = region[0].elapsed_time(region[1]) / args.steps  # per fold call, launch gaps included
+        exposed_avg = 0.0
     if world > 1:
         t = torch.tensor([kern_avg, exposed_avg], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Host-side cost of one engine.fold_stacked call, piece by piece (GPU box).
+
+    python tools/host_overhead.py [--clients N] [--params P]  -> one JSON line
+
+Host microseconds per call (perf_counter, no device synchronisation inside the
+measured loop, a sync every 50 calls so the queue stays short), for the whole
+call and for its parts: factor rounding, factor staging (pinned ring + async
+H2D), the output allocation, the stream query and the ctypes launch.  For a
+small model the GPU waits for this work between back-to-back calls.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedlesscan_amd import _lib, engine, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--clients", type=int, default=1024)
+ap.add_argument("--params", type=int, default=67267)
+ap.add_argument("--reps", type=int, default=500)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+N, P = args.clients, args.params
+X = torch.empty((N, P), dtype=torch.float32, device=dev)
+_lib.check(_lib.load_bench().fa_synth_f32(X.data_ptr(), N, P, P, 9, 0, 0, engine.stream_ptr(dev)), "synth",
+           bench=True)
+w = synth.cardinalities(9, N)
+sc = [(r + 1) / 11 for r in synth.round_ids(9, N, 10, 2)]
+torch.cuda.synchronize()
+
+
+def us(fn):
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    tot = 0.0
+    for k in range(args.reps):
+        t0 = time.perf_counter()
+        fn()
+        tot += time.perf_counter() - t0
+        if k % 50 == 49:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return round(tot / args.reps * 1e6, 2)
+
+
+f = engine.Factors(w, None, np.dtype(np.float32))
+res = {
+    "clients": N, "params": P,
+    "fold_stacked_us": us(lambda: engine.fold_stacked(X, w)),
+    "fold_stacked_scored_us": us(lambda: engine.fold_stacked(X, w, sc)),
+    "result_dtype_us": us(lambda: engine.result_dtype(np.dtype(np.float32), w, None)),
+    "factors_us": us(lambda: engine.Factors(w, None, np.dtype(np.float32))),
+    "factors_scored_us": us(lambda: engine.Factors(w, sc, np.dtype(np.float32))),
+    "stage_us": us(lambda: f.to(dev)),
+    "empty_out_us": us(lambda: torch.empty(P, dtype=torch.float32, device=dev)),
+    "stream_ptr_us": us(lambda: engine.stream_ptr(dev)),
+}
+a, _ = f.to(dev)
+out = torch.empty(P, dtype=torch.float32, device=dev)
+st = engine.stream_ptr(dev)
+L = _lib.load()
+res["ctypes_launch_us"] = us(lambda: L.fa_fedavg_f32(X.data_ptr(), N, P, P, a.data_ptr(), None, float(f.div),
+                                                     out.data_ptr(), st))
+print(json.dumps(res))

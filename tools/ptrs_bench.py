@@ -12,6 +12,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -55,7 +56,6 @@ rs_views = engine.RowSet(views)
 t_views_rs = timed(lambda: engine.fold_rows(rs_views, w))
 # the kernel alone: pointer table and factors built once, as a caller that
 # keeps its client tensors would
-import numpy as np  # noqa: E402
 ptr_tab = torch.from_numpy(np.array([r.data_ptr() for r in rows], dtype=np.int64)).to(dev)
 a_dev = torch.tensor([float(np.float32(x)) for x in w], dtype=torch.float32, device=dev)
 out = torch.empty(P, dtype=torch.float32, device=dev)
@@ -63,12 +63,27 @@ div = float(np.float32(sum(w)))
 t_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), None,
                                                                div, out.data_ptr(), st), "ptrs"))
 t_stack = timed(lambda: engine.fold_stacked(X, w))
+# rows of ONE allocation in a shuffled order: the pointer-table kernel over the
+# same memory as the stacked fold (tells the kernel apart from the placement
+# of separately allocated rows)
+perm = np.random.default_rng(5).permutation(N)
+rs_shuf = engine.RowSet([X[int(i)] for i in perm])
+w_shuf = [w[int(i)] for i in perm]
+assert rs_shuf.view is None
+t_shuf = timed(lambda: engine.fold_rows(rs_shuf, w_shuf))
+shuf_tab = rs_shuf.ptrs
+a_shuf = torch.tensor([float(np.float32(x)) for x in w_shuf], dtype=torch.float32, device=dev)
+t_shuf_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(shuf_tab.data_ptr(), N, P, a_shuf.data_ptr(),
+                                                                    None, div, out.data_ptr(), st), "ptrs"))
+same_shuf = torch.equal(engine.fold_rows(rs_shuf, w_shuf).view(torch.int32),
+                        engine.fold_stacked(X[torch.from_numpy(perm).to(dev)], w_shuf).view(torch.int32))
 ref = engine.fold_stacked(X, w).view(torch.int32)
 same = all(torch.equal(engine.fold_rows(r, w).view(torch.int32), ref) for r in (rows, rs, views, rs_views))
 gb = (N * P * 4 + P * 4) / 1e9
 print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_GBps": round(gb / t_rows * 1e3, 1),
                   "rowset_ms": round(t_rowset, 4), "views_ms": round(t_views, 4),
-                  "views_rowset_ms": round(t_views_rs, 4),
+                  "views_rowset_ms": round(t_views_rs, 4), "shuffled_rowset_ms": round(t_shuf, 4),
+                  "shuffled_kernel_ms": round(t_shuf_kern, 4),
                   "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
                   "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
-                  "bit_identical": bool(same)}))
+                  "bit_identical": bool(same and same_shuf)}))
