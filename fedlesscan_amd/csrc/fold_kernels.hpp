@@ -258,36 +258,26 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     // last partial chunk take the checked path, outside that loop.
     const bool interior = q0 + TQ <= nq;
     const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
-    // ROWS: one wave-instruction covers RPW = 64/TQ whole rows, so its row
-    // pointers are wave-uniform: scalar loads of RPW consecutive table
-    // entries, then each lane picks its row's.  The pointers of the NEXT chunk
-    // are fetched while this chunk's data loads go out (the pipelined loop
-    // loads chunks in increasing order), so no table load sits in front of a
-    // data load.
-    constexpr int RPW = 64 / TQ;
-    static_assert(!ROWS || (64 % TQ == 0 && NT % 64 == 0), "rows per wave-instruction");
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const float* nxt[ROWS ? LQ * RPW : 1];
+    // ROWS: each lane reads its own row's pointer from the table (8 B, a
+    // cache-resident line shared by the lanes of a row).  The pointers of the
+    // NEXT chunk are fetched while this chunk's data loads go out (the
+    // pipelined loop loads chunks in increasing order), so no table load sits
+    // right in front of a data load.  Vector loads on purpose: a scalar load
+    // would share lgkmcnt with the fold's LDS reads and, returning out of
+    // order, force the fold to wait for it.
+    const float* nxt[ROWS ? LQ : 1];
     auto fetch_ptrs = [&](int64_t c) {  // chunk c < nfull
         if constexpr (ROWS) {
 #pragma unroll
-            for (int j = 0; j < LQ; ++j)
-#pragma unroll
-                for (int k = 0; k < RPW; ++k) nxt[j * RPW + k] = xi[c * R + (j * NT + wv * 64) / TQ + k];
+            for (int j = 0; j < LQ; ++j) nxt[j] = xi[c * R + (t + j * NT) / TQ];
         }
     };
     if (ROWS && nfull > 0) fetch_ptrs(0);
     auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
         if constexpr (ROWS) {
-            const int lane = t & 63;
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) {
-                const float* rp = nxt[j * RPW];
-#pragma unroll
-                for (int k = 1; k < RPW; ++k) rp = (lane / TQ == k) ? nxt[j * RPW + k] : rp;
-                // a global (not flat) load: the table holds device pointers
-                g.v[j] = __builtin_nontemporal_load((const gf32x4*)rp + q0 + lane % TQ);
-            }
+            for (int j = 0; j < LQ; ++j)  // a global (not flat) load: the table holds device pointers
+                g.v[j] = __builtin_nontemporal_load((const gf32x4*)nxt[j] + q0 + (t + j * NT) % TQ);
             if (c + 1 < nfull) fetch_ptrs(c + 1);
         } else {
 #pragma unroll
