@@ -75,6 +75,10 @@ shuf_tab = rs_shuf.ptrs
 a_shuf = torch.tensor([float(np.float32(x)) for x in w_shuf], dtype=torch.float32, device=dev)
 t_shuf_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(shuf_tab.data_ptr(), N, P, a_shuf.data_ptr(),
                                                                     None, div, out.data_ptr(), st), "ptrs"))
+# the same kernel over rows of one allocation in their natural order (a table of X[i])
+ord_tab = torch.from_numpy(np.array([X[i].data_ptr() for i in range(N)], dtype=np.int64)).to(dev)
+t_ord_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ord_tab.data_ptr(), N, P, a_dev.data_ptr(),
+                                                                  None, div, out.data_ptr(), st), "ptrs"))
 same_shuf = torch.equal(engine.fold_rows(rs_shuf, w_shuf).view(torch.int32),
                         engine.fold_stacked(X[torch.from_numpy(perm).to(dev)], w_shuf).view(torch.int32))
 ref = engine.fold_stacked(X, w).view(torch.int32)
@@ -83,7 +87,7 @@ gb = (N * P * 4 + P * 4) / 1e9
 print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_GBps": round(gb / t_rows * 1e3, 1),
                   "rowset_ms": round(t_rowset, 4), "views_ms": round(t_views, 4),
                   "views_rowset_ms": round(t_views_rs, 4), "shuffled_rowset_ms": round(t_shuf, 4),
-                  "shuffled_kernel_ms": round(t_shuf_kern, 4),
+                  "shuffled_kernel_ms": round(t_shuf_kern, 4), "inorder_table_kernel_ms": round(t_ord_kern, 4),
                   "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
                   "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
                   "bit_identical": bool(same and same_shuf)}))
