@@ -211,13 +211,20 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
 //   and parked in LDS; wave 0 then folds the chunk from LDS in client order
 //   (lane = one quad) while the next chunk's loads are already in flight.  The
 //   adds stay one lane per column, strictly in row order: bit-identical to
-//   every other fold.  The partial quad of the P%4 tail columns is staged
-//   like a full one (element loads, zero-filled) and only its real columns
-//   are stored.  Per-chunk factors a[], s[] are staged in LDS too.
+//   every other fold.  Per-chunk factors a[], s[] are staged in LDS too.
+//
+//   Every block that owns full quads runs the pipelined loop, the last one
+//   too: its quad indices past the end are clamped to the last full quad (a
+//   valid address; the value is never stored), so no load carries a branch.
+//   (A checked, unpipelined last block used to be the straggler of the whole
+//   launch: one dependent HBM round trip per chunk, 64 of them at N = 1024.)
+//   The P%4 tail columns get one extra block of their own: every thread
+//   loads one row's tail elements and forms its term (elementwise, as in the
+//   fold), NT rows in flight per pass, and thread 0 adds the pass in row order.
+//
 //   ROWS: X is really `const float* const* xi`, a device table of N row
 //   pointers (separately allocated client rows, every row 16-B aligned;
-//   fa_fedavg_f32_ptrs_aligned); ldx is unused.  The table is read per lane
-//   (8 B, cache-resident: every block reads the same N entries).
+//   fa_fedavg_f32_ptrs_aligned); ldx is unused.
 template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1, bool ROWS = false>
 __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
@@ -228,21 +235,65 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     static_assert(TQ <= 64 && (R * TQ) % NT == 0 && R <= NT, "tile shape");
     __shared__ f32x4 tile[R * TQ];
     __shared__ float fa[R], fs[SCORED ? R : 1];
-    const int64_t nq = P >> 2;
-    const int64_t nqa = (P + 3) >> 2;  // quads incl. the partial tail quad
-    const int64_t q0 = (int64_t)blockIdx.x * TQ;
-    const int tq = (int)((nqa - q0) < TQ ? (nqa - q0) : TQ);
-    const int64_t ldq = ldx >> 2;
+    const int64_t nq = P >> 2;                     // full quads
+    const int64_t nbq = (nq + TQ - 1) / TQ;        // blocks over the full quads
     const int t = threadIdx.x;
-    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const int64_t ldq = ldx >> 2;
     const float* const* __restrict__ xi = reinterpret_cast<const float* const*>(X);
-    auto row4 = [&](int64_t row) -> const f32x4* {  // quad 0 of a client row
-        if constexpr (ROWS) return reinterpret_cast<const f32x4*>(xi[row]);
-        else return X4 + row * ldq;
-    };
     auto rowf = [&](int64_t row) -> const float* {
         if constexpr (ROWS) return xi[row];
         else return X + row * ldx;
+    };
+
+    if ((int64_t)blockIdx.x >= nbq) {
+        // ---- the P%4 tail columns (block-uniform branch: this block only) ----
+        const int w4 = (int)(P & 3);
+        const int64_t col0 = nq * 4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (ACC && t == 0)
+            for (int k = 0; k < w4; ++k) acc[k] = acc_in[col0 + k];
+        for (int64_t r0 = 0; r0 < N; r0 += NT) {
+            const int64_t row = r0 + t;
+            if (row < N) {
+                const float* rp = rowf(row);
+                f32x4 x = {0.f, 0.f, 0.f, 0.f};
+                for (int k = 0; k < w4; ++k) x[k] = rp[col0 + k];
+                tile[t] = term4<SCORED>(x, a[row], SCORED ? s[row] : 1.0f);
+            }
+            __syncthreads();
+            if (t == 0) {
+                const int rows = (N - r0) < NT ? (int)(N - r0) : NT;
+                int i = 0;
+                if (!ACC && r0 == 0) {
+                    acc = tile[0];
+                    i = 1;
+                }
+                for (; i + 8 <= rows; i += 8) {
+                    f32x4 v[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = tile[i + k];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc = add4(acc, v[k]);
+                }
+                for (; i < rows; ++i) acc = add4(acc, tile[i]);
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            const f32x4 res = FIN ? div4(acc, divisor) : acc;
+            for (int k = 0; k < w4; ++k) out[col0 + k] = res[k];
+        }
+        return;
+    }
+
+    // ---- full quads [q0, q0 + tq) ----
+    const int64_t q0 = (int64_t)blockIdx.x * TQ;
+    const int tq = (int)((nq - q0) < TQ ? (nq - q0) : TQ);
+    // this lane's quad within the tile for its j-th load, clamped to the last
+    // full quad (the last block's lanes past the end re-read a valid quad)
+    auto qof = [&](int j) -> int64_t {
+        const int64_t q = q0 + (t + j * NT) % TQ;
+        return q < nq ? q : nq - 1;
     };
     // one chunk in registers: its LQ quads per lane and (lanes < R) its factors
     struct Stage {
@@ -250,14 +301,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         float fv, sv;
     };
     Stage A, B;
-    // Interior blocks (TQ full quads) stream their full chunks through a loop
-    // whose loads carry no checks and no control flow: a branch between a
-    // load and its use (the tail-quad loop, or a join with a checked path)
-    // makes the compiler wait for the load right after issuing it, which
-    // would serialise the chunk loads with the fold.  The last block and the
-    // last partial chunk take the checked path, outside that loop.
-    const bool interior = q0 + TQ <= nq;
-    const int64_t nfull = interior ? N / R : 0;  // chunks taken by the pipelined loop
+    const int64_t nfull = N / R;  // chunks taken by the pipelined loop
     // ROWS: each lane reads its own row's pointer from the table (8 B, a
     // cache-resident line shared by the lanes of a row).  The pointers of the
     // NEXT chunk are fetched while this chunk's data loads go out (the
@@ -273,39 +317,32 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         }
     };
     if (ROWS && nfull > 0) fetch_ptrs(0);
-    auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R), every quad in range
+    // Full chunks stream through loops whose loads carry no checks and no
+    // control flow: a branch between a load and its use makes the compiler
+    // wait for the load right after issuing it, which would serialise the
+    // chunk loads with the fold.
+    auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R)
         if constexpr (ROWS) {
 #pragma unroll
             for (int j = 0; j < LQ; ++j)  // a global (not flat) load: the table holds device pointers
-                g.v[j] = __builtin_nontemporal_load((const gf32x4*)nxt[j] + q0 + (t + j * NT) % TQ);
+                g.v[j] = __builtin_nontemporal_load((const gf32x4*)nxt[j] + qof(j));
             if (c + 1 < nfull) fetch_ptrs(c + 1);
         } else {
+            const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) {
-                const int e = t + j * NT;
-                g.v[j] = __builtin_nontemporal_load(row4(c * R + e / TQ) + q0 + e % TQ);
-            }
+            for (int j = 0; j < LQ; ++j)
+                g.v[j] = __builtin_nontemporal_load(X4 + (c * R + (t + j * NT) / TQ) * ldq + qof(j));
         }
         if (t < R) {
             g.fv = a[c * R + t];
             if constexpr (SCORED) g.sv = s[c * R + t];
         }
     };
-    auto load_checked = [&](int64_t c, Stage& g) {
+    auto load_rows_checked = [&](int64_t c, Stage& g) {  // the last, partial chunk: rows < N only
 #pragma unroll
         for (int j = 0; j < LQ; ++j) {
-            const int e = t + j * NT, r = e / TQ, qq = e % TQ;
-            const int64_t row = c * R + r, q = q0 + qq;
-            if (row < N && qq < tq) {
-                if (q < nq) {
-                    g.v[j] = __builtin_nontemporal_load(row4(row) + q);
-                } else {  // partial tail quad: P%4 real columns
-                    f32x4 x = {0.f, 0.f, 0.f, 0.f};
-                    const float* rp = rowf(row);
-                    for (int k = 0; k < (int)(P & 3); ++k) x[k] = rp[q * 4 + k];
-                    g.v[j] = x;
-                }
-            }
+            const int64_t row = c * R + (t + j * NT) / TQ;
+            if (row < N) g.v[j] = __builtin_nontemporal_load((const gf32x4*)rowf(row) + qof(j));
         }
         if (t < R && c * R + t < N) {
             g.fv = a[c * R + t];
@@ -322,14 +359,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     };
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if constexpr (ACC) {
-        if (t < tq) {
-            const int64_t q = q0 + t;
-            if (q < nq) {
-                acc = reinterpret_cast<const f32x4*>(acc_in)[q];
-            } else {
-                for (int k = 0; k < (int)(P & 3); ++k) acc[k] = acc_in[q * 4 + k];
-            }
-        }
+        if (t < tq) acc = reinterpret_cast<const f32x4*>(acc_in)[q0 + t];
     }
     // fold the staged chunk c (rows valid rows) in client order, lane = quad
     auto fold = [&](int64_t c, int rows) {
@@ -404,22 +434,23 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         __syncthreads();
         ++c;
     }
-    for (; c * R < N; ++c) {  // the rest, checked (no overlap)
-        if (c < nfull) load_full(c, A);
-        else load_checked(c, A);
+    for (; c < nfull; ++c) {  // full chunks the pipeline left (DEPTH 2 with nfull in 4 + 2k+1 ...)
+        load_full(c, A);
         stash(A);
         __syncthreads();
-        fold(c, (N - c * R) < R ? (int)(N - c * R) : R);
+        fold(c, R);
+        __syncthreads();
+    }
+    if (c * R < N) {  // the last, partial chunk
+        load_rows_checked(c, A);
+        stash(A);
+        __syncthreads();
+        fold(c, (int)(N - c * R));
         __syncthreads();
     }
     if (t < tq) {
         const f32x4 res = FIN ? div4(acc, divisor) : acc;
-        const int64_t q = q0 + t;
-        if (q < nq) {
-            __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q);
-        } else {
-            for (int k = 0; k < (int)(P & 3); ++k) out[q * 4 + k] = res[k];
-        }
+        __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q0 + t);
     }
 }
 
@@ -994,7 +1025,8 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false, bool ROWS = false>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
-    const int64_t blocks = (((P + 3) >> 2) + TQ - 1) / TQ;
+    // blocks over the full quads, plus one for the P%4 tail columns
+    const int64_t blocks = ((P >> 2) + TQ - 1) / TQ + ((P & 3) ? 1 : 0);
     if (blocks * NW * 64 > (int64_t)0xFFFFFFFF)  // work-items per launch dimension
         return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
     const dim3 grid((unsigned)blocks), block(NW * 64);
