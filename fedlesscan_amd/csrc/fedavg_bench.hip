@@ -139,6 +139,9 @@ constexpr const char* kVariants[] = {
     // LDS-staged narrow folds
     "lds_w8r64t32", "lds_w4r64t64", "lds_w16r128t64",
     "lds2_w4r32t16", "lds2_w4r16t32", "lds2_w4r64t32", "lds2_w8r32t32", "lds2_w4r32t8", "lds2_w2r32t16",
+    // LDS-DMA ring: ring_w<waves>r<rows per chunk>t<quads per block>s<slots>
+    "ring_w4r32t16s4", "ring_w4r32t16s6", "ring_w4r32t16s8", "ring_w4r32t32s4", "ring_w4r32t32s6",
+    "ring_w4r64t16s4", "ring_w4r16t32s8", "ring_w8r64t32s3", "ring_w4r32t8s8", "ring_w2r32t16s8",
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -276,6 +279,18 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 23: rc = FA_VL(8, 32, 32, 2); break;
         case 24: rc = FA_VL(4, 32, 8, 2); break;
         case 25: rc = FA_VL(2, 32, 16, 2); break;
+#define FA_VR(NW, R, TQ, S) launch_ring_flags<NW, R, TQ, S>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 26: rc = FA_VR(4, 32, 16, 4); break;
+        case 27: rc = FA_VR(4, 32, 16, 6); break;
+        case 28: rc = FA_VR(4, 32, 16, 8); break;
+        case 29: rc = FA_VR(4, 32, 32, 4); break;
+        case 30: rc = FA_VR(4, 32, 32, 6); break;
+        case 31: rc = FA_VR(4, 64, 16, 4); break;
+        case 32: rc = FA_VR(4, 16, 32, 8); break;
+        case 33: rc = FA_VR(8, 64, 32, 3); break;
+        case 34: rc = FA_VR(4, 32, 8, 8); break;
+        case 35: rc = FA_VR(2, 32, 16, 8); break;
+#undef FA_VR
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF

@@ -454,6 +454,205 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Narrow models, deep ring: LDS-DMA (global_load_lds) into an S-slot ring.
+//   Same tile and fold as k_fold_f32_lds (a block owns TQ quads of every row;
+//   wave 0 folds each R-row chunk from LDS in client order, one lane per quad),
+//   but the chunks are copied HBM -> LDS by global_load_lds_dwordx4, which
+//   needs no VGPRs: S - 1 chunks stay in flight per block (the register-staged
+//   fold holds two), which is what a narrow model is short of.  Counters on
+//   1024 x 16K / 67K (profiles/r02_narrow/SUMMARY.md): SQ_WAIT_ANY = 72-80 %
+//   of the wave cycles with at most two chunks in flight, i.e. latency-bound.
+//   Synchronisation per chunk: each wave's counted `s_waitcnt vmcnt` retires
+//   its own copies of chunk c (later chunks stay in flight), then a raw
+//   s_barrier makes everyone's copies visible and tells the loaders that wave
+//   0 has finished the chunk before (whose slot the next copy reuses).  No
+//   ordinary global load sits inside the ring (hipcc would drain the ring at
+//   its first use), and all LDS is one __shared__ array.
+//   The factors of a chunk travel the same way (4-byte copies, lanes < R).
+//   The last partial chunk (N % R rows) and the P%4 tail columns take the
+//   register paths of k_fold_f32_lds after the ring has drained.
+// ---------------------------------------------------------------------------
+template <int N_>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N_ & 0xF) | ((N_ >> 4) << 14) | 0x70 | 0xF00);  // vmcnt(N_) only
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+template <int NW, int R, int TQ, int S, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(NW * 64) void k_fold_f32_ring(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    constexpr int NT = NW * 64;
+    constexpr int LQ = R * TQ / NT;                 // 16-B copies per thread per chunk
+    constexpr int F = SCORED ? 2 : 1;               // factor copies per chunk (wave 0)
+    constexpr int TILE_B = R * TQ * 16;
+    constexpr int SLOT_B = TILE_B + ((F * R * 4 + 15) / 16) * 16;
+    static_assert(TQ <= 64 && 64 % TQ == 0 && (R * TQ) % NT == 0 && R <= 64 && S >= 3, "ring shape");
+    static_assert((S - 2) * (LQ + F) < 64, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) char smem[S * SLOT_B];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t nq = P >> 2;
+    const int64_t nbq = (nq + TQ - 1) / TQ;
+    const int64_t ldq = ldx >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    f32x4* tile0 = reinterpret_cast<f32x4*>(smem);
+
+    if ((int64_t)blockIdx.x >= nbq) {
+        // ---- the P%4 tail columns: row-parallel terms, thread 0 adds in order ----
+        const int w4 = (int)(P & 3);
+        const int64_t col0 = nq * 4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (ACC && t == 0)
+            for (int k = 0; k < w4; ++k) acc[k] = acc_in[col0 + k];
+        for (int64_t r0 = 0; r0 < N; r0 += NT) {
+            const int64_t row = r0 + t;
+            if (row < N) {
+                f32x4 x = {0.f, 0.f, 0.f, 0.f};
+                for (int k = 0; k < w4; ++k) x[k] = X[row * ldx + col0 + k];
+                tile0[t] = term4<SCORED>(x, a[row], SCORED ? s[row] : 1.0f);
+            }
+            __syncthreads();
+            if (t == 0) {
+                const int rows = (N - r0) < NT ? (int)(N - r0) : NT;
+                int i = 0;
+                if (!ACC && r0 == 0) {
+                    acc = tile0[0];
+                    i = 1;
+                }
+                for (; i < rows; ++i) acc = add4(acc, tile0[i]);
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            const f32x4 res = FIN ? div4(acc, divisor) : acc;
+            for (int k = 0; k < w4; ++k) out[col0 + k] = res[k];
+        }
+        return;
+    }
+
+    const int64_t q0 = (int64_t)blockIdx.x * TQ;
+    const int tq = (int)((nq - q0) < TQ ? (nq - q0) : TQ);
+    auto qof = [&](int j) -> int64_t {  // clamped: the last block's lanes past the end re-read a valid quad
+        const int64_t q = q0 + (t + j * NT) % TQ;
+        return q < nq ? q : nq - 1;
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (ACC) {
+        if (t < tq) acc = reinterpret_cast<const f32x4*>(acc_in)[q0 + t];
+        wait_vmcnt<0>();  // before the ring: no ordinary load may be pending inside it
+    }
+    const int64_t nfull = N / R;
+    auto issue = [&](int64_t c) {  // copy chunk c into slot c % S (every wave its share)
+        char* slot = smem + (int)(c % S) * SLOT_B;
+#pragma unroll
+        for (int j = 0; j < LQ; ++j)
+            glds16(X4 + (c * R + (t + j * NT) / TQ) * ldq + qof(j), slot + (j * NT + w * 64) * 16);
+        if (w == 0 && lane < R) {
+            glds4(a + c * R + lane, slot + TILE_B);
+            if constexpr (SCORED) glds4(s + c * R + lane, slot + TILE_B + R * 4);
+        }
+    };
+    auto fold = [&](const char* slot, int rows, bool first) {
+        const f32x4* tile = reinterpret_cast<const f32x4*>(slot);
+        const float* fa = reinterpret_cast<const float*>(slot + TILE_B);
+        const float* fs = fa + R;
+        if (t < tq) {
+            int r = 0;
+            if (first) {
+                acc = term4<SCORED>(tile[t], fa[0], SCORED ? fs[0] : 1.0f);
+                r = 1;
+            }
+            for (; r + 8 <= rows; r += 8) {
+                f32x4 x[8];
+                float f[8], g[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    x[k] = tile[(r + k) * TQ + t];
+                    f[k] = fa[r + k];
+                    g[k] = SCORED ? fs[r + k] : 1.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc = add4(acc, term4<SCORED>(x[k], f[k], g[k]));
+            }
+            for (; r < rows; ++r) acc = add4(acc, term4<SCORED>(tile[r * TQ + t], fa[r], SCORED ? fs[r] : 1.0f));
+        }
+    };
+    const int64_t pre = nfull < S - 1 ? nfull : S - 1;
+    for (int64_t c = 0; c < pre; ++c) issue(c);
+    for (int64_t c = 0; c < nfull; ++c) {
+        // retire this wave's copies of chunk c; chunks c+1 .. c+S-2 stay in flight
+        if (c + S - 2 < nfull) {
+            if (w == 0) wait_vmcnt<(S - 2) * (LQ + F)>();
+            else wait_vmcnt<(S - 2) * LQ>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // everyone's copies of c landed; wave 0 is done with c-1
+        if (c + S - 1 < nfull) issue(c + S - 1);
+        if (w == 0) fold(smem + (int)(c % S) * SLOT_B, R, !ACC && c == 0);
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (nfull * R < N) {  // the last, partial chunk: register path through slot 0
+        const int64_t c = nfull;
+        f32x4* tile = tile0;
+        float* fa = reinterpret_cast<float*>(smem + TILE_B);
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int64_t row = c * R + (t + j * NT) / TQ;
+            if (row < N) tile[t + j * NT] = __builtin_nontemporal_load(X4 + row * ldq + qof(j));
+        }
+        if (t < R && c * R + t < N) {
+            fa[t] = a[c * R + t];
+            if constexpr (SCORED) fa[R + t] = s[c * R + t];
+        }
+        __syncthreads();
+        if (w == 0) fold(smem, (int)(N - c * R), !ACC && c == 0);
+        __syncthreads();
+    }
+    if (t < tq) {
+        const f32x4 res = FIN ? div4(acc, divisor) : acc;
+        __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q0 + t);
+    }
+}
+
+template <int NW, int R, int TQ, int S, bool ALLF = false>
+int launch_ring_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t blocks = ((P >> 2) + TQ - 1) / TQ + ((P & 3) ? 1 : 0);
+    if (blocks * NW * 64 > (int64_t)0xFFFFFFFF)
+        return fail(FA_ERR_ARG, "P=%lld too large for a ring launch", (long long)P);
+    const dim3 grid((unsigned)blocks), block(NW * 64);
+#define FA_RG(SC, ACC, FIN) \
+    hipLaunchKernelGGL((k_fold_f32_ring<NW, R, TQ, S, SC, ACC, FIN>), grid, block, 0, st, X, N, P, ldx, a, s, \
+                       acc_in, d, out)
+    if constexpr (!ALLF) {
+        if (sc) FA_RG(true, false, true); else FA_RG(false, false, true);
+    } else if (sc) {
+        if (acc) { if (fin) FA_RG(true, true, true); else FA_RG(true, true, false); }
+        else     { if (fin) FA_RG(true, false, true); else FA_RG(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_RG(false, true, true); else FA_RG(false, true, false); }
+        else     { if (fin) FA_RG(false, false, true); else FA_RG(false, false, false); }
+    }
+#undef FA_RG
+    return FA_OK;
+}
+
 // Split-client fold (opt-in, NOT bit-exact; fa_fedavg_f32_splitn).
 //   For models too narrow to fill the chip even with LDS staging, the
 //   clients of every column are cut into S = 4*NW contiguous slices.  A block

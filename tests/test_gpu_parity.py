@@ -570,7 +570,7 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
 
 
 def _lds_variants(B):
-    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith(b"lds")]
+    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"lds", b"ring"))]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
