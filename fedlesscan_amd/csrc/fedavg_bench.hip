@@ -142,6 +142,9 @@ constexpr const char* kVariants[] = {
     // LDS-DMA ring: ring_w<waves>r<rows per chunk>t<quads per block>s<slots>
     "ring_w4r32t16s4", "ring_w4r32t16s6", "ring_w4r32t16s8", "ring_w4r32t32s4", "ring_w4r32t32s6",
     "ring_w4r64t16s4", "ring_w4r16t32s8", "ring_w8r64t32s3", "ring_w4r32t8s8", "ring_w2r32t16s8",
+    // register-staged LDS fold with <d> chunks in flight: lds<d>_w..r..t..
+    "lds3_w4r32t16", "lds4_w4r32t16", "lds6_w4r32t16", "lds4_w4r16t32", "lds3_w4r16t32", "lds4_w2r32t16",
+    "lds4_w4r32t8", "lds3_w8r32t32", "lds4_w4r64t32",
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -291,6 +294,15 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 34: rc = FA_VR(4, 32, 8, 8); break;
         case 35: rc = FA_VR(2, 32, 16, 8); break;
 #undef FA_VR
+        case 36: rc = FA_VL(4, 32, 16, 3); break;
+        case 37: rc = FA_VL(4, 32, 16, 4); break;
+        case 38: rc = FA_VL(4, 32, 16, 6); break;
+        case 39: rc = FA_VL(4, 16, 32, 4); break;
+        case 40: rc = FA_VL(4, 16, 32, 3); break;
+        case 41: rc = FA_VL(2, 32, 16, 4); break;
+        case 42: rc = FA_VL(4, 32, 8, 4); break;
+        case 43: rc = FA_VL(8, 32, 32, 3); break;
+        case 44: rc = FA_VL(4, 64, 32, 4); break;
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF

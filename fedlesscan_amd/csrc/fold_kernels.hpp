@@ -300,7 +300,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         f32x4 v[LQ];
         float fv, sv;
     };
-    Stage A, B;
+    Stage st[DEPTH > 1 ? DEPTH : 1];
     const int64_t nfull = N / R;  // chunks taken by the pipelined loop
     // ROWS: each lane reads its own row's pointer from the table (8 B, a
     // cache-resident line shared by the lanes of a row).  The pointers of the
@@ -387,63 +387,59 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         }
     };
     int64_t c = 0;  // next chunk to fold
-    if (DEPTH == 2 && nfull >= 4) {
-        // two chunks in flight: LDS holds chunk c, A = c+1 and B = c+2 are loading.
-        // The loop is peeled so that no load in it is conditional.
-        load_full(0, A);
-        stash(A);
+    if (DEPTH >= 2 && nfull > DEPTH) {
+        // DEPTH chunks in flight: LDS holds chunk c, stage st[(c+i) % DEPTH]
+        // holds chunk c+i (i = 1..DEPTH), loading.  Stage indices are static
+        // after unrolling (c stays a multiple of DEPTH at the loop head), so the
+        // stages live in registers; the steady-state loop has no conditional load.
+        load_full(0, st[0]);
+        stash(st[0]);
         __syncthreads();
-        load_full(1, A);
-        load_full(2, B);
-        for (; c + 4 < nfull; c += 2) {
-            fold(c, R);
-            __syncthreads();  // chunk c consumed
-            stash(A);         // waits for A only; B stays in flight
-            __syncthreads();  // chunk c+1 staged
-            load_full(c + 3, A);
-            fold(c + 1, R);
-            __syncthreads();
-            stash(B);
-            __syncthreads();  // chunk c+2 staged
-            load_full(c + 4, B);
+#pragma unroll
+        for (int k = 1; k <= DEPTH; ++k) load_full(k, st[k % DEPTH]);
+        for (; c + 2 * DEPTH < nfull; c += DEPTH) {
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) {
+                fold(c + k, R);
+                __syncthreads();                    // chunk c+k consumed
+                stash(st[(k + 1) % DEPTH]);         // waits for that stage only
+                __syncthreads();                    // chunk c+k+1 staged
+                load_full(c + k + 1 + DEPTH, st[(k + 1) % DEPTH]);
+            }
         }
-        // LDS = c, A = c+1, B = c+2 (c + 2 < nfull <= c + 4)
-        fold(c, R);
-        __syncthreads();
-        stash(A);
-        __syncthreads();
-        fold(c + 1, R);
-        __syncthreads();
-        stash(B);
-        __syncthreads();
-        fold(c + 2, R);
-        __syncthreads();
-        c += 3;
+        // drain: LDS = c, stages = c+1 .. c+DEPTH (all < nfull), c+2*DEPTH >= nfull
+#pragma unroll
+        for (int k = 0; k < 2 * DEPTH; ++k) {
+            const int64_t cc = c + k;
+            if (cc < nfull) {
+                fold(cc, R);
+                __syncthreads();
+                if (cc + 1 < nfull) {
+                    stash(st[(k + 1) % DEPTH]);
+                    __syncthreads();
+                    if (cc + 1 + DEPTH < nfull) load_full(cc + 1 + DEPTH, st[(k + 1) % DEPTH]);
+                }
+            }
+        }
+        c = nfull;
     } else if (nfull > 0) {
-        load_full(0, A);
-        stash(A);
+        load_full(0, st[0]);
+        stash(st[0]);
         __syncthreads();
         for (; c + 1 < nfull; ++c) {
-            load_full(c + 1, A);  // in flight while wave 0 folds chunk c
+            load_full(c + 1, st[0]);  // in flight while wave 0 folds chunk c
             fold(c, R);
             __syncthreads();  // chunk c consumed
-            stash(A);
+            stash(st[0]);
             __syncthreads();  // chunk c+1 staged
         }
         fold(c, R);
         __syncthreads();
         ++c;
     }
-    for (; c < nfull; ++c) {  // full chunks the pipeline left (DEPTH 2 with nfull in 4 + 2k+1 ...)
-        load_full(c, A);
-        stash(A);
-        __syncthreads();
-        fold(c, R);
-        __syncthreads();
-    }
     if (c * R < N) {  // the last, partial chunk
-        load_rows_checked(c, A);
-        stash(A);
+        load_rows_checked(c, st[0]);
+        stash(st[0]);
         __syncthreads();
         fold(c, (int)(N - c * R));
         __syncthreads();
