@@ -257,20 +257,24 @@ def main():
                 wl.launch(v)
         order = list(range(nvar))
         rng = np.random.default_rng(12345)
+        # back-to-back launches of one variant between two events: per-launch
+        # events would add a few microseconds to every small-model launch
+        batch = max(1, min(20, int(2e9 // max(wl.bytes, 1))))
         for _ in range(max(args.steps, 5)):
             rng.shuffle(order)  # a fresh order each round: no variant always runs first
             for v in order:  # interleaved rounds in one process
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                for k in range(rounds):
-                    wl.launch(v, k)
+                for _b in range(batch):
+                    for k in range(rounds):
+                        wl.launch(v, k)
                 e1.record(stream)
                 e1.synchronize()
-                res[v].append(e0.elapsed_time(e1))
+                res[v].append(e0.elapsed_time(e1) / batch)
         for v, ts in res.items():
             ts = sorted(ts)
-            log(f"variant {v} {vname(v).decode():10s} median {ts[len(ts)//2]:.3f} ms  "
-                f"min {ts[0]:.3f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
+            log(f"variant {v} {vname(v).decode():10s} median {ts[len(ts)//2]:.4f} ms  "
+                f"min {ts[0]:.4f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
 
     sub = lay.sub
     # the exchanged model: fp32 result for fp32 updates, the RNE bf16 result
