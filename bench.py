@@ -220,13 +220,18 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
 
 
 def read_traffic(config: str):
-    """PMC HBM bytes per launch measured by the committed rocprofv3 pass (profiles/)."""
+    """PMC HBM bytes per launch from the committed rocprofv3 --pmc passes
+    (profiles/pmc_<config>.json, written by scripts/profile_c3.sh): counters
+    cannot be read from inside the timed run, so the line names that pass."""
     p = os.path.join(REPO, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, REPO)
+    src = os.path.relpath(p, REPO)
+    if d.get("provenance"):
+        src += f" ({d['provenance']})"
+    return d.get("hbm_bytes_per_launch"), src
 
 
 def main():

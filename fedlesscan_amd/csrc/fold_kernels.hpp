@@ -1118,8 +1118,9 @@ int cu_count() {
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
 //   P < 256K params                    LDS-staged, 4 waves, two chunks in flight per block:
-//                                      32-row chunks of 16-quad tiles (16-row chunks of
-//                                      32-quad tiles for 32K-128K params)
+//                                      32-row chunks of 16-quad tiles, four chunks in flight
+//                                      above 256 rows (16-row chunks of 32-quad tiles for
+//                                      32K-128K params)
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
@@ -1310,7 +1311,12 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     int rc = FA_OK;
     switch (pick_f32(N, P)) {  // every (scored, accumulate, finalize) combination
         case F32Pick::kLdsW4:
-            rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            // the narrowest models run out of bytes in flight: four chunks ahead
+            // once there are enough rows for it (1024 x 16K: +7 % over two)
+            if (N / 32 > 8)
+                rc = launch_lds_flags<4, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            else
+                rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW4T32:
             rc = launch_lds_flags<4, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--dispatches-per-call", type=int, default=1,
                     help="kernel dispatches one fa_fedavg_f32 call makes (column bands); bytes are summed per call")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--provenance", default="", help="where the passes ran (commit, date, command)")
     a = ap.parse_args()
     fetch = per_dispatch(counter_rows(a.fetch), "FETCH_SIZE", a.kernel)
     write = per_dispatch(counter_rows(a.write), "WRITE_SIZE", a.kernel)
@@ -71,6 +72,7 @@ def main():
         "traffic_over_algorithmic": (read_bytes + write_bytes) / a.bytes,
         "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads); "
                       "write = WRITE_SIZE x 1024",
+        "provenance": a.provenance,
     }
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:

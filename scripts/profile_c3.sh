@@ -1,18 +1,27 @@
 #!/bin/bash
 # Reproduce the committed C3 profiles on an MI355X (run from the repo root, e.g. via gpurun):
-#   scripts/gpu_steps.sh "prof:600:scripts/profile_c3.sh"
-# kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
-# (never combined with trace domains), then the traffic summary.
+#   scripts/gpu_steps.sh "prof:900:scripts/profile_c3.sh <tag> <commit>"
+# the bench line itself, then kernel trace + stats of the same command, then
+# FETCH_SIZE and WRITE_SIZE in separate --pmc passes (never combined with trace
+# domains), then the traffic summary profiles/pmc_c3.json that bench.py reports
+# as roofline.traffic.  Outputs: gpurun_out/prof_<tag>/.
 set -euo pipefail
+TAG=${1:-r02}
+COMMIT=${2:-unknown}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c3" -o c3 --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_c3_fetch" -o c3 -- \
-    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_c3_write" -o c3 -- \
-    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
+timeout -k 10 300 python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o c3 --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c3 -- \
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/fetch.err"
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c3 -- \
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/write.err"
 cd "$ROOT"
-python3 scripts/pmc_traffic.py --fetch "$OUT/pmc_c3_fetch" --write "$OUT/pmc_c3_write" \
-    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --dispatches-per-call 3 --out profiles/pmc_c3.json
+python3 scripts/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" \
+    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --dispatches-per-call 3 \
+    --provenance "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (C3), round $TAG, commit $COMMIT, $(date -u +%Y-%m-%dT%H:%MZ)" \
+    --out "$OUT/pmc_c3.json"
+echo done
