@@ -79,7 +79,8 @@ def round_scalars(values: Sequence, dt: np.dtype) -> np.ndarray:
     else takes the per-element loop."""
     dt = np.dtype(dt)
     try:
-        v = np.asarray(values, dtype=np.float64)
+        v = (values.astype(np.float64) if isinstance(values, np.ndarray)
+             else np.fromiter(values, dtype=np.float64, count=len(values)))
     except (TypeError, ValueError, OverflowError):
         v = None
     if v is not None and v.ndim == 1 and dt.kind == "f" and not (v.size and np.abs(v).max() >= _EXACT_F64):
