@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
+    ap.add_argument("--variants", default="", help="with --sweep: comma-separated variant numbers only")
     ap.add_argument("--splitn", action="store_true",
                     help="time the opt-in split-client fold (fa_fedavg_f32_splitn, NOT bit-exact) instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -256,11 +257,12 @@ def main():
     if args.sweep and rank == 0:
         nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()
         vname = B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name
-        res = {v: [] for v in range(nvar)}
+        chosen = [int(x) for x in args.variants.split(",") if x] or list(range(nvar))
+        res = {v: [] for v in chosen}
         for _ in range(2):
-            for v in range(nvar):
+            for v in chosen:
                 wl.launch(v)
-        order = list(range(nvar))
+        order = list(chosen)
         rng = np.random.default_rng(12345)
         # back-to-back launches of one variant between two events: per-launch
         # events would add a few microseconds to every small-model launch
