@@ -145,6 +145,8 @@ constexpr const char* kVariants[] = {
     // register-staged LDS fold with <d> chunks in flight: lds<d>_w..r..t..
     "lds3_w4r32t16", "lds4_w4r32t16", "lds6_w4r32t16", "lds4_w4r16t32", "lds3_w4r16t32", "lds4_w2r32t16",
     "lds4_w4r32t8", "lds3_w8r32t32", "lds4_w4r64t32",
+    // one-wave blocks, one quad per lane, U rows in flight in registers (gsw<threads>_u<rows>)
+    "gsw64_u16c1", "gsw64_u32c1", "gsw64_u48c1", "gsw128_u32c1", "gsw64_u24c2",
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -303,6 +305,11 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 42: rc = FA_VL(4, 32, 8, 4); break;
         case 43: rc = FA_VL(8, 32, 32, 3); break;
         case 44: rc = FA_VL(4, 64, 32, 4); break;
+        case 45: FA_VGB(8, 16, 1, 64); break;
+        case 46: FA_VGB(8, 32, 1, 64); break;
+        case 47: FA_VGB(8, 48, 1, 64); break;
+        case 48: FA_VGB(8, 32, 1, 128); break;
+        case 49: FA_VGB(8, 24, 2, 64); break;
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF

@@ -125,6 +125,9 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int c = 0; c < C; ++c) v[u][c] = ld4<NT>(p + (i + u) * ldq + c * B);
+        // deep unrolls (one-wave blocks): keep every load of the group issued
+        // before the first add (the scheduler would otherwise sink them)
+        if constexpr (U >= 16) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
