@@ -18,6 +18,7 @@ computed by libfedavg_hip.so on the GPU, or the call raises.
 from __future__ import annotations
 
 import os
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -100,25 +101,27 @@ class _FactorRing:
         self.host = [torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True) for _ in range(self.SLOTS)]
         self.done = [None] * self.SLOTS
         self.k = 0
+        self.lock = threading.Lock()  # callers on several threads share the ring
 
     def stage(self, parts: List[np.ndarray], dev: torch.device) -> List[torch.Tensor]:
         nbytes = sum(p.nbytes for p in parts)
         if nbytes > self.SLOT_BYTES:  # very many clients: plain copies
             return [torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in parts]
-        k = self.k
-        self.k = (k + 1) % self.SLOTS
-        if self.done[k] is not None:
-            self.done[k].synchronize()
-        hv = self.host[k].numpy()
-        off = 0
-        for p in parts:
-            hv[off:off + p.nbytes] = np.ascontiguousarray(p).view(np.uint8).reshape(-1)
-            off += p.nbytes
-        d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        d.copy_(self.host[k][:nbytes], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        self.done[k] = ev
+        with self.lock:
+            k = self.k
+            self.k = (k + 1) % self.SLOTS
+            if self.done[k] is not None:
+                self.done[k].synchronize()
+            hv = self.host[k].numpy()
+            off = 0
+            for p in parts:
+                hv[off:off + p.nbytes] = np.ascontiguousarray(p).view(np.uint8).reshape(-1)
+                off += p.nbytes
+            d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            d.copy_(self.host[k][:nbytes], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self.done[k] = ev
         out, off = [], 0
         for p in parts:
             out.append(d[off:off + p.nbytes].view(_NP_TO_TORCH[p.dtype]))
@@ -127,12 +130,15 @@ class _FactorRing:
 
 
 _rings: dict = {}
+_rings_lock = threading.Lock()
 
 
 def stage_factors(parts: List[np.ndarray], dev: torch.device) -> List[torch.Tensor]:
     ring = _rings.get(dev)
     if ring is None:
-        ring = _rings[dev] = _FactorRing()
+        with _rings_lock:
+            ring = _rings.setdefault(dev, None) or _FactorRing()
+            _rings[dev] = ring
     return ring.stage(parts, dev)
 
 

@@ -1,0 +1,139 @@
+"""The multi-GPU path with the HIP fold on the MI355X.
+
+The 8-GPU run belongs to the driver; here the same code runs on the one GPU
+of the box:
+  - world size 1: ShardedAggregator with its default fold (engine.fold_stacked
+    -> libfedavg_hip.so) over round-robin slots, fp32 and bf16 (the bf16 model
+    is exchanged as RNE bf16), and the reference-shaped per-layer entry;
+  - world size 2, both ranks on cuda:0, gloo exchange (host-staged): every
+    rank folds its own slots with the HIP kernels and reassembles the model.
+Everything bit-exact against the oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+from fedlesscan_amd import synth
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _scores(seed, n):
+    return [(r + 1) / 11 for r in synth.round_ids(seed, n, 10, 2)]
+
+
+@pytest.mark.parametrize("P,rounds,scored", [(10007, 3, False), (4096, 4, True), (1, 1, False)])
+def test_slots_world1_fp32(P, rounds, scored):
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    from oracle import oracle_lib as OL
+    dev = torch.device("cuda", 0)
+    N, seed = 37, 5
+    lay = SlotLayout(P, 1, rounds)
+    X = torch.zeros((N, lay.local_width), dtype=torch.float32, device=dev)
+    Xh = synth.clients_f32(seed, N, 0, P)
+    for k, (lo, hi) in enumerate(lay.slots(0)):
+        if hi > lo:
+            X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(Xh[:, lo:hi]).to(dev)
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N) if scored else None
+    full = ShardedAggregator().aggregate_slots(X, w, sc, lay)
+    exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    assert G.same_bits(full.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("P,rounds", [(8 * 1000 + 3, 2), (65536, 4)])
+def test_slots_world1_bf16_exchange(P, rounds):
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    from oracle import fedavg_oracle as O
+    dev = torch.device("cuda", 0)
+    N, seed = 29, 6
+    lay = SlotLayout(P, 1, rounds)
+    X = torch.zeros((N, lay.local_width), dtype=torch.int16, device=dev)
+    Xb = synth.clients_bf16(seed, N, 0, P)
+    for k, (lo, hi) in enumerate(lay.slots(0)):
+        if hi > lo:
+            X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(Xb[:, lo:hi].view(np.int16)).to(dev)
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N)
+    full = ShardedAggregator().aggregate_slots(X.view(torch.bfloat16), w, sc, lay)
+    assert full.dtype == torch.bfloat16
+    _, expb = O.fedavg_stacked_bf16(Xb, w, sc)
+    assert np.array_equal(full.view(torch.int16).cpu().numpy().view(np.uint16), expb)
+
+
+def test_aggregate_layers_world1_matches_reference_goldens():
+    """The reference's own fixture shapes through the sharded per-layer entry."""
+    from fedlesscan_amd.sharding import ShardedAggregator
+    case = "f32_small"
+    m = G.manifest()[case]
+    out = ShardedAggregator().aggregate_layers(G.parameters(case), m["weights"])
+    exp = G.expected(case, "fedavg")
+    assert len(out) == len(exp)
+    assert all(a.shape == b.shape and G.same_bits(a, b) for a, b in zip(out, exp))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, N, P, rounds, seed, bf16, q):
+    import torch as T
+    import torch.distributed as dist
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    T.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = T.device("cuda", 0)
+        lay = SlotLayout(P, world, rounds)
+        if bf16:
+            X = T.zeros((N, lay.local_width), dtype=T.int16, device=dev)
+        else:
+            X = T.zeros((N, lay.local_width), dtype=T.float32, device=dev)
+        for k, (lo, hi) in enumerate(lay.slots(rank)):
+            if hi > lo:
+                part = (synth.clients_bf16(seed, N, lo, hi - lo).view(np.int16) if bf16
+                        else synth.clients_f32(seed, N, lo, hi - lo))
+                X[:, k * lay.sub:k * lay.sub + hi - lo] = T.from_numpy(part).to(dev)
+        w = synth.cardinalities(seed, N)
+        sc = _scores(seed, N)
+        full = ShardedAggregator().aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc, lay)
+        q.put((rank, full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_two_ranks_on_one_gpu(bf16):
+    import torch.multiprocessing as mp
+    from oracle import fedavg_oracle as O
+    N, P, rounds, seed, world = 17, 20011, 3, 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, N, P, rounds, seed, bf16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N)
+    if bf16:
+        _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(seed, N, 0, P), w, sc)
+        for r in range(world):
+            assert np.array_equal(np.frombuffer(got[r], dtype=np.uint16), exp), r
+    else:
+        exp = O.fedavg_stacked(synth.clients_f32(seed, N, 0, P), w, sc)
+        for r in range(world):
+            assert np.array_equal(np.frombuffer(got[r], dtype=np.uint32), exp.view(np.uint32)), r
