@@ -147,6 +147,8 @@ constexpr const char* kVariants[] = {
     "lds4_w4r32t8", "lds3_w8r32t32", "lds4_w4r64t32",
     // one-wave blocks, one quad per lane, U rows in flight in registers (gsw<threads>_u<rows>)
     "gsw64_u16c1", "gsw64_u32c1", "gsw64_u48c1", "gsw128_u32c1", "gsw64_u24c2",
+    // non-power-of-two column tiles (more blocks per CU at the same row segment length)
+    "lds2_w4r32t24", "lds2_w4r64t20", "lds2_w4r32t40", "lds2_w2r16t32", "lds2_w4r16t48", "lds2_w4r64t28",
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -310,6 +312,12 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 47: FA_VGB(8, 48, 1, 64); break;
         case 48: FA_VGB(8, 32, 1, 128); break;
         case 49: FA_VGB(8, 24, 2, 64); break;
+        case 50: rc = FA_VL(4, 32, 24, 2); break;
+        case 51: rc = FA_VL(4, 64, 20, 2); break;
+        case 52: rc = FA_VL(4, 32, 40, 2); break;
+        case 53: rc = FA_VL(2, 16, 32, 2); break;
+        case 54: rc = FA_VL(4, 16, 48, 2); break;
+        case 55: rc = FA_VL(4, 64, 28, 2); break;
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
