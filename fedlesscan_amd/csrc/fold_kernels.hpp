@@ -1120,19 +1120,37 @@ int cu_count() {
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
-//   P < 256K params                    LDS-staged, 4 waves, two chunks in flight per block:
-//                                      32-row chunks of 16-quad tiles, four chunks in flight
-//                                      above 256 rows (16-row chunks of 32-quad tiles for
-//                                      32K-128K params)
+//   P < 32K params                     LDS-staged, 4 waves, 32-row chunks of 16-quad tiles,
+//                                      two chunks in flight per block (four above 256 rows)
+//   32K <= P < 256K                    LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
+//                                      40-quad tiles by how evenly the blocks fill the CUs
+//                                      (pick_lds_tile)
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 4 passes x CUs tiles
 // all with non-temporal output stores.
-enum class F32Pick { kLdsW4, kLdsW4T32, kLdsW8, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW4, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kGsBalC2, kGsBalC4 };
+// Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
+// per CU, so how evenly the blocks fill the CUs decides the time (a scan over
+// P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
+// 5.9).  Of 24-, 32- and 40-quad tiles take the one whose block count wastes
+// the least of the last round of CUs (ties: 32).
+inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
+    const int64_t nq = P >> 2, tail = (P & 3) ? 1 : 0;
+    auto waste = [&](int64_t tq) {
+        const int64_t b = (nq + tq - 1) / tq + tail;
+        return (double)(((b + cus - 1) / cus) * cus) / (double)b;
+    };
+    const double w24 = waste(24), w32 = waste(32), w40 = waste(40);
+    if (w32 <= w24 && w32 <= w40) return F32Pick::kLdsW4T32;
+    return w24 <= w40 ? F32Pick::kLdsW4T24 : F32Pick::kLdsW4T40;
+}
+
 inline F32Pick pick_f32(int64_t N, int64_t P) {
     const int64_t nq = P >> 2, cus = cu_count();
-    if (nq < (1 << 16)) return nq >= (1 << 13) && nq < (1 << 15) ? F32Pick::kLdsW4T32 : F32Pick::kLdsW4;
+    if (nq < (1 << 13)) return F32Pick::kLdsW4;
+    if (nq < (1 << 16)) return pick_lds_tile(P, cus);
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
     if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
@@ -1321,8 +1339,14 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             else
                 rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
+        case F32Pick::kLdsW4T24:
+            rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
         case F32Pick::kLdsW4T32:
             rc = launch_lds_flags<4, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW4T40:
+            rc = launch_lds_flags<4, 32, 40, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW8:
             rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

@@ -299,6 +299,35 @@ def test_rowset_lds_pointer_fold(dev, N, P, scored):
             rows[i].copy_(torch.from_numpy(X[i]))
 
 
+@pytest.mark.parametrize("P", [67267, 131072, 200001, 40003])  # 24-, 32-, 40-, 40-quad tiles (pick_lds_tile)
+@pytest.mark.parametrize("N", [70, 257])
+def test_lds_tile_picks(dev, lib, N, P):
+    """Each column tile the auto policy picks for 32K-256K params: stacked and
+    pointer-table folds, plain and stall-aware, and a two-part continued fold
+    (acc carried across rows 0..32 | 33..N-1), all bit-exact vs the oracle."""
+    from fedlesscan_amd import engine
+    L = lib.load()
+    X = synth.clients_f32(510 + N, N, 0, P)
+    w = synth.cardinalities(510 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(510, N, 10, 2)]
+    Xd = torch.from_numpy(X).to(dev)
+    s32 = np.array(sc, np.float32)
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=s32)
+    assert _bits_equal(engine.fold_stacked(Xd, w, out=_sentinel(P, dev)).cpu().numpy(), exp)
+    assert _bits_equal(engine.fold_stacked(Xd, w, sc, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]
+    assert _bits_equal(engine.fold_rows(rows, w, sc, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    div = float(np.float32(sum(w)))
+    acc = _sentinel(P, dev)
+    lib.check(L.fa_fold_f32(Xd.data_ptr(), 33, P, P, a.data_ptr(), None, None, div, 0, acc.data_ptr(), st), "f")
+    lib.check(L.fa_fold_f32(Xd[33].data_ptr(), N - 33, P, P, a[33:].data_ptr(), None, acc.data_ptr(), div, 1,
+                            acc.data_ptr(), st), "f")
+    assert _bits_equal(acc.cpu().numpy(), exp)
+
+
 def test_rowset_rejects_mixed_rows(dev):
     from fedlesscan_amd import InvalidParameterShapeError, engine
     with pytest.raises(InvalidParameterShapeError):
