@@ -12,7 +12,7 @@ bucket over xGMI (the one real exchange step of the path: SURVEY 8e).
 Default workload = BASELINE config 3: 1024 clients x 10,000,000 fp32 params on
 ONE GPU.  With --gpus N (torch.distributed.run, one process per GPU) every rank
 owns its own 10M-param bucket of a 10M*N-param model (weak scaling) and the
-global model is reassembled by all_gather_into_tensor.
+global model is reassembled by allgather_into_tensor.
 
 Inputs: integer-exact synthetic generator (fedlesscan_amd/synth.py), generated
 directly in HBM by fa_synth_*; random-init, no dataset.  Rank 0 at N=1 also
@@ -36,7 +36,7 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import SlotLayout, _gather_into  # noqa: E402
+from fedlesscan_amd.sharding import SlotLayout, gather_into  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -299,7 +299,7 @@ def main():
                 ev[0][k][1].record(stream)
             if world > 1:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
                 lo, hi = lay.round_range(k)
-                w = _gather_into(full[lo:hi], send[k * sub:(k + 1) * sub], None, async_op=True)
+                w = gather_into(full[lo:hi], send[k * sub:(k + 1) * sub], None, async_op=True)
                 if w is not None:
                     works.append(w)
         for w in works:

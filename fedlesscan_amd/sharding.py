@@ -45,7 +45,7 @@ class SlotLayout:
     (64-element aligned, the last ones partly or wholly past P).  Slot
     j = k*world + r belongs to rank r, so round k's slots of all ranks form the
     CONTIGUOUS global range [k*world*sub, (k+1)*world*sub): one
-    all_gather_into_tensor per round writes it in place, while the fold of
+    allgather_into_tensor per round writes it in place, while the fold of
     round k+1 runs.  A rank stores its slots side by side, local width
     rounds*sub.  rounds=1 is exactly bucket_bounds().
     """
@@ -71,8 +71,8 @@ class SlotLayout:
         return k * self.world * self.sub, (k + 1) * self.world * self.sub
 
 
-def _gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
-    """all_gather_into_tensor of `piece` into `full`.  16-bit payloads travel
+def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
+    """allgather_into_tensor of `piece` into `full`.  16-bit payloads travel
     as bytes (bit-identical; an all-gather moves bytes, and gloo takes neither
     bfloat16 nor int16).  Under gloo a device piece is staged through host
     memory (CPU rehearsals only); under nccl this is RCCL over xGMI."""
@@ -80,10 +80,10 @@ def _gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool)
         full, piece = full.view(torch.uint8), piece.view(torch.uint8)
     if piece.is_cuda and dist.get_backend(group) == "gloo":
         host = torch.empty(full.shape, dtype=full.dtype)
-        dist.all_gather_into_tensor(host, piece.cpu(), group=group)
+        dist.allgather_into_tensor(host, piece.cpu(), group=group)
         full.copy_(host)
         return None
-    return dist.all_gather_into_tensor(full, piece, group=group, async_op=async_op)
+    return dist.allgather_into_tensor(full, piece, group=group, async_op=async_op)
 
 
 class ShardedAggregator:
@@ -129,7 +129,7 @@ class ShardedAggregator:
             full = out[: chunk * self.world]
         else:
             full = torch.empty(chunk * self.world, dtype=local.dtype, device=local.device)
-        _gather_into(full, padded, self.group, async_op=False)
+        gather_into(full, padded, self.group, async_op=False)
         return full[:P]
 
     def aggregate(self, X_local: torch.Tensor, weights: Sequence, scores: Optional[Sequence] = None,
@@ -185,7 +185,7 @@ class ShardedAggregator:
             if self.world == 1:
                 full[lo:hi].copy_(send)
                 continue
-            w = _gather_into(full[lo:hi], send, self.group, async_op=True)
+            w = gather_into(full[lo:hi], send, self.group, async_op=True)
             if w is not None:
                 works.append(w)
         for w in works:
