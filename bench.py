@@ -12,7 +12,7 @@ bucket over xGMI (the one real exchange step of the path: SURVEY 8e).
 Default workload = BASELINE config 3: 1024 clients x 10,000,000 fp32 params on
 ONE GPU.  With --gpus N (torch.distributed.run, one process per GPU) every rank
 owns its own 10M-param bucket of a 10M*N-param model (weak scaling) and the
-global model is reassembled by allgather_into_tensor.
+global model is reassembled by all_gather_into_tensor.
 
 Inputs: integer-exact synthetic generator (fedlesscan_amd/synth.py), generated
 directly in HBM by fa_synth_*; random-init, no dataset.  Rank 0 at N=1 also

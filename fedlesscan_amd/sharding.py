@@ -45,7 +45,7 @@ class SlotLayout:
     (64-element aligned, the last ones partly or wholly past P).  Slot
     j = k*world + r belongs to rank r, so round k's slots of all ranks form the
     CONTIGUOUS global range [k*world*sub, (k+1)*world*sub): one
-    allgather_into_tensor per round writes it in place, while the fold of
+    all_gather_into_tensor per round writes it in place, while the fold of
     round k+1 runs.  A rank stores its slots side by side, local width
     rounds*sub.  rounds=1 is exactly bucket_bounds().
     """
@@ -72,7 +72,7 @@ class SlotLayout:
 
 
 def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
-    """allgather_into_tensor of `piece` into `full`.  16-bit payloads travel
+    """all_gather_into_tensor of `piece` into `full`.  16-bit payloads travel
     as bytes (bit-identical; an all-gather moves bytes, and gloo takes neither
     bfloat16 nor int16).  Under gloo a device piece is staged through host
     memory (CPU rehearsals only); under nccl this is RCCL over xGMI."""
@@ -80,10 +80,10 @@ def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
         full, piece = full.view(torch.uint8), piece.view(torch.uint8)
     if piece.is_cuda and dist.get_backend(group) == "gloo":
         host = torch.empty(full.shape, dtype=full.dtype)
-        dist.allgather_into_tensor(host, piece.cpu(), group=group)
+        dist.all_gather_into_tensor(host, piece.cpu(), group=group)
         full.copy_(host)
         return None
-    return dist.allgather_into_tensor(full, piece, group=group, async_op=async_op)
+    return dist.all_gather_into_tensor(full, piece, group=group, async_op=async_op)
 
 
 class ShardedAggregator:
