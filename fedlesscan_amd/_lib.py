@@ -41,6 +41,9 @@ _PROTOS = {
     "fa_fedavg_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_ptrs": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_ptrs_aligned": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
+    "fa_fedavg_f32_hostf": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
+    "fa_fedavg_f32_ptrs_hostf": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _int, _vp, _vp]),
+    "fa_fedavg_bf16_hostf": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
     "fa_fedavg_f32_splitn": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fold_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _f32, _int, _vp, _vp]),
     "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),
@@ -71,6 +74,9 @@ _BENCH_PROTOS = {
     "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
     "fa_num_bf16_variants": (_int, []),
     "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_f32_ptrs_variant": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
+    "fa_num_ptrs_variants": (_int, []),
+    "fa_ptrs_variant_name": (ctypes.c_char_p, [_int]),
 }
 
 _lock = threading.Lock()

@@ -9,7 +9,78 @@
 // bench.py and the variant tests load; nothing here depends on them.
 #include "fold_kernels.hpp"
 
+#include <mutex>
+
 namespace {
+
+// ---- per-client factors handed over in HOST memory (the *_hostf entries) ----
+// The reference's weights are Python numbers; its caller has them on the host.
+// A ring of slots per device, each a page-locked buffer, a device buffer and
+// an event: the factors are copied into the slot's pinned buffer, travel in
+// one async H2D on the caller's stream, the fold reads the device copy, and
+// an event recorded after the fold guards the slot, which is reused only
+// after that fold has completed.  One C call instead of an allocation, a
+// copy and an event from the host language per fold.
+constexpr int kFactorSlots = 8;
+struct FactorSlot {
+    float* host = nullptr;
+    float* dev = nullptr;
+    size_t cap = 0;  // floats
+    hipEvent_t done = nullptr;
+    bool pending = false;
+};
+struct FactorRing {
+    std::mutex mu;
+    FactorSlot slot[kFactorSlots];
+    int next = 0;
+};
+FactorRing g_factor_rings[16];
+
+// Stage a[0..N) (and s[0..N) when s != NULL) and run launch(a_dev, s_dev) on
+// `stream` with the ring slot held; the slot's event is recorded after it.
+template <class Launch>
+int with_host_factors(const float* a, const float* s, int64_t N, void* stream, Launch launch) {
+    if (N <= 0) return launch((const float*)nullptr, (const float*)nullptr);  // the entry's own checks report
+    if (!a) return fail(FA_ERR_ARG, "null host factor pointer");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return fail(FA_ERR_HIP, "hipGetDevice");
+    FactorRing& R = g_factor_rings[dev];
+    std::lock_guard<std::mutex> lk(R.mu);
+    FactorSlot& S = R.slot[R.next];
+    R.next = (R.next + 1) % kFactorSlots;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t need = (size_t)N * (s ? 2 : 1);
+    if (S.pending) {
+        hipError_t e = hipEventSynchronize(S.done);
+        if (e != hipSuccess) return fail(FA_ERR_HIP, "factor slot wait: %s", hipGetErrorString(e));
+        S.pending = false;
+    }
+    if (need > S.cap) {
+        if (S.host) (void)hipHostFree(S.host);
+        if (S.dev) (void)hipFree(S.dev);
+        S.host = nullptr;
+        S.dev = nullptr;
+        S.cap = 0;
+        const size_t cap = need < 16384 ? 16384 : need;
+        hipError_t e = hipHostMalloc((void**)&S.host, cap * sizeof(float), hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void**)&S.dev, cap * sizeof(float));
+        if (e != hipSuccess) return fail(FA_ERR_HIP, "factor slot allocation: %s", hipGetErrorString(e));
+        S.cap = cap;
+    }
+    if (!S.done) {
+        hipError_t e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+        if (e != hipSuccess) return fail(FA_ERR_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+    }
+    memcpy(S.host, a, (size_t)N * sizeof(float));
+    if (s) memcpy(S.host + N, s, (size_t)N * sizeof(float));
+    hipError_t e = hipMemcpyAsync(S.dev, S.host, need * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "factor H2D: %s", hipGetErrorString(e));
+    const int rc = launch((const float*)S.dev, s ? (const float*)(S.dev + N) : (const float*)nullptr);
+    e = hipEventRecord(S.done, st);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
+    S.pending = true;
+    return rc;
+}
 
 // One client row into a running fold with scalar factors (fa_accumulate_f32):
 // acc = (first ? t : acc + t), t = fl(fl(x*a)*s).  s == 1 multiplies exactly.
@@ -106,9 +177,9 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     // from the table
     const F32Pick pk = pick_f32(N, P);
     rc = FA_OK;
-    if (pk == F32Pick::kLdsW4)
-        rc = launch_lds_flags<4, 32, 16, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
+    if (pk == F32Pick::kLdsW2T16)  // as the stacked pick, with the pointer ring (LOPT 4)
+        rc = launch_lds_flags<2, 32, 16, 4, false, true, true, 4>(st, s != nullptr, false, true, (const float*)xi, N,
+                                                                  P, P, a, s, nullptr, divisor, out);
     else if (pk == F32Pick::kLdsW4T24)
         rc = launch_lds_flags<4, 32, 24, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
                                                          s, nullptr, divisor, out);
@@ -190,6 +261,29 @@ int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx, const int
     hipLaunchKernelGGL((k_fedavg_int<int64_t, uint64_t>), grid_for(P), dim3(kBlock), 0, (hipStream_t)stream,
                        X, N, P, ldx, a, divisor, out);
     return check_launch("k_fedavg_int<int64>");
+}
+
+// ---- the same folds with the per-client factors in host memory ---------------
+int fa_fedavg_f32_hostf(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                        float divisor, float* out, void* stream) {
+    return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
+        return fold_f32_auto(X, N, P, ldx, ad, sd, nullptr, divisor, 1, out, stream);
+    });
+}
+
+int fa_fedavg_f32_ptrs_hostf(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                             float divisor, int rows_aligned, float* out, void* stream) {
+    return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
+        return rows_aligned ? fa_fedavg_f32_ptrs_aligned(xi, N, P, ad, sd, divisor, out, stream)
+                            : fa_fedavg_f32_ptrs(xi, N, P, ad, sd, divisor, out, stream);
+    });
+}
+
+int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                         float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+    return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
+        return bf16_auto(X, N, P, ldx, ad, sd, divisor, out_f32, out_bf16, stream);
+    });
 }
 
 // ---- host staging: page-locked documents and direct DMA ---------------------

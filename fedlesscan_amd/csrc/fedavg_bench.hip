@@ -149,6 +149,17 @@ constexpr const char* kVariants[] = {
     "gsw64_u16c1", "gsw64_u32c1", "gsw64_u48c1", "gsw128_u32c1", "gsw64_u24c2",
     // non-power-of-two column tiles (more blocks per CU at the same row segment length)
     "lds2_w4r32t24", "lds2_w4r64t20", "lds2_w4r32t40", "lds2_w2r16t32", "lds2_w4r16t48", "lds2_w4r64t28",
+    // the round-2 quad fold (wave 0 alone, lane = quad) of the product's LDS picks, for A/B
+    "qf_lds4_w4r32t16", "qf_lds2_w4r32t16", "qf_lds2_w4r32t24", "qf_lds2_w4r16t32", "qf_lds2_w4r32t40",
+    "qf_lds_w8r64t32",
+    // column fold, more tile shapes (one column per lane)
+    "lds4_w4r16t16", "lds4_w2r32t8", "lds4_w4r64t16", "lds6_w4r64t16", "lds4_w8r64t16", "lds2_w2r32t4",
+    // loader A/B on the product picks: o<LOPT>[q]_... (bit 0: every lane loads a factor;
+    // bit 1: a scheduling barrier after each stage's loads; q: quad fold)
+    "o0q_lds4_w4r32t16", "o0q_lds2_w4r32t24", "o0q_lds2_w4r16t32", "o0q_lds2_w4r32t40",
+    "o1_lds4_w4r32t16", "o1_lds2_w4r32t24", "o1_lds2_w4r16t32", "o1_lds2_w4r32t40",
+    "o2_lds4_w4r32t16", "o2_lds2_w4r32t24", "o2_lds2_w4r16t32", "o2_lds2_w4r32t40",
+    "o0_lds4_w4r32t16", "o0_lds2_w4r32t24", "o0_lds2_w4r16t32", "o0_lds2_w4r32t40",
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -171,6 +182,12 @@ constexpr const char* kBf16Variants[] = {
     "bf16band2u2c8", "bf16band4u2c8", "bf16band4u8c2",
 };
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
+constexpr const char* kPtrsVariants[] = {
+    "ptrs_o0_t16", "ptrs_o4_t16", "ptrs_o0_t24", "ptrs_o4_t24", "ptrs_o0_t32", "ptrs_o4_t32",
+    "ptrs_o0_t40", "ptrs_o4_t40", "ptrs_o0q_t24", "ptrs_o4_t16d4", "ptrs_o0_t16d4",
+    "ptrs_o0_w2t16d4", "ptrs_o4_w2t16d4", "ptrs_o0_w8r64t32",
+};
+constexpr int kNumPtrsVariants = sizeof(kPtrsVariants) / sizeof(kPtrsVariants[0]);
 
 
 // Resident blocks of one balanced-kernel instantiation on the current device
@@ -318,6 +335,40 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 53: rc = FA_VL(2, 16, 32, 2); break;
         case 54: rc = FA_VL(4, 16, 48, 2); break;
         case 55: rc = FA_VL(4, 64, 28, 2); break;
+#define FA_VQ(NW, R, TQ, D) \
+    launch_lds_flags<NW, R, TQ, D, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 56: rc = FA_VQ(4, 32, 16, 4); break;
+        case 57: rc = FA_VQ(4, 32, 16, 2); break;
+        case 58: rc = FA_VQ(4, 32, 24, 2); break;
+        case 59: rc = FA_VQ(4, 16, 32, 2); break;
+        case 60: rc = FA_VQ(4, 32, 40, 2); break;
+        case 61: rc = FA_VQ(8, 64, 32, 1); break;
+#undef FA_VQ
+        case 62: rc = FA_VL(4, 16, 16, 4); break;
+        case 63: rc = FA_VL(2, 32, 8, 4); break;
+        case 64: rc = FA_VL(4, 64, 16, 4); break;
+        case 65: rc = FA_VL(4, 64, 16, 6); break;
+        case 66: rc = FA_VL(8, 64, 16, 4); break;
+        case 67: rc = FA_VL(2, 32, 4, 2); break;
+#define FA_VO(NW, R, TQ, D, CF, O) \
+    launch_lds_flags<NW, R, TQ, D, false, false, CF, O>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 68: rc = FA_VO(4, 32, 16, 4, false, 0); break;
+        case 69: rc = FA_VO(4, 32, 24, 2, false, 0); break;
+        case 70: rc = FA_VO(4, 16, 32, 2, false, 0); break;
+        case 71: rc = FA_VO(4, 32, 40, 2, false, 0); break;
+        case 72: rc = FA_VO(4, 32, 16, 4, true, 1); break;
+        case 73: rc = FA_VO(4, 32, 24, 2, true, 1); break;
+        case 74: rc = FA_VO(4, 16, 32, 2, true, 1); break;
+        case 75: rc = FA_VO(4, 32, 40, 2, true, 1); break;
+        case 76: rc = FA_VO(4, 32, 16, 4, true, 2); break;
+        case 77: rc = FA_VO(4, 32, 24, 2, true, 2); break;
+        case 78: rc = FA_VO(4, 16, 32, 2, true, 2); break;
+        case 79: rc = FA_VO(4, 32, 40, 2, true, 2); break;
+        case 80: rc = FA_VO(4, 32, 16, 4, true, 0); break;
+        case 81: rc = FA_VO(4, 32, 24, 2, true, 0); break;
+        case 82: rc = FA_VO(4, 16, 32, 2, true, 0); break;
+        case 83: rc = FA_VO(4, 32, 40, 2, true, 0); break;
+#undef FA_VO
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
@@ -383,6 +434,48 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
     }
 #undef FA_BF
     return check_launch("fedavg_bf16_variant");
+}
+
+// LDS-staged pointer-table fold (fa_fedavg_f32_ptrs_aligned's narrow picks)
+// with an explicit tile and loader: ptrs_o<LOPT>[q]_t<TQ> (see k_fold_f32_lds).
+int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                               float divisor, float* out, void* stream, int variant) {
+    int rc = check_common(N, P, P, xi, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
+    hipStream_t st = (hipStream_t)stream;
+    const float* X = (const float*)xi;
+    const bool sc = s != nullptr;
+#define FA_PV(R, TQ, D, CF, O) \
+    launch_lds_flags<4, R, TQ, D, false, true, CF, O>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor, out)
+#define FA_PW(NW, R, TQ, D, O) \
+    launch_lds_flags<NW, R, TQ, D, false, true, true, O>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor, out)
+    switch (variant) {  // must match kPtrsVariants[]
+        case 0: rc = FA_PV(32, 16, 2, true, 0); break;
+        case 1: rc = FA_PV(32, 16, 2, true, 4); break;
+        case 2: rc = FA_PV(32, 24, 2, true, 0); break;
+        case 3: rc = FA_PV(32, 24, 2, true, 4); break;
+        case 4: rc = FA_PV(16, 32, 2, true, 0); break;
+        case 5: rc = FA_PV(16, 32, 2, true, 4); break;
+        case 6: rc = FA_PV(32, 40, 2, true, 0); break;
+        case 7: rc = FA_PV(32, 40, 2, true, 4); break;
+        case 8: rc = FA_PV(32, 24, 2, false, 0); break;
+        case 9: rc = FA_PV(32, 16, 4, true, 4); break;
+        case 10: rc = FA_PV(32, 16, 4, true, 0); break;
+        case 11: rc = FA_PW(2, 32, 16, 4, 0); break;
+        case 12: rc = FA_PW(2, 32, 16, 4, 4); break;
+        case 13: rc = FA_PW(8, 64, 32, 1, 0); break;
+        default: return fail(FA_ERR_ARG, "unknown pointer variant %d", variant);
+    }
+#undef FA_PV
+#undef FA_PW
+    if (rc) return rc;
+    return check_launch("fa_fedavg_f32_ptrs_variant");
+}
+int fa_num_ptrs_variants(void) { return kNumPtrsVariants; }
+const char* fa_ptrs_variant_name(int variant) {
+    return (variant >= 0 && variant < kNumPtrsVariants) ? kPtrsVariants[variant] : "";
 }
 
 int fa_num_bf16_variants(void) { return kNumBf16Variants; }

@@ -228,7 +228,17 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
 //   ROWS: X is really `const float* const* xi`, a device table of N row
 //   pointers (separately allocated client rows, every row 16-B aligned;
 //   fa_fedavg_f32_ptrs_aligned); ldx is unused.
-template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1, bool ROWS = false>
+//
+//   COLF (the default): the staged chunk is folded by ALL waves, one column per
+//   lane: wave w owns columns [w*CPW, (w+1)*CPW) of the block's TQ*4, CPW =
+//   TQ*4/NW.  Per row a lane issues one 4-byte LDS read, a multiply and an add,
+//   and the NW waves fold side by side on their own SIMDs.  The quad fold
+//   (COLF = false, wave 0 alone, lane = quad: two packed multiplies and two
+//   packed adds per row with TQ of 64 lanes active) kept the other waves at the
+//   barrier for most of each chunk when a CU holds only one block (1024 x 16K:
+//   ~0.5 us of fold per 8 KB chunk).  Per column the arithmetic is the same.
+template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1, bool ROWS = false,
+          bool COLF = true, int LOPT = 0>
 __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
@@ -298,48 +308,87 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         const int64_t q = q0 + (t + j * NT) % TQ;
         return q < nq ? q : nq - 1;
     };
-    // one chunk in registers: its LQ quads per lane and (lanes < R) its factors
+    // one chunk in registers: its LQ quads per lane and (lanes < R) its
+    // factors; ROWS with the pointer ring: also the row pointers of the chunk
+    // this stage loads next
+    constexpr bool PRING = ROWS && (LOPT & 4);
     struct Stage {
         f32x4 v[LQ];
         float fv, sv;
+        const float* p[PRING ? LQ : 1];
     };
     Stage st[DEPTH > 1 ? DEPTH : 1];
     const int64_t nfull = N / R;  // chunks taken by the pipelined loop
-    // ROWS: each lane reads its own row's pointer from the table (8 B, a
-    // cache-resident line shared by the lanes of a row).  The pointers of the
-    // NEXT chunk are fetched while this chunk's data loads go out (the
-    // pipelined loop loads chunks in increasing order), so no table load sits
-    // right in front of a data load.  Vector loads on purpose: a scalar load
-    // would share lgkmcnt with the fold's LDS reads and, returning out of
-    // order, force the fold to wait for it.
-    const float* nxt[ROWS ? LQ : 1];
-    auto fetch_ptrs = [&](int64_t c) {  // chunk c < nfull
+    // ROWS: each lane reads its own rows' pointers from the table (8 B, a
+    // cache-resident line shared by the lanes of a row), with vector loads: a
+    // scalar load would share lgkmcnt with the fold's LDS reads and, returning
+    // out of order, force the fold to wait for it.  Two schedules:
+    //   next-chunk (LOPT bit 2 clear): the pointers of chunk c+1 are fetched
+    //     right behind chunk c's data loads; issuing chunk c+1 then waits for
+    //     them, and so (waits count loads in issue order) for chunk c's data;
+    //   pointer ring (bit 2 set): chunk c always goes through stage c % DEPTH,
+    //     which right after its data fetches the pointers of chunk c + dist
+    //     (dist = stages in flight), the next chunk it loads; that wait falls
+    //     after chunk c has been stashed anyway.
+    // Loader options (LOPT, measured with the tuning variants o<LOPT>_*):
+    //   bit 0: every lane loads a factor (lanes >= R a duplicate) instead of
+    //     `if (t < R)`.  Whole waves skip the guarded load, so the compiler
+    //     cannot count a stage's loads and waits for more than the oldest
+    //     stage before a stash (down to vmcnt(0)): the guarded form keeps
+    //     fewer bytes in flight per block;
+    //   bit 1: a scheduling barrier after each stage's loads, so the
+    //     prologue's factor loads are not sunk behind later stages' data (the
+    //     loop-carried wait counts would merge to the worst case).
+    //   Bits 0+1 give exact waits (all DEPTH stages in flight) -- and ran
+    //   SLOWER where several blocks share a CU: 1024 x 67K, 24-quad tiles,
+    //   bit 0 alone 47.3 us against 45.0 with neither (the same sweep,
+    //   profiles/r02_lds/loader_ab_sweep.log); both bits were slower still in
+    //   a first run of it.  The shallower effective pipeline of the guarded
+    //   loader is the better one there.  The product uses LOPT 0, and 4 (the
+    //   pointer ring) only for the pointer-table form of the narrowest pick,
+    //   one block per CU (1024 x 16K rows: 20.3 against 26.1 us; 1024 x 67K,
+    //   24-quad tiles: 57.3 against 53.8 us, profiles/r02_lds/ptrs_variants.log).
+    const float* nxt[ROWS && !PRING ? LQ : 1];
+    auto fetch_ptrs = [&](int64_t c, Stage& g) {  // chunk index clamped, no branch
         if constexpr (ROWS) {
+            const int64_t cc = c < nfull ? c : nfull - 1;
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) nxt[j] = xi[c * R + (t + j * NT) / TQ];
+            for (int j = 0; j < LQ; ++j) {
+                const float* p = xi[cc * R + (t + j * NT) / TQ];
+                if constexpr (PRING) g.p[j] = p;
+                else nxt[j] = p;
+            }
         }
     };
-    if (ROWS && nfull > 0) fetch_ptrs(0);
     // Full chunks stream through loops whose loads carry no checks and no
     // control flow: a branch between a load and its use makes the compiler
     // wait for the load right after issuing it, which would serialise the
     // chunk loads with the fold.
-    auto load_full = [&](int64_t c, Stage& g) {  // chunk c: rows [c*R, c*R + R)
+    auto load_full = [&](int64_t c, Stage& g, int dist) {  // chunk c: rows [c*R, c*R + R)
         if constexpr (ROWS) {
 #pragma unroll
-            for (int j = 0; j < LQ; ++j)  // a global (not flat) load: the table holds device pointers
-                g.v[j] = __builtin_nontemporal_load((const gf32x4*)nxt[j] + qof(j));
-            if (c + 1 < nfull) fetch_ptrs(c + 1);
+            for (int j = 0; j < LQ; ++j) {  // a global (not flat) load: the table holds device pointers
+                const float* p;
+                if constexpr (PRING) p = g.p[j];
+                else p = nxt[j];
+                g.v[j] = __builtin_nontemporal_load((const gf32x4*)p + qof(j));
+            }
         } else {
             const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
 #pragma unroll
             for (int j = 0; j < LQ; ++j)
                 g.v[j] = __builtin_nontemporal_load(X4 + (c * R + (t + j * NT) / TQ) * ldq + qof(j));
         }
-        if (t < R) {
+        if constexpr (LOPT & 1) {
+            g.fv = a[c * R + t % R];
+            if constexpr (SCORED) g.sv = s[c * R + t % R];
+        } else if (t < R) {
             g.fv = a[c * R + t];
             if constexpr (SCORED) g.sv = s[c * R + t];
         }
+        if constexpr (PRING) fetch_ptrs(c + dist, g);
+        else if (c + 1 < nfull) fetch_ptrs(c + 1, g);
+        if constexpr ((LOPT & 2) != 0) __builtin_amdgcn_sched_barrier(0);
     };
     auto load_rows_checked = [&](int64_t c, Stage& g) {  // the last, partial chunk: rows < N only
 #pragma unroll
@@ -360,13 +409,45 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
             if constexpr (SCORED) fs[t] = g.sv;
         }
     };
+    // column fold: this lane's column of the block (COLF)
+    constexpr int TC = TQ * 4, CPW = (TC + NW - 1) / NW;
+    static_assert(!COLF || CPW <= 64, "column fold: at most one column per lane");
+    const int ccol = (t >> 6) * CPW + (t & 63);
+    const bool cfold = (t & 63) < CPW && ccol < tq * 4;
+    const float* tilef = reinterpret_cast<const float*>(tile);
+    float acc1 = 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if constexpr (ACC) {
-        if (t < tq) acc = reinterpret_cast<const f32x4*>(acc_in)[q0 + t];
+        if constexpr (COLF) {
+            if (cfold) acc1 = acc_in[q0 * 4 + ccol];
+        } else {
+            if (t < tq) acc = reinterpret_cast<const f32x4*>(acc_in)[q0 + t];
+        }
     }
-    // fold the staged chunk c (rows valid rows) in client order, lane = quad
+    // fold the staged chunk c (rows valid rows) in client order
     auto fold = [&](int64_t c, int rows) {
-        if (t < tq) {
+        if constexpr (COLF) {
+            if (cfold) {
+                int r = 0;
+                if (!ACC && c == 0) {
+                    acc1 = term1<SCORED>(tilef[ccol], fa[0], SCORED ? fs[0] : 1.0f);
+                    r = 1;
+                }
+                for (; r + 8 <= rows; r += 8) {
+                    float x[8], f[8], g[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        x[k] = tilef[(r + k) * TC + ccol];
+                        f[k] = fa[r + k];
+                        g[k] = SCORED ? fs[r + k] : 1.0f;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc1 = acc1 + term1<SCORED>(x[k], f[k], g[k]);
+                }
+                for (; r < rows; ++r)
+                    acc1 = acc1 + term1<SCORED>(tilef[r * TC + ccol], fa[r], SCORED ? fs[r] : 1.0f);
+            }
+        } else if (t < tq) {  // lane = quad, wave 0 only
             int r = 0;
             if (!ACC && c == 0) {
                 acc = term4<SCORED>(tile[t], fa[0], SCORED ? fs[0] : 1.0f);
@@ -395,11 +476,13 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         // holds chunk c+i (i = 1..DEPTH), loading.  Stage indices are static
         // after unrolling (c stays a multiple of DEPTH at the loop head), so the
         // stages live in registers; the steady-state loop has no conditional load.
-        load_full(0, st[0]);
+#pragma unroll
+        for (int k = 0; k < (PRING ? DEPTH : 1); ++k) fetch_ptrs(k, st[k]);
+        load_full(0, st[0], DEPTH);
         stash(st[0]);
         __syncthreads();
 #pragma unroll
-        for (int k = 1; k <= DEPTH; ++k) load_full(k, st[k % DEPTH]);
+        for (int k = 1; k <= DEPTH; ++k) load_full(k, st[k % DEPTH], DEPTH);
         for (; c + 2 * DEPTH < nfull; c += DEPTH) {
 #pragma unroll
             for (int k = 0; k < DEPTH; ++k) {
@@ -407,7 +490,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
                 __syncthreads();                    // chunk c+k consumed
                 stash(st[(k + 1) % DEPTH]);         // waits for that stage only
                 __syncthreads();                    // chunk c+k+1 staged
-                load_full(c + k + 1 + DEPTH, st[(k + 1) % DEPTH]);
+                load_full(c + k + 1 + DEPTH, st[(k + 1) % DEPTH], DEPTH);
             }
         }
         // drain: LDS = c, stages = c+1 .. c+DEPTH (all < nfull), c+2*DEPTH >= nfull
@@ -420,17 +503,18 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
                 if (cc + 1 < nfull) {
                     stash(st[(k + 1) % DEPTH]);
                     __syncthreads();
-                    if (cc + 1 + DEPTH < nfull) load_full(cc + 1 + DEPTH, st[(k + 1) % DEPTH]);
+                    if (cc + 1 + DEPTH < nfull) load_full(cc + 1 + DEPTH, st[(k + 1) % DEPTH], DEPTH);
                 }
             }
         }
         c = nfull;
     } else if (nfull > 0) {
-        load_full(0, st[0]);
+        fetch_ptrs(0, st[0]);
+        load_full(0, st[0], 1);
         stash(st[0]);
         __syncthreads();
         for (; c + 1 < nfull; ++c) {
-            load_full(c + 1, st[0]);  // in flight while wave 0 folds chunk c
+            load_full(c + 1, st[0], 1);  // in flight while chunk c is folded
             fold(c, R);
             __syncthreads();  // chunk c consumed
             stash(st[0]);
@@ -447,7 +531,9 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         fold(c, (int)(N - c * R));
         __syncthreads();
     }
-    if (t < tq) {
+    if constexpr (COLF) {
+        if (cfold) __builtin_nontemporal_store(FIN ? acc1 / divisor : acc1, out + q0 * 4 + ccol);
+    } else if (t < tq) {
         const f32x4 res = FIN ? div4(acc, divisor) : acc;
         __builtin_nontemporal_store(res, reinterpret_cast<f32x4*>(out) + q0 + t);
     }
@@ -1120,8 +1206,8 @@ int cu_count() {
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
-//   P < 32K params                     LDS-staged, 4 waves, 32-row chunks of 16-quad tiles,
-//                                      two chunks in flight per block (four above 256 rows)
+//   P < 32K params                     LDS-staged, 2 waves, 32-row chunks of 16-quad tiles,
+//                                      four chunks in flight per block
 //   32K <= P < 256K                    LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
 //                                      40-quad tiles by how evenly the blocks fill the CUs
 //                                      (pick_lds_tile)
@@ -1130,7 +1216,7 @@ int cu_count() {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 4 passes x CUs tiles
 // all with non-temporal output stores.
-enum class F32Pick { kLdsW4, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kGsBalC2, kGsBalC4 };
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1149,7 +1235,7 @@ inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
 
 inline F32Pick pick_f32(int64_t N, int64_t P) {
     const int64_t nq = P >> 2, cus = cu_count();
-    if (nq < (1 << 13)) return F32Pick::kLdsW4;
+    if (nq < (1 << 13)) return F32Pick::kLdsW2T16;
     if (nq < (1 << 16)) return pick_lds_tile(P, cus);
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
@@ -1239,7 +1325,8 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 }
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
-template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false, bool ROWS = false>
+template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false, bool ROWS = false, bool COLF = true,
+          int LOPT = 0>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
     // blocks over the full quads, plus one for the P%4 tail columns
@@ -1248,7 +1335,7 @@ int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
         return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
     const dim3 grid((unsigned)blocks), block(NW * 64);
 #define FA_L(SC, ACC, FIN)                                                                                   \
-    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH, ROWS>), grid, block, 0, st, X, N, P, ldx, a, s, \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH, ROWS, COLF, LOPT>), grid, block, 0, st, X, N, P, ldx, a, s, \
                        acc_in, d, out)
     if constexpr (!ALLF) {
         if (sc) FA_L(true, false, true); else FA_L(false, false, true);
@@ -1331,13 +1418,11 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     }
     int rc = FA_OK;
     switch (pick_f32(N, P)) {  // every (scored, accumulate, finalize) combination
-        case F32Pick::kLdsW4:
-            // the narrowest models run out of bytes in flight: four chunks ahead
-            // once there are enough rows for it (1024 x 16K: +7 % over two)
-            if (N / 32 > 8)
-                rc = launch_lds_flags<4, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            else
-                rc = launch_lds_flags<4, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+        case F32Pick::kLdsW2T16:
+            // the narrowest models (one block per CU): two-wave blocks, four
+            // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
+            // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
+            rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW4T24:
             rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

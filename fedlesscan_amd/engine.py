@@ -156,6 +156,10 @@ class Factors:
             self.div = np.dtype(dt).type(self.total)
         self.s = None if scores is None else round_scalars(scores, dt)
 
+    def host(self):
+        """(a, s) as host addresses for the *_hostf entries (s: None)."""
+        return self.a.ctypes.data, (None if self.s is None else self.s.ctypes.data)
+
     def to(self, device):
         parts = [self.a] if self.s is None else [self.a, self.s]
         staged = stage_factors(parts, device)
@@ -193,10 +197,9 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
     st = stream_ptr(dev)
     if X.dtype == torch.bfloat16:
         f = Factors(weights, scores, np.dtype(np.float32), total=total)
-        a, s = f.to(dev)
         out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
         outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
-        _lib.call("fa_fedavg_bf16", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+        _lib.call("fa_fedavg_bf16_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div),
                   out.data_ptr(), _ptr(outb), st)
         return (out, outb) if want_bf16 else out
     in_dt = np.dtype(_TORCH_TO_NP.get(X.dtype, np.void))
@@ -218,15 +221,19 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
         X = X.to(_NP_TO_TORCH[dt])
         ldx = X.stride(0) if N > 1 else max(P, 1)
     f = Factors(weights, scores, dt, total=total)
-    a, s = f.to(dev)
     out = out if out is not None else torch.empty(P, dtype=_NP_TO_TORCH[dt], device=dev)
     if dt == np.float32:
         # the split-client kernel needs 16-B aligned rows; any other layout
         # takes the exact fold, which is bit-identical to the reference
         split = not exact and X.data_ptr() % 16 == 0 and ldx % 4 == 0 and out.data_ptr() % 16 == 0
-        name = "fa_fedavg_f32_splitn" if split else "fa_fedavg_f32"
-        _lib.call(name, X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), st)
+        if split:
+            a, s = f.to(dev)
+            _lib.call("fa_fedavg_f32_splitn", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                      out.data_ptr(), st)
+        else:  # factors from host memory: the library stages them (one C call)
+            _lib.call("fa_fedavg_f32_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div), out.data_ptr(), st)
     else:
+        a, s = f.to(dev)
         _lib.call("fa_fedavg_f64", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
                   out.data_ptr(), st)
     return out
@@ -310,11 +317,10 @@ def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
         return fold_stacked(X, weights, scores, out=out, total=total)
     dev = rs.device
     f = Factors(weights, scores, np.dtype(np.float32), total=total)
-    a, s = f.to(dev)
     out = out if out is not None else torch.empty(rs.P, dtype=torch.float32, device=dev)
     aligned = rs.aligned and out.data_ptr() % 16 == 0
-    _lib.call("fa_fedavg_f32_ptrs_aligned" if aligned else "fa_fedavg_f32_ptrs", rs.ptrs.data_ptr(), rs.N, rs.P,
-              a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), stream_ptr(dev))
+    _lib.call("fa_fedavg_f32_ptrs_hostf", rs.ptrs.data_ptr(), rs.N, rs.P, *f.host(), float(f.div), int(aligned),
+              out.data_ptr(), stream_ptr(dev))
     return out
 
 

@@ -109,6 +109,24 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                    const float* a, const float* s, float divisor,
                    float* out_f32, uint16_t* out_bf16, void* stream);
 
+/* The same folds with the per-client factors a[0..N), s[0..N) (s may be
+ * NULL) in HOST memory, as the reference's caller holds them (Python numbers,
+ * fed_avg_aggregator.py:32-41).  The library copies them into a page-locked
+ * slot of its own, sends them in one async H2D on `stream` ahead of the fold
+ * and reuses the slot only after that fold has completed, so a and s may be
+ * freed or rewritten as soon as the call returns.  X, xi, out stay device
+ * pointers.  _ptrs: rows_aligned != 0 takes fa_fedavg_f32_ptrs_aligned's
+ * kernels (every row 16-B aligned, out 16-B aligned), 0 fa_fedavg_f32_ptrs. */
+int fa_fedavg_f32_hostf(const float* X, int64_t N, int64_t P, int64_t ldx,
+                        const float* a, const float* s, float divisor,
+                        float* out, void* stream);
+int fa_fedavg_f32_ptrs_hostf(const float* const* xi, int64_t N, int64_t P,
+                             const float* a, const float* s, float divisor,
+                             int rows_aligned, float* out, void* stream);
+int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                         const float* a, const float* s, float divisor,
+                         float* out_f32, uint16_t* out_bf16, void* stream);
+
 /* float64 updates (the reference unit-test fixture is float64,
  * test/test_aggregation.py:23-38). */
 int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx,

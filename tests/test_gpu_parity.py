@@ -299,6 +299,33 @@ def test_rowset_lds_pointer_fold(dev, N, P, scored):
             rows[i].copy_(torch.from_numpy(X[i]))
 
 
+@pytest.mark.parametrize("N,P", [(1, 5), (31, 16387), (33, 4099), (100, 67267), (257, 20011)])
+def test_ptrs_loader_variants(dev, lib, N, P):
+    """Every loader schedule / tile of the LDS pointer-table fold (tuning
+    library): chunk edges (N % R), the last clamped block and the P % 4 tail
+    block, plain and stall-aware, bit-exact vs the oracle."""
+    B = lib.load_bench()
+    X = synth.clients_f32(81 + N, N, 0, P)
+    w = synth.cardinalities(81 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(81, N, 10, 2)]
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]
+    tab = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    assert B.fa_num_ptrs_variants() >= 8
+    for v in range(B.fa_num_ptrs_variants()):
+        for sp, e in ((None, exp), (s, exp_s)):
+            o = _sentinel(P, dev)
+            _bcheck(B.fa_fedavg_f32_ptrs_variant(tab.data_ptr(), N, P, a.data_ptr(),
+                                                 None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v),
+                    "ptrs variant")
+            assert _bits_equal(o.cpu().numpy(), e), (B.fa_ptrs_variant_name(v), N, P, sp is not None)
+
+
 @pytest.mark.parametrize("P", [67267, 131072, 200001, 40003])  # 24-, 32-, 40-, 40-quad tiles (pick_lds_tile)
 @pytest.mark.parametrize("N", [70, 257])
 def test_lds_tile_picks(dev, lib, N, P):
@@ -399,6 +426,55 @@ def test_gpu_synth_matches_host(dev, lib):
     Xb = torch.empty((3, 1000), dtype=torch.int16, device=dev)
     _bcheck(B.fa_synth_bf16(Xb.data_ptr(), 3, 1000, 1000, 78, 0, 5, st), "synth_bf16")
     assert np.array_equal(Xb.cpu().numpy().view(np.uint16), synth.clients_bf16(78, 3, 5, 1000))
+
+
+def test_host_factor_entries_reuse_slots(dev, lib):
+    """fa_*_hostf: factors handed over in host memory.  More calls than the
+    library's staging slots, queued without synchronising, with the host
+    arrays overwritten right after each call, and client counts that make the
+    slots grow: every result still bit-exact vs the oracle."""
+    L = lib.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    P = 4099
+    Nmax = 9001  # with scores: 18002 floats > a slot's initial 16384
+    X = torch.from_numpy(synth.clients_f32(17, Nmax, 0, P)).to(dev)
+    Xh = X.cpu().numpy()
+    Xb = torch.from_numpy(synth.clients_bf16(18, 40, 0, P).view(np.int16)).to(dev)
+    rows = [X[i].clone() for i in range(64)]
+    tab = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+    jobs = []
+    for k in range(21):
+        N = (3, 64, 40, 700, Nmax)[k % 5]
+        w = synth.cardinalities(300 + k, N)
+        sc = [(r + 1) / 11 for r in synth.round_ids(300 + k, N, 10, 2)] if k % 2 else None
+        a = np.array(w, np.float32)
+        s = None if sc is None else np.array(sc, np.float32)
+        div = float(np.float32(sum(w)))
+        sp = None if s is None else s.ctypes.data
+        kind = ("stacked", "ptrs", "bf16")[k % 3] if N <= 64 else "stacked"
+        if kind == "bf16" and N > 40:
+            kind = "stacked"
+        o = _sentinel(P, dev)
+        if kind == "stacked":
+            lib.check(L.fa_fedavg_f32_hostf(X.data_ptr(), N, P, P, a.ctypes.data, sp, div, o.data_ptr(), st), "hostf")
+            exp = OL.fedavg_f32(Xh[:N], a, np.float32(sum(w)), s=s)
+        elif kind == "ptrs":
+            lib.check(L.fa_fedavg_f32_ptrs_hostf(tab.data_ptr(), N, P, a.ctypes.data, sp, div, k % 4 == 1,
+                                               o.data_ptr(), st), "ptrs_hostf")
+            exp = OL.fedavg_f32(Xh[:N], a, np.float32(sum(w)), s=s)
+        else:
+            lib.check(L.fa_fedavg_bf16_hostf(Xb.data_ptr(), N, P, P, a.ctypes.data, sp, div, o.data_ptr(), None, st),
+                   "bf16_hostf")
+            from oracle import fedavg_oracle as O
+            exp, _ = O.fedavg_stacked_bf16(synth.clients_bf16(18, 40, 0, P)[:N], w, sc)
+        a[:] = -7.0  # the library copied them: overwriting now must not matter
+        if s is not None:
+            s[:] = 3.0
+        jobs.append((o, exp, kind, N))
+    for o, exp, kind, N in jobs:
+        assert _bits_equal(o.cpu().numpy(), np.asarray(exp, np.float32)), (kind, N)
+    with pytest.raises(Exception):
+        lib.check(L.fa_fedavg_f32_hostf(X.data_ptr(), 0, P, P, None, None, 1.0, X.data_ptr(), st), "hostf N=0")
 
 
 def test_error_mapping(dev, lib):
@@ -599,7 +675,7 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
 
 
 def _lds_variants(B):
-    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"lds", b"ring"))]
+    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"lds", b"ring", b"qf_", b"o0", b"o1", b"o2"))]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])

@@ -22,6 +22,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--clients", type=int, default=1024)
 ap.add_argument("--params", type=int, default=1_000_000)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--variants", action="store_true", help="also time the tuning library's pointer variants")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 N, P = args.clients, args.params
@@ -79,6 +80,17 @@ t_shuf_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(shuf_tab.dat
 ord_tab = torch.from_numpy(np.array([X[i].data_ptr() for i in range(N)], dtype=np.int64)).to(dev)
 t_ord_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ord_tab.data_ptr(), N, P, a_dev.data_ptr(),
                                                                   None, div, out.data_ptr(), st), "ptrs"))
+# loader / tile variants of the LDS pointer fold (tuning library), kernel alone
+var = {}
+if args.variants:
+    B = _lib.load_bench()
+    for v in range(B.fa_num_ptrs_variants()):
+        name = B.fa_ptrs_variant_name(v).decode()
+        o2 = torch.empty(P, dtype=torch.float32, device=dev)
+        fn = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), None, div,
+                                                             o2.data_ptr(), st, v), "ptrs variant", bench=True)
+        var[name] = round(timed(fn), 4)
+        assert torch.equal(o2.view(torch.int32), engine.fold_stacked(X, w).view(torch.int32)), name
 same_shuf = torch.equal(engine.fold_rows(rs_shuf, w_shuf).view(torch.int32),
                         engine.fold_stacked(X[torch.from_numpy(perm).to(dev)], w_shuf).view(torch.int32))
 ref = engine.fold_stacked(X, w).view(torch.int32)
@@ -90,4 +102,4 @@ print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_
                   "shuffled_kernel_ms": round(t_shuf_kern, 4), "inorder_table_kernel_ms": round(t_ord_kern, 4),
                   "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
                   "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
-                  "bit_identical": bool(same and same_shuf)}))
+                  "bit_identical": bool(same and same_shuf), **({"variants_kernel_ms": var} if var else {})}))
