@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--splitn", action="store_true",
                     help="time the opt-in split-client fold (fa_fedavg_f32_splitn, NOT bit-exact) instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unpadded", action="store_true",
+                    help="row pitch = the model size exactly (experiments: odd sizes give rows that are not 16-B "
+                         "aligned, as a torch.stack of such a model)")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=8)
     ap.add_argument("--clients", type=int, default=0, help="override the config's client count (experiments)")
@@ -106,10 +109,11 @@ class Workload:
     slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
     With rounds=1 that is one contiguous bucket per rank."""
 
-    def __init__(self, cfg, rank, world, dev, rounds):
+    def __init__(self, cfg, rank, world, dev, rounds, align=None):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
-        self.layout = SlotLayout(self.P_total, world, rounds)
+        self.layout = (SlotLayout(self.P_total, world, rounds) if align is None
+                       else SlotLayout(self.P_total, world, rounds, align=align))
         self.slots = self.layout.slots(rank)
         self.P = sum(hi - lo for lo, hi in self.slots)  # real columns this rank folds
         self.rank, self.world, self.dev = rank, world, dev
@@ -247,7 +251,7 @@ def main():
     rounds = args.rounds or (1 if world == 1 else 4)
     if args.splitn:
         args.variant = -1
-    wl = Workload(cfg, rank, world, dev, rounds)
+    wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None)
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,

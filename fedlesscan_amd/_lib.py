@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import sysconfig
 import threading
 
 from .aggregator.exceptions import (
@@ -22,6 +23,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip.so")
 BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
+# host-only CPython helper (csrc/hostfast.c), built next to the libraries
+HOSTFAST_PATH = os.path.join(PKG, "_native", "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
 ABI_VERSION = 2

@@ -171,10 +171,10 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
             hipLaunchKernelGGL((k_fold_f32_rows_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, xi,  \
                                N, P, a, s, divisor, out, tiles);                                               \
     }
+    // narrow models (the stacked fold's LDS-staged picks) and everything up
+    // to ~3M params: the LDS-staged fold reading row bases from the table;
     // large models: ~one block per CU walking 16 KiB tiles (as the stacked
-    // default); mid-size: one block per 4 KiB tile; narrow models (the
-    // stacked fold's LDS-staged picks): the LDS-staged fold reading row bases
-    // from the table
+    // default)
     const F32Pick pk = pick_f32(N, P);
     rc = FA_OK;
     if (pk == F32Pick::kLdsW2T16)  // as the stacked pick, with the pointer ring (LOPT 4)
@@ -192,8 +192,15 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     else if (pk == F32Pick::kLdsW8)
         rc = launch_lds_flags<8, 64, 32, 1, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
                                                          s, nullptr, divisor, out);
-    else if ((P >> 2) >= (int64_t)kBlock * 4 * cu_count()) FA_R(8, 4, (int64_t)cu_count())
-    else FA_R(8, 1, 0)
+    else if ((P >> 2) < ((int64_t)3 << 18))
+        // up to ~3M params, past the stacked fold's LDS range: the 32-quad LDS
+        // fold beat the tile kernel below on table rows (100 x 582K: 42.3
+        // against 76.6 us; 1024 x 2.5M: 1.62 against 1.70 ms), but not at 4M
+        // with 1024 clients (2.60 against 2.49 ms) (profiles/r02_lds/dw_ptrs.log,
+        // ptrs_large.log, ptrs_mid.log)
+        rc = launch_lds_flags<4, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
+    else FA_R(8, 4, (int64_t)cu_count())
 #undef FA_R
     if (rc) return rc;
     return check_launch("fa_fedavg_f32_ptrs_aligned");
@@ -205,13 +212,28 @@ int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
-    if (s)
-        hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, true>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P, a,
-                           s, divisor, out);
+    // rows at any 4-B offset.  Narrow models: the LDS-staged fold with 4-byte
+    // loads and row bases from the table; otherwise one lane per column, row
+    // bases wave-uniform.  (The round-2 kernel, a lane per 4 columns with a
+    // per-row alignment test, ran 7-10x slower on unaligned rows:
+    // profiles/r02_lds/dw_ptrs.log.)
+    const int64_t nq = P >> 2;
+    const float* X = (const float*)xi;
+    const bool sc = s != nullptr;
+    if (nq > 0 && nq < (1 << 13))
+        rc = launch_lds_flags<2, 32, 16, 4, false, true, true, 4, true>(st, sc, false, true, X, N, P, P, a, s, nullptr,
+                                                                        divisor, out);
+    else if (nq > 0 && N >= 256 && nq < (1 << 16))
+        rc = launch_lds_flags<4, 32, 24, 2, false, true, true, 0, true>(st, sc, false, true, X, N, P, P, a, s, nullptr,
+                                                                        divisor, out);
+    else if (sc)
+        hipLaunchKernelGGL(k_fold_f32_rows_scalar<true>, grid_for(P), dim3(kBlock), 0, st, xi, N, P, a, s, divisor,
+                           out);
     else
-        hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, false>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N, P,
-                           a, s, divisor, out);
-    return check_launch("k_fedavg_f32_ptrs");
+        hipLaunchKernelGGL(k_fold_f32_rows_scalar<false>, grid_for(P), dim3(kBlock), 0, st, xi, N, P, a, s, divisor,
+                           out);
+    if (rc) return rc;
+    return check_launch("fa_fedavg_f32_ptrs");
 }
 
 int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,

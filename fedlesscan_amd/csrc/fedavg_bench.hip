@@ -160,7 +160,12 @@ constexpr const char* kVariants[] = {
     "o1_lds4_w4r32t16", "o1_lds2_w4r32t24", "o1_lds2_w4r16t32", "o1_lds2_w4r32t40",
     "o2_lds4_w4r32t16", "o2_lds2_w4r32t24", "o2_lds2_w4r16t32", "o2_lds2_w4r32t40",
     "o0_lds4_w4r32t16", "o0_lds2_w4r32t24", "o0_lds2_w4r16t32", "o0_lds2_w4r32t40",
+    // 4-byte loads (rows not 16-B aligned; these also run on unaligned input), and
+    // the per-column scalar fold the product used for such input in round 2
+    "dw_lds4_w2r32t16", "dw_lds2_w4r32t24", "dw_lds2_w4r16t32", "dw_lds2_w4r32t40", "dw_lds2_w8r32t32",
+    "dw_lds2_w4r64t32", "dw_lds3_w8r32t32", "scalar",
 };
+constexpr int kFirstAnyAlign = 84;  // variants from here on take any 4-B aligned layout
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // Quads per lane of the round-1 row-streaming policy (variant "v4_pickq_nts"):
@@ -186,6 +191,8 @@ constexpr const char* kPtrsVariants[] = {
     "ptrs_o0_t16", "ptrs_o4_t16", "ptrs_o0_t24", "ptrs_o4_t24", "ptrs_o0_t32", "ptrs_o4_t32",
     "ptrs_o0_t40", "ptrs_o4_t40", "ptrs_o0q_t24", "ptrs_o4_t16d4", "ptrs_o0_t16d4",
     "ptrs_o0_w2t16d4", "ptrs_o4_w2t16d4", "ptrs_o0_w8r64t32",
+    // any row alignment (4-byte loads / lane = column / the round-2 generic kernel)
+    "ptrs_dw_w2t16d4", "ptrs_dw_t40", "ptrs_dw_t32", "ptrs_dw_t24", "ptrs_rows_scalar", "ptrs_generic",
 };
 constexpr int kNumPtrsVariants = sizeof(kPtrsVariants) / sizeof(kPtrsVariants[0]);
 
@@ -253,8 +260,8 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
     int rc = check_common(N, P, ldx, X, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
-    // unaligned layouts take the product's scalar fold, whatever the variant
-    if (!aligned16(X) || (ldx % 4) || !aligned16(out))
+    // unaligned layouts take the product's fold, except the any-alignment variants
+    if (variant < kFirstAnyAlign && (!aligned16(X) || (ldx % 4) || !aligned16(out)))
         return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream);
     hipStream_t st = (hipStream_t)stream;
     const bool sc = s != nullptr, acc = false, fin = true;
@@ -369,6 +376,20 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 82: rc = FA_VO(4, 16, 32, 2, true, 0); break;
         case 83: rc = FA_VO(4, 32, 40, 2, true, 0); break;
 #undef FA_VO
+#define FA_VD(NW, R, TQ, D) \
+    launch_lds_flags<NW, R, TQ, D, false, false, true, 0, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 84: rc = FA_VD(2, 32, 16, 4); break;
+        case 85: rc = FA_VD(4, 32, 24, 2); break;
+        case 86: rc = FA_VD(4, 16, 32, 2); break;
+        case 87: rc = FA_VD(4, 32, 40, 2); break;
+        case 88: rc = FA_VD(8, 32, 32, 2); break;
+        case 89: rc = FA_VD(4, 64, 32, 2); break;
+        case 90: rc = FA_VD(8, 32, 32, 3); break;
+#undef FA_VD
+        case 91:
+            if (sc) launch_scalar<true, false, true>(st, X, N, P, ldx, a, s, acc_in, divisor, out);
+            else launch_scalar<false, false, true>(st, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
@@ -443,7 +464,7 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
     int rc = check_common(N, P, P, xi, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
-    if (!aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
+    if (variant < 14 && !aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
     hipStream_t st = (hipStream_t)stream;
     const float* X = (const float*)xi;
     const bool sc = s != nullptr;
@@ -466,6 +487,26 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
         case 11: rc = FA_PW(2, 32, 16, 4, 0); break;
         case 12: rc = FA_PW(2, 32, 16, 4, 4); break;
         case 13: rc = FA_PW(8, 64, 32, 1, 0); break;
+#define FA_PD(NW, R, TQ, D, O) \
+    launch_lds_flags<NW, R, TQ, D, false, true, true, O, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor, \
+                                                              out)
+        case 14: rc = FA_PD(2, 32, 16, 4, 4); break;
+        case 15: rc = FA_PD(4, 32, 40, 2, 0); break;
+        case 16: rc = FA_PD(4, 16, 32, 2, 0); break;
+        case 17: rc = FA_PD(4, 32, 24, 2, 0); break;
+#undef FA_PD
+        case 18:
+            if (sc) hipLaunchKernelGGL(k_fold_f32_rows_scalar<true>, grid_for(P), dim3(kBlock), 0, st, xi, N, P, a, s,
+                                       divisor, out);
+            else hipLaunchKernelGGL(k_fold_f32_rows_scalar<false>, grid_for(P), dim3(kBlock), 0, st, xi, N, P, a, s,
+                                    divisor, out);
+            break;
+        case 19:
+            if (sc) hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, true>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi, N,
+                                       P, a, s, divisor, out);
+            else hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, false>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi,
+                                    N, P, a, s, divisor, out);
+            break;
         default: return fail(FA_ERR_ARG, "unknown pointer variant %d", variant);
     }
 #undef FA_PV

@@ -63,6 +63,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // f32x4 in the global address space: loads through pointers read from memory
 // (row tables) are global_load, not flat_load
 typedef __attribute__((address_space(1))) const f32x4 gf32x4;
+typedef __attribute__((address_space(1))) const float gf32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -237,8 +238,15 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
 //   packed adds per row with TQ of 64 lanes active) kept the other waves at the
 //   barrier for most of each chunk when a CU holds only one block (1024 x 16K:
 //   ~0.5 us of fold per 8 KB chunk).  Per column the arithmetic is the same.
+//
+//   DW: 4-byte loads (lane = one float of a row segment) instead of 16-byte
+//   quads, for rows that are not 16-B aligned (a row pitch that is not a
+//   multiple of 4 floats: a torch.stack of an odd-sized model, or separately
+//   allocated rows at any 4-B offset).  Consecutive lanes still read
+//   consecutive floats of one row, so every wave-load is one contiguous
+//   256-byte run; the tile in LDS and the fold are the same.
 template <int NW, int R, int TQ, bool SCORED, bool ACC, bool FIN, int DEPTH = 1, bool ROWS = false,
-          bool COLF = true, int LOPT = 0>
+          bool COLF = true, int LOPT = 0, bool DW = false>
 __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
@@ -312,10 +320,19 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     // factors; ROWS with the pointer ring: also the row pointers of the chunk
     // this stage loads next
     constexpr bool PRING = ROWS && (LOPT & 4);
+    constexpr int LU = DW ? 4 * LQ : LQ;  // loads per thread per chunk
+    constexpr int RW = DW ? 4 * TQ : TQ;  // load units per row of the tile
     struct Stage {
-        f32x4 v[LQ];
+        f32x4 v[DW ? 1 : LQ];
+        float vf[DW ? LU : 1];
         float fv, sv;
-        const float* p[PRING ? LQ : 1];
+        const float* p[PRING ? LU : 1];
+    };
+    // DW: this lane's float of the tile for its j-th load, clamped to the last
+    // column of the full quads
+    auto fof = [&](int j) -> int64_t {
+        const int64_t col = q0 * 4 + (t + j * NT) % RW;
+        return col < nq * 4 ? col : nq * 4 - 1;
     };
     Stage st[DEPTH > 1 ? DEPTH : 1];
     const int64_t nfull = N / R;  // chunks taken by the pipelined loop
@@ -348,13 +365,13 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     //   pointer ring) only for the pointer-table form of the narrowest pick,
     //   one block per CU (1024 x 16K rows: 20.3 against 26.1 us; 1024 x 67K,
     //   24-quad tiles: 57.3 against 53.8 us, profiles/r02_lds/ptrs_variants.log).
-    const float* nxt[ROWS && !PRING ? LQ : 1];
+    const float* nxt[ROWS && !PRING ? LU : 1];
     auto fetch_ptrs = [&](int64_t c, Stage& g) {  // chunk index clamped, no branch
         if constexpr (ROWS) {
             const int64_t cc = c < nfull ? c : nfull - 1;
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) {
-                const float* p = xi[cc * R + (t + j * NT) / TQ];
+            for (int j = 0; j < LU; ++j) {
+                const float* p = xi[cc * R + (t + j * NT) / RW];
                 if constexpr (PRING) g.p[j] = p;
                 else nxt[j] = p;
             }
@@ -367,12 +384,17 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     auto load_full = [&](int64_t c, Stage& g, int dist) {  // chunk c: rows [c*R, c*R + R)
         if constexpr (ROWS) {
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) {  // a global (not flat) load: the table holds device pointers
+            for (int j = 0; j < LU; ++j) {  // a global (not flat) load: the table holds device pointers
                 const float* p;
                 if constexpr (PRING) p = g.p[j];
                 else p = nxt[j];
-                g.v[j] = __builtin_nontemporal_load((const gf32x4*)p + qof(j));
+                if constexpr (DW) g.vf[j] = __builtin_nontemporal_load((const gf32*)p + fof(j));
+                else g.v[j] = __builtin_nontemporal_load((const gf32x4*)p + qof(j));
             }
+        } else if constexpr (DW) {
+#pragma unroll
+            for (int j = 0; j < LU; ++j)
+                g.vf[j] = __builtin_nontemporal_load(X + (c * R + (t + j * NT) / RW) * ldx + fof(j));
         } else {
             const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
 #pragma unroll
@@ -392,9 +414,12 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     };
     auto load_rows_checked = [&](int64_t c, Stage& g) {  // the last, partial chunk: rows < N only
 #pragma unroll
-        for (int j = 0; j < LQ; ++j) {
-            const int64_t row = c * R + (t + j * NT) / TQ;
-            if (row < N) g.v[j] = __builtin_nontemporal_load((const gf32x4*)rowf(row) + qof(j));
+        for (int j = 0; j < LU; ++j) {
+            const int64_t row = c * R + (t + j * NT) / RW;
+            if (row < N) {
+                if constexpr (DW) g.vf[j] = __builtin_nontemporal_load((const gf32*)rowf(row) + fof(j));
+                else g.v[j] = __builtin_nontemporal_load((const gf32x4*)rowf(row) + qof(j));
+            }
         }
         if (t < R && c * R + t < N) {
             g.fv = a[c * R + t];
@@ -402,8 +427,14 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         }
     };
     auto stash = [&](const Stage& g) {
+        if constexpr (DW) {
+            float* tw = reinterpret_cast<float*>(tile);  // [R][TQ*4] floats, the quad layout's bytes
 #pragma unroll
-        for (int j = 0; j < LQ; ++j) tile[t + j * NT] = g.v[j];
+            for (int j = 0; j < LU; ++j) tw[t + j * NT] = g.vf[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < LQ; ++j) tile[t + j * NT] = g.v[j];
+        }
         if (t < R) {
             fa[t] = g.fv;
             if constexpr (SCORED) fs[t] = g.sv;
@@ -875,6 +906,29 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_f32_ptrs(
     }
 }
 
+// List-of-rows form, rows at any 4-B offset, large models: lane = one column,
+// row i's base a wave-uniform load from the table, 8 rows of loads ahead of the
+// ordered adds.  Consecutive lanes read consecutive floats of a row: every
+// wave-load is one contiguous 256-byte run, whatever the row's alignment.
+template <bool SCORED>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_rows_scalar(
+    const float* const* __restrict__ xi, int64_t N, int64_t P,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor, float* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= P) return;
+    float acc = term1<SCORED>(((const gf32*)xi[0])[c], a[0], SCORED ? s[0] : 1.0f);
+    int64_t i = 1;
+    for (; i + 8 <= N; i += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load((const gf32*)xi[i + u] + c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + term1<SCORED>(v[u], a[i + u], SCORED ? s[i + u] : 1.0f);
+    }
+    for (; i < N; ++i) acc = acc + term1<SCORED>(((const gf32*)xi[i])[c], a[i], SCORED ? s[i] : 1.0f);
+    out[c] = acc / divisor;
+}
+
 // List-of-rows form with every row 16-B aligned (fa_fedavg_f32_ptrs_aligned):
 // the tile structure of the stacked fold (C quads per lane, U rows ahead) with
 // row i's base read from xi[i] (a wave-uniform scalar load).  No branch sits
@@ -1326,7 +1380,7 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).
 template <int NW, int R, int TQ, int DEPTH = 1, bool ALLF = false, bool ROWS = false, bool COLF = true,
-          int LOPT = 0>
+          int LOPT = 0, bool DW = false>
 int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
     // blocks over the full quads, plus one for the P%4 tail columns
@@ -1335,7 +1389,7 @@ int launch_lds_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X
         return fail(FA_ERR_ARG, "P=%lld too large for an LDS-staged launch", (long long)P);
     const dim3 grid((unsigned)blocks), block(NW * 64);
 #define FA_L(SC, ACC, FIN)                                                                                   \
-    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH, ROWS, COLF, LOPT>), grid, block, 0, st, X, N, P, ldx, a, s, \
+    hipLaunchKernelGGL((k_fold_f32_lds<NW, R, TQ, SC, ACC, FIN, DEPTH, ROWS, COLF, LOPT, DW>), grid, block, 0, st, X, N, P, ldx, a, s, \
                        acc_in, d, out)
     if constexpr (!ALLF) {
         if (sc) FA_L(true, false, true); else FA_L(false, false, true);
@@ -1404,6 +1458,22 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     const bool sc = s != nullptr, acc = acc_in != nullptr, fin = finalize != 0;
     const bool vec = (N == 0 || aligned16(X)) && (ldx % 4 == 0) && aligned16(out) &&
                      (!acc || aligned16(acc_in));
+    if (!vec && N > 0 && (P >> 2) > 0 && ((P >> 2) < (1 << 13) || (N >= 256 && (P >> 2) < (1 << 16)))) {
+        // rows not 16-B aligned (an odd pitch: a torch.stack of an odd-sized
+        // model), narrow models: the LDS-staged fold with 4-byte loads.  The
+        // per-column scalar fold below re-reads each row's segment once per
+        // lane-column and ran 1.7x slower at 1024 x 16K-67K; from ~256K params
+        // (or below 256 clients) it is as fast (profiles/r02_lds/dw_sweep.log)
+        int rc;
+        if ((P >> 2) < (1 << 13))
+            rc = launch_lds_flags<2, 32, 16, 4, true, false, true, 0, true>(st, sc, acc, fin, X, N, P, ldx, a, s,
+                                                                            acc_in, divisor, out);
+        else
+            rc = launch_lds_flags<4, 32, 40, 2, true, false, true, 0, true>(st, sc, acc, fin, X, N, P, ldx, a, s,
+                                                                            acc_in, divisor, out);
+        if (rc) return rc;
+        return check_launch("fold_f32 (4-byte loads)");
+    }
     if (!vec) {
 #define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
         if (sc) {

@@ -72,6 +72,32 @@ def result_dtype(in_dtype: np.dtype, weights: Sequence, scores: Optional[Sequenc
 _EXACT_F64 = float(2 ** 53)
 
 
+def _load_hostfast():
+    """The optional CPython helper built next to the HIP libraries (hostfast.c);
+    None when it is absent (the numpy path below gives the same bits)."""
+    if not os.path.exists(_lib.HOSTFAST_PATH):
+        return None
+    from importlib.util import module_from_spec, spec_from_file_location
+    spec = spec_from_file_location("_hostfast", _lib.HOSTFAST_PATH)
+    mod = module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_hostfast = _load_hostfast()
+
+
+def weak_f32(values) -> Optional[np.ndarray]:
+    """np.float32 roundings of `values` when every item is exactly a Python
+    bool, int (|v| < 2**53) or float -- numpy's weak scalars, which keep a
+    float32 fold float32 -- in one C loop; None otherwise (or without the
+    helper), for the general path: result_dtype + round_scalars."""
+    if _hostfast is None:
+        return None
+    b = _hostfast.round_weak_f32(values)
+    return None if b is None else np.frombuffer(b, dtype=np.float32)
+
+
 def round_scalars(values: Sequence, dt: np.dtype) -> np.ndarray:
     """[dt(v) for v in values] -- numpy's rounding of Python (or numpy) scalars
     to `dt`, vectorised.  Going through float64 first is exact whenever every
@@ -156,6 +182,28 @@ class Factors:
             self.div = np.dtype(dt).type(self.total)
         self.s = None if scores is None else round_scalars(scores, dt)
 
+    @classmethod
+    def weak_f32(cls, weights: Sequence, scores: Optional[Sequence], total=None) -> Optional["Factors"]:
+        """Factors of a float32 fold whose weights, scores and total are all
+        weak Python scalars (the reference's cardinalities and scores are):
+        the result dtype is float32 without a type scan and the rounding is
+        one C loop.  None when any value is something else."""
+        if total is not None and type(total) not in (bool, int, float):
+            return None
+        a = weak_f32(weights)
+        if a is None:
+            return None
+        s = None
+        if scores is not None:
+            s = weak_f32(scores)
+            if s is None:
+                return None
+        f = cls.__new__(cls)
+        f.total = sum(weights) if total is None else total
+        f.a, f.s = a, s
+        f.div = np.float32(f.total)
+        return f
+
     def host(self):
         """(a, s) as host addresses for the *_hostf entries (s: None)."""
         return self.a.ctypes.data, (None if self.s is None else self.s.ctypes.data)
@@ -196,7 +244,7 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
     dev = X.device
     st = stream_ptr(dev)
     if X.dtype == torch.bfloat16:
-        f = Factors(weights, scores, np.dtype(np.float32), total=total)
+        f = Factors.weak_f32(weights, scores, total) or Factors(weights, scores, np.dtype(np.float32), total=total)
         out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
         outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
         _lib.call("fa_fedavg_bf16_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div),
@@ -205,7 +253,9 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
     in_dt = np.dtype(_TORCH_TO_NP.get(X.dtype, np.void))
     if in_dt == np.void:
         raise InvalidParameterShapeError(f"unsupported dtype {X.dtype}")
-    dt = result_dtype(in_dt, weights, scores, total)
+    # the common case (float32 layers, Python-number weights) skips the type scan
+    fw = Factors.weak_f32(weights, scores, total) if in_dt == np.float32 else None
+    dt = np.dtype(np.float32) if fw is not None else result_dtype(in_dt, weights, scores, total)
     int_path = in_dt.kind == "i" and scores is None and all(isinstance(w, int) for w in weights)
     if int_path:
         f = Factors(weights, None, dt, int_weights=True, total=total)
@@ -220,7 +270,7 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
         # numpy promotes the operand before multiplying; same on the device.
         X = X.to(_NP_TO_TORCH[dt])
         ldx = X.stride(0) if N > 1 else max(P, 1)
-    f = Factors(weights, scores, dt, total=total)
+    f = fw or Factors(weights, scores, dt, total=total)
     out = out if out is not None else torch.empty(P, dtype=_NP_TO_TORCH[dt], device=dev)
     if dt == np.float32:
         # the split-client kernel needs 16-B aligned rows; any other layout
@@ -309,14 +359,16 @@ def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
     if len(weights) != rs.N or (scores is not None and len(scores) != rs.N):
         raise InvalidParameterShapeError(f"{rs.N} rows but {len(weights)} weights"
                                          + ("" if scores is None else f" / {len(scores)} scores"))
-    if rs.dtype != torch.float32 or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32:
+    fw = Factors.weak_f32(weights, scores, total) if rs.dtype == torch.float32 else None
+    if fw is None and (rs.dtype != torch.float32
+                       or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32):
         return fold_stacked(torch.stack(rs.rows), weights, scores, out=out, total=total)
     if rs.view is not None or rs.P == 0:
         # rows of one allocation at a fixed pitch: the stacked fold, no pointer table
         X = rs.view if rs.view is not None else torch.stack(rs.rows)
         return fold_stacked(X, weights, scores, out=out, total=total)
     dev = rs.device
-    f = Factors(weights, scores, np.dtype(np.float32), total=total)
+    f = fw or Factors(weights, scores, np.dtype(np.float32), total=total)
     out = out if out is not None else torch.empty(rs.P, dtype=torch.float32, device=dev)
     aligned = rs.aligned and out.data_ptr() % 16 == 0
     _lib.call("fa_fedavg_f32_ptrs_hostf", rs.ptrs.data_ptr(), rs.N, rs.P, *f.host(), float(f.div), int(aligned),

@@ -6,8 +6,10 @@
                           host ingest (NPZ index / pack, BSON walk)
   libfedavg_hip_bench.so  bench / tuning support: fedavg_bench.hip (kernel
                           variants, HBM input generator, read-sweep calibration)
+  _hostfast.<abi>.so      host-only CPython helper (gcc): rounding a list of
+                          Python weights to float32 in one C loop (hostfast.c)
 
-Both compile in parallel.  The .so files land in fedlesscan_amd/_native/
+All compile in parallel.  The .so files land in fedlesscan_amd/_native/
 (git-ignored, but shipped to the GPU box by gpurun with the rest of the tree).
 """
 from __future__ import annotations
@@ -16,6 +18,7 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
@@ -29,10 +32,13 @@ BENCH_HDR = os.path.join(REPO, "include", "fedavg_hip_bench.h")
 OUT_DIR = os.path.join(PKG, "_native")
 LIB = os.path.join(OUT_DIR, "libfedavg_hip.so")
 BENCH_LIB = os.path.join(OUT_DIR, "libfedavg_hip_bench.so")
+HOSTFAST_SRC = os.path.join(CSRC, "hostfast.c")
+HOSTFAST = os.path.join(OUT_DIR, "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))  # = _lib.HOSTFAST_PATH
 # library -> (sources compiled into it, files it depends on)
 TARGETS = {
     LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, HDR, *HOST_SRCS]),
     BENCH_LIB: ([BENCH_SRC], [BENCH_SRC, KERNELS, HDR, BENCH_HDR]),
+    HOSTFAST: ([HOSTFAST_SRC], [HOSTFAST_SRC]),
 }
 ARCH = os.environ.get("FEDAVG_OFFLOAD_ARCH", "gfx950")
 
@@ -64,8 +70,13 @@ def build(force: bool = False, isa_dir: str | None = None) -> str:
         if not force and not _stale(lib):
             continue
         tmp = lib + ".tmp"
-        cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, *srcs]
         cwd = None
+        if lib == HOSTFAST:
+            cc = os.environ.get("CC") or shutil.which("gcc") or "cc"
+            cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", "-I", sysconfig.get_paths()["include"], "-o", tmp, *srcs]
+            jobs.append((lib, tmp, subprocess.Popen(cmd)))
+            continue
+        cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), "-o", tmp, *srcs]
         if isa_dir:
             cwd = os.path.join(isa_dir, os.path.basename(lib).split(".")[0])
             os.makedirs(cwd, exist_ok=True)
@@ -73,7 +84,7 @@ def build(force: bool = False, isa_dir: str | None = None) -> str:
         jobs.append((lib, tmp, subprocess.Popen(cmd, cwd=cwd)))
     failed = [lib for lib, _, p in jobs if p.wait() != 0]
     if failed:
-        raise RuntimeError(f"hipcc failed for {', '.join(os.path.basename(f) for f in failed)}")
+        raise RuntimeError(f"native build failed for {', '.join(os.path.basename(f) for f in failed)}")
     for lib, tmp, _ in jobs:
         os.replace(tmp, lib)
     return LIB

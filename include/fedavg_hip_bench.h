@@ -46,9 +46,11 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                            float* out_f32, uint16_t* out_bf16, void* stream, int variant);
 int fa_num_bf16_variants(void);
 const char* fa_bf16_variant_name(int variant);
-/* The LDS-staged pointer-table fold (xi = device table of N 16-B aligned
- * row pointers, as fa_fedavg_f32_ptrs_aligned) with an explicit tile and
- * loader schedule, variant in [0, fa_num_ptrs_variants()). */
+/* The pointer-table fold (xi = device table of N row pointers) with an
+ * explicit kernel, tile and loader schedule, variant in
+ * [0, fa_num_ptrs_variants()): variants named ptrs_o* need every row and out
+ * 16-B aligned (as fa_fedavg_f32_ptrs_aligned); ptrs_dw_*, ptrs_rows_scalar
+ * and ptrs_generic take rows at any 4-B offset (as fa_fedavg_f32_ptrs). */
 int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P,
                                const float* a, const float* s, float divisor,
                                float* out, void* stream, int variant);

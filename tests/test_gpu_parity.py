@@ -326,6 +326,49 @@ def test_ptrs_loader_variants(dev, lib, N, P):
             assert _bits_equal(o.cpu().numpy(), e), (B.fa_ptrs_variant_name(v), N, P, sp is not None)
 
 
+@pytest.mark.parametrize("N,P", [(1, 7), (33, 4099), (257, 16387), (300, 67267), (70, 300_001)])
+def test_ptrs_any_alignment(dev, lib, N, P):
+    """Row tables whose rows are NOT 16-B aligned (X[i] of an unpadded [N, P]
+    tensor with P % 4 != 0, shifted by one float): the product's
+    fa_fedavg_f32_ptrs / RowSet path and every any-alignment pointer variant,
+    plain and stall-aware, bit-exact vs the oracle."""
+    from fedlesscan_amd import engine
+    L, B = lib.load(), lib.load_bench()
+    Xh = synth.clients_f32(520 + N, N, 0, P)
+    buf = torch.zeros(N * P + 1, dtype=torch.float32, device=dev)
+    X = buf[1:].view(N, P)
+    X.copy_(torch.from_numpy(Xh).to(dev))
+    rows = [X[i] for i in range(N)]
+    tab = torch.tensor([r.data_ptr() for r in rows[::-1]], dtype=torch.int64, device=dev)  # reversed order
+    w = synth.cardinalities(520 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(520 + N, N, 10, 2)]
+    wr, scr = w[::-1], sc[::-1]
+    a = torch.tensor(wr, dtype=torch.float32, device=dev)
+    s = torch.tensor(scr, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Xr = Xh[::-1].copy()
+    exp = OL.fedavg_f32(Xr, np.array(wr, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(Xr, np.array(wr, np.float32), np.float32(sum(w)), s=np.array(scr, np.float32))
+    vs = [v for v in range(B.fa_num_ptrs_variants())
+          if B.fa_ptrs_variant_name(v).startswith((b"ptrs_dw", b"ptrs_rows_scalar", b"ptrs_generic"))]
+    assert len(vs) >= 5
+    for v in [None] + vs:
+        for sp, e in ((None, exp), (s, exp_s)):
+            o = _sentinel(P, dev)
+            spp = None if sp is None else sp.data_ptr()
+            if v is None:
+                lib.check(L.fa_fedavg_f32_ptrs(tab.data_ptr(), N, P, a.data_ptr(), spp, div, o.data_ptr(), st), "ptrs")
+            else:
+                _bcheck(B.fa_fedavg_f32_ptrs_variant(tab.data_ptr(), N, P, a.data_ptr(), spp, div, o.data_ptr(), st,
+                                                     v), "ptrs any-align variant")
+            assert _bits_equal(o.cpu().numpy(), e), ("product" if v is None else B.fa_ptrs_variant_name(v), N, P,
+                                                     sp is not None)
+    rs = engine.RowSet(rows[::-1])
+    assert rs.view is None and not rs.aligned
+    assert _bits_equal(engine.fold_rows(rs, wr, scr, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
+
+
 @pytest.mark.parametrize("P", [67267, 131072, 200001, 40003])  # 24-, 32-, 40-, 40-quad tiles (pick_lds_tile)
 @pytest.mark.parametrize("N", [70, 257])
 def test_lds_tile_picks(dev, lib, N, P):
@@ -675,7 +718,8 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
 
 
 def _lds_variants(B):
-    return [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"lds", b"ring", b"qf_", b"o0", b"o1", b"o2"))]
+    return [v for v in range(B.fa_num_variants())
+            if B.fa_variant_name(v).startswith((b"lds", b"ring", b"qf_", b"o0", b"o1", b"o2", b"dw_", b"scalar"))]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
@@ -705,6 +749,41 @@ def test_lds_variants_chunk_and_tile_edges(dev, lib, N, P):
                                               None if sp is None else sp.data_ptr(), div, o.data_ptr(), st, v),
                       "lds variant")
             assert _bits_equal(o.cpu().numpy(), e), (B.fa_variant_name(v), N, P, sp is not None)
+
+
+@pytest.mark.parametrize("N,P,pitch,off", [(1, 5, 5, 1), (33, 4099, 4099, 0), (70, 16387, 16390, 3),
+                                           (257, 67267, 67267, 0), (100, 582026, 582027, 1), (31, 3, 7, 2)])
+def test_any_alignment_variants(dev, lib, N, P, pitch, off):
+    """The 4-byte-load LDS folds (and the scalar fold) on rows that are not
+    16-B aligned: odd pitches and a base offset of 1-3 floats, plain and
+    stall-aware, bit-exact vs the oracle; the product fold on the same layout."""
+    L, B = lib.load(), lib.load_bench()
+    Xh = synth.clients_f32(410 + N, N, 0, P)
+    buf = torch.zeros(N * pitch + off + 4, dtype=torch.float32, device=dev)
+    view = buf[off:off + N * pitch].view(N, pitch)[:, :P]
+    view.copy_(torch.from_numpy(Xh).to(dev))
+    w = synth.cardinalities(410 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(410 + N, N, 10, 2)]
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    vs = [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"dw_", b"scalar"))]
+    assert len(vs) >= 5
+    for v in [None] + vs:
+        for sp, e in ((None, exp), (s, exp_s)):
+            o = torch.full((P + 1,), float("nan"), dtype=torch.float32, device=dev)[1:]  # 4-B offset output
+            spp = None if sp is None else sp.data_ptr()
+            if v is None:
+                lib.check(L.fa_fedavg_f32(view.data_ptr(), N, P, pitch, a.data_ptr(), spp, div, o.data_ptr(), st),
+                          "auto")
+            else:
+                _bcheck(B.fa_fedavg_f32_variant(view.data_ptr(), N, P, pitch, a.data_ptr(), spp, div, o.data_ptr(),
+                                                st, v), "any-align variant")
+            name = "auto" if v is None else B.fa_variant_name(v)
+            assert _bits_equal(o.cpu().numpy(), e), (name, N, P, pitch, off, sp is not None)
 
 
 @pytest.mark.parametrize("N,P,pad", [(9, 1030, 2), (300, 65537, 63), (5, 300001, 3), (257, 2_100_003, 61),

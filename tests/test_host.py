@@ -108,6 +108,39 @@ def test_factors_round_like_numpy():
     assert f.s[0] == (np.ones(1, np.float32) * (1 / 3))[0]
 
 
+def test_weak_f32_helper_matches_numpy():
+    """The C rounding helper (hostfast.c) gives numpy's float32 of every weak
+    Python scalar bit for bit, and declines (None) whatever numpy would treat
+    differently; Factors.weak_f32 then equals the general Factors."""
+    assert engine._hostfast is not None, "native build did not produce _hostfast"
+
+    class F(float):
+        pass
+
+    rng = np.random.default_rng(3)
+    floats = [float(x) for x in rng.standard_normal(300) * 10.0 ** rng.integers(-45, 40, 300)]
+    floats += [0.0, -0.0, float("inf"), -float("inf"), 1e39, -1e39, 5e-324, 1.4e-45, 7e-46, 3.4028235e38,
+               3.4028236e38, 0.1, 1 / 3, 16777217.0]
+    ints = [int(x) for x in rng.integers(-2 ** 52, 2 ** 52, 200)] + [0, 1, -1, 16777217, 2 ** 53 - 1, -(2 ** 53 - 1)]
+    vals = floats + ints + [True, False]
+    got = engine.weak_f32(vals)
+    exp = np.array([np.float32(v) for v in vals], dtype=np.float32)
+    assert got.view(np.uint32).tolist() == exp.view(np.uint32).tolist()
+    nan = engine.weak_f32([float("nan")])
+    assert np.isnan(nan[0])
+    assert engine.weak_f32(tuple(ints)).tolist() == [np.float32(v) for v in ints]
+    assert engine.weak_f32([]).size == 0
+    for bad in ([1, 2 ** 53], [1, -(2 ** 53)], [2 ** 70], [np.float64(1.0)], [np.int64(3)], [1, F(2.0)],
+                [1, "2"], [1, None], [np.float32(1)]):
+        assert engine.weak_f32(bad) is None, bad
+    w, sc = [3, 16777217, 2.5, 0.1, True], [1 / 3, 2 / 3, 0.7, 1.0, 0.5]
+    fw, fg = engine.Factors.weak_f32(w, sc), engine.Factors(w, sc, np.dtype(np.float32))
+    assert fw.a.tobytes() == fg.a.tobytes() and fw.s.tobytes() == fg.s.tobytes()
+    assert np.float32(fw.div).tobytes() == np.float32(fg.div).tobytes() and fw.total == fg.total
+    assert engine.Factors.weak_f32(w, None, total=np.int64(7)) is None
+    assert engine.Factors.weak_f32([np.float64(1.0)], None) is None
+
+
 def test_cardinality_resolution_quirks():
     from fedlesscan_amd import UnknownCardinalityError
     assert resolve_cardinality(5, None) == 5

@@ -31,6 +31,10 @@ st = torch.cuda.current_stream(dev).cuda_stream
 X = torch.empty((N, P), dtype=torch.float32, device=dev)
 _lib.check(_lib.load_bench().fa_synth_f32(X.data_ptr(), N, P, P, 9, 0, 0, st), "synth", bench=True)
 rows = [X[i].clone() for i in range(N)]  # separate allocations
+# a table of X[i]: rows of one allocation in their natural order (16-B aligned only when P % 4 == 0)
+ord_tab = torch.from_numpy(np.array([X[i].data_ptr() for i in range(N)], dtype=np.int64)).to(dev)
+# the product entry for tables of X[i] rows: the aligned one only when they are
+xrows_fold = L.fa_fedavg_f32_ptrs_aligned if P % 4 == 0 else L.fa_fedavg_f32_ptrs
 w = synth.cardinalities(9, N)
 
 
@@ -74,11 +78,9 @@ assert rs_shuf.view is None
 t_shuf = timed(lambda: engine.fold_rows(rs_shuf, w_shuf))
 shuf_tab = rs_shuf.ptrs
 a_shuf = torch.tensor([float(np.float32(x)) for x in w_shuf], dtype=torch.float32, device=dev)
-t_shuf_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(shuf_tab.data_ptr(), N, P, a_shuf.data_ptr(),
+t_shuf_kern = timed(lambda: _lib.check(xrows_fold(shuf_tab.data_ptr(), N, P, a_shuf.data_ptr(),
                                                                     None, div, out.data_ptr(), st), "ptrs"))
-# the same kernel over rows of one allocation in their natural order (a table of X[i])
-ord_tab = torch.from_numpy(np.array([X[i].data_ptr() for i in range(N)], dtype=np.int64)).to(dev)
-t_ord_kern = timed(lambda: _lib.check(L.fa_fedavg_f32_ptrs_aligned(ord_tab.data_ptr(), N, P, a_dev.data_ptr(),
+t_ord_kern = timed(lambda: _lib.check(xrows_fold(ord_tab.data_ptr(), N, P, a_dev.data_ptr(),
                                                                   None, div, out.data_ptr(), st), "ptrs"))
 # loader / tile variants of the LDS pointer fold (tuning library), kernel alone
 var = {}
@@ -91,6 +93,12 @@ if args.variants:
                                                              o2.data_ptr(), st, v), "ptrs variant", bench=True)
         var[name] = round(timed(fn), 4)
         assert torch.equal(o2.view(torch.int32), engine.fold_stacked(X, w).view(torch.int32)), name
+        if name.startswith(("ptrs_dw", "ptrs_rows_scalar", "ptrs_generic")):
+            # the same rows through a table of X[i] (16-B aligned only when P % 4 == 0)
+            fu = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ord_tab.data_ptr(), N, P, a_dev.data_ptr(), None,
+                                                                 div, o2.data_ptr(), st, v), "ptrs variant", bench=True)
+            var[name + "@xrows"] = round(timed(fu), 4)
+            assert torch.equal(o2.view(torch.int32), engine.fold_stacked(X, w).view(torch.int32)), name
 same_shuf = torch.equal(engine.fold_rows(rs_shuf, w_shuf).view(torch.int32),
                         engine.fold_stacked(X[torch.from_numpy(perm).to(dev)], w_shuf).view(torch.int32))
 ref = engine.fold_stacked(X, w).view(torch.int32)
