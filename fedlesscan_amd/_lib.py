@@ -56,6 +56,7 @@ _PROTOS = {
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i64": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_npz_index": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int]),
+    "fa_crc32": (_int, [_vp, _i64, ctypes.c_uint32, _int, ctypes.POINTER(ctypes.c_uint32)]),
     "fa_pack": (_int, [_vp, _vp, _vp, _vp, _i64, _int]),
     "fa_bson_elements": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),
     "fa_bson_walk": (_i64, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64]),

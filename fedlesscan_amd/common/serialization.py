@@ -53,6 +53,12 @@ class NpzWeightsSerializer:
     def serialize(self, weights: List[np.ndarray]) -> bytes:
         # not wrapped: only deserialize carries wrap_exceptions_as_serialization_error
         # (serialization.py:292-306), so e.g. serialize(None) raises TypeError
+        if not self.compressed:
+            # byte-identical np.savez with native checksums (fedlesscan_amd/npz.py)
+            from ..npz import write_npz
+            b = write_npz(weights)
+            if b is not None:
+                return b
         with io.BytesIO() as f:
             (np.savez_compressed if self.compressed else np.savez)(f, *weights)
             return f.getvalue()

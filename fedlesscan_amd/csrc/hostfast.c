@@ -14,6 +14,8 @@
  *   int -- returns None and the caller takes the general numpy path
  *   (engine.result_dtype / engine.round_scalars), so results never depend on
  *   whether this module is present.
+ *
+ * alloc_bytes(n) -> (bytes, address): see below.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -54,7 +56,30 @@ general:
     Py_RETURN_NONE;
 }
 
+/* alloc_bytes(n) -> (bytes, address)
+ *   A new, uninitialised bytes object of n bytes and the address of its
+ *   storage, for a native writer to fill (fedlesscan_amd/npz.py write_npz
+ *   assembles the saved model with the threaded fa_pack) before the object is
+ *   handed to anyone else. */
+static PyObject* alloc_bytes(PyObject* self, PyObject* arg) {
+    (void)self;
+    const Py_ssize_t n = PyLong_AsSsize_t(arg);
+    if (n < 0) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "alloc_bytes: negative size");
+        return NULL;
+    }
+    PyObject* b = PyBytes_FromStringAndSize(NULL, n);
+    if (!b) return NULL;
+    PyObject* addr = PyLong_FromVoidPtr((void*)PyBytes_AS_STRING(b));
+    if (!addr) {
+        Py_DECREF(b);
+        return NULL;
+    }
+    return Py_BuildValue("(NN)", b, addr);
+}
+
 static PyMethodDef methods[] = {
+    {"alloc_bytes", alloc_bytes, METH_O, "(uninitialised bytes of n bytes, its storage address)"},
     {"round_weak_f32", round_weak_f32, METH_O,
      "float32 roundings of a sequence of Python bool/int/float as bytes, or None for anything else"},
     {NULL, NULL, 0, NULL},

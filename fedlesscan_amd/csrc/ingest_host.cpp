@@ -157,6 +157,83 @@ class PackPool {
     bool stop_ = false;
 };
 
+// ---- CRC-32 (ISO-HDLC / zlib: reflected polynomial 0xEDB88320) -------------
+// The NPZ writer's member checksum (zipfile computes it with zlib.crc32 over
+// the .npy header and payload).  Slicing-by-16 tables on each thread over its
+// own byte range, then the ranges' CRCs are joined with the GF(2) "shift by
+// n zero bytes" operator (the published zlib crc32_combine method: x^(8n)
+// mod P by repeated squaring), so any thread count gives zlib's value.
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+
+struct CrcTables {
+    uint32_t t[16][256];
+    uint32_t x2n[32];  // x^(2^k) mod P
+    CrcTables() {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+            t[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int s = 1; s < 16; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+        uint32_t p = 1u << 30;  // x^1 (bit 31 is x^0 in the reflected order)
+        x2n[0] = p;
+        for (int k = 1; k < 32; ++k) x2n[k] = p = mult(p, p);
+    }
+    // a * b mod P, polynomials in the reflected bit order
+    static uint32_t mult(uint32_t a, uint32_t b) {
+        uint32_t m = 1u << 31, r = 0;
+        for (;;) {
+            if (a & m) {
+                r ^= b;
+                if ((a & (m - 1)) == 0) break;
+            }
+            m >>= 1;
+            b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+        }
+        return r;
+    }
+    // x^(8n) mod P
+    uint32_t shift_bytes(uint64_t n) const {
+        uint32_t p = 1u << 31;  // x^0
+        int k = 3;              // 8 = 2^3
+        while (n) {
+            if (n & 1) p = mult(x2n[k & 31], p);
+            n >>= 1;
+            ++k;
+        }
+        return p;
+    }
+    // raw register update (no pre/post inversion)
+    uint32_t update(uint32_t c, const uint8_t* p, size_t n) const {
+        while (n && ((uintptr_t)p & 7)) {
+            c = t[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+            --n;
+        }
+        while (n >= 16) {
+            uint32_t w0, w1, w2, w3;
+            memcpy(&w0, p, 4);
+            memcpy(&w1, p + 4, 4);
+            memcpy(&w2, p + 8, 4);
+            memcpy(&w3, p + 12, 4);
+            w0 ^= c;
+            c = t[15][w0 & 0xFF] ^ t[14][(w0 >> 8) & 0xFF] ^ t[13][(w0 >> 16) & 0xFF] ^ t[12][w0 >> 24] ^
+                t[11][w1 & 0xFF] ^ t[10][(w1 >> 8) & 0xFF] ^ t[9][(w1 >> 16) & 0xFF] ^ t[8][w1 >> 24] ^
+                t[7][w2 & 0xFF] ^ t[6][(w2 >> 8) & 0xFF] ^ t[5][(w2 >> 16) & 0xFF] ^ t[4][w2 >> 24] ^
+                t[3][w3 & 0xFF] ^ t[2][(w3 >> 8) & 0xFF] ^ t[1][(w3 >> 16) & 0xFF] ^ t[0][w3 >> 24];
+            p += 16;
+            n -= 16;
+        }
+        while (n--) c = t[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+        return c;
+    }
+};
+
+const CrcTables& crc_tables() {
+    static const CrcTables tables;
+    return tables;
+}
+
 }  // namespace
 
 extern "C" {
@@ -274,6 +351,37 @@ int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, cons
     } catch (...) {  // e.g. thread creation failure: finish on this thread
         for (int t = 0; t < T; ++t) work(t);
     }
+    return FA_OK;
+}
+
+int fa_crc32(const void* data, int64_t n, uint32_t crc_in, int nthreads, uint32_t* crc_out) {
+    if (n < 0 || (n > 0 && !data) || !crc_out) return FA_ERR_ARG;
+    const CrcTables& K = crc_tables();
+    const uint8_t* p = (const uint8_t*)data;
+    int T = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n >> 21));  // >= 2 MiB per thread
+    if (T == 1) {
+        *crc_out = ~K.update(~crc_in, p, (size_t)n);
+        return FA_OK;
+    }
+    // thread t: the raw register over its range starting from 0; range 0 starts from ~crc_in
+    std::vector<uint32_t> part(T, 0);
+    auto work = [&](int t) {
+        const int64_t b0 = n * t / T, b1 = n * (t + 1) / T;
+        part[t] = K.update(t == 0 ? ~crc_in : 0u, p + b0, (size_t)(b1 - b0));
+    };
+    try {
+        PackPool::get().run(T, work);
+    } catch (...) {
+        for (int t = 0; t < T; ++t) work(t);
+    }
+    // register after range t = (register after t-1) * x^(8 len_t) + part[t]  (CRC linearity)
+    uint32_t c = part[0];
+    for (int t = 1; t < T; ++t) {
+        const int64_t len = n * (t + 1) / T - n * t / T;
+        c = CrcTables::mult(K.shift_bytes((uint64_t)len), c) ^ part[t];
+    }
+    *crc_out = ~c;
     return FA_OK;
 }
 

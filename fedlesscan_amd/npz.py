@@ -151,3 +151,120 @@ def read_layers(blob) -> List[np.ndarray]:
     with io.BytesIO(bytes(blob)) as f:
         with np.load(f, allow_pickle=False) as z:
             return [z[k] for k in z.files]
+
+
+# ---------------------------------------------------------------------------
+# writer: byte-identical np.savez(BytesIO, *arrays) for the saved global model
+# ---------------------------------------------------------------------------
+def write_npz(arrays) -> Optional[bytes]:
+    """`np.savez` of `arrays` into memory, byte for byte, with the member
+    checksums computed natively (fa_crc32, threaded) and each payload copied
+    once.
+
+    np.savez (numpy `_savez`) opens member arr_i.npy with
+    `zipfile.ZipFile.open(name, 'w', force_zip64=True)` on a ZIP_STORED,
+    allowZip64 archive and streams the .npy header and the raw C-order data
+    through it; zipfile checksums every write with zlib.crc32 and rewrites the
+    local header at the end.  Here the same ZipInfo fields are filled in
+    directly and written once, and zipfile itself writes the central
+    directory, so the archive layout is zipfile's own.  The reference saves
+    the aggregated model this way (NpzWeightsSerializer.serialize,
+    serialization.py:290-296 -> ParameterDao.save, aggregation.py:139-147).
+
+    Returns None (the caller runs np.savez) for anything numpy writes another
+    way: object dtypes (pickled), arrays that are not C-contiguous, members of
+    4 GiB or more.
+    """
+    from numpy.lib import format as npformat
+    from . import _lib
+
+    arrs = [np.asanyarray(a) for a in arrays]
+    for a in arrs:
+        if a.dtype.hasobject or not a.flags.c_contiguous or a.nbytes >= zipfile.ZIP64_LIMIT:
+            return None
+    L = _lib.load()
+    import ctypes
+    crc = ctypes.c_uint32()
+    parts: list = []  # local header, .npy header, payload for each member; then the directory
+    infos = []
+    offset = 0
+    for i, a in enumerate(arrs):
+        hdr = io.BytesIO()
+        npformat._write_array_header(hdr, npformat.header_data_from_array_1_0(a), None)
+        hdr = hdr.getvalue()
+        data = a.reshape(-1).view(np.uint8) if a.nbytes else np.empty(0, np.uint8)
+        zi = zipfile.ZipInfo("arr_%d.npy" % i)  # as ZipFile.open(name, 'w'): default date_time
+        zi.compress_type = zipfile.ZIP_STORED
+        zi._compresslevel = None
+        zi.flag_bits = 0x00  # seekable output: no data descriptor
+        zi.external_attr = 0o600 << 16
+        zi.file_size = zi.compress_size = len(hdr) + data.nbytes
+        _lib.check(L.fa_crc32(data.ctypes.data if data.nbytes else None, data.nbytes,
+                              zlib_crc32(hdr), 0, ctypes.byref(crc)), "fa_crc32")
+        zi.CRC = crc.value
+        zi.header_offset = offset
+        lh = zi.FileHeader(True)  # force_zip64=True, as np.savez
+        parts += [lh, hdr, data.data]
+        infos.append(zi)
+        offset += len(lh) + len(hdr) + data.nbytes
+    # zipfile writes the central directory and end records itself, to a
+    # stream that reports the archive offsets
+    tail = _OffsetStream(offset)
+    zf = zipfile.ZipFile(tail, mode="w", compression=zipfile.ZIP_STORED, allowZip64=True)
+    for zi in infos:
+        zf.filelist.append(zi)
+        zf.NameToInfo[zi.filename] = zi
+    zf._didModify = True
+    zf.close()
+    parts.append(tail.getvalue())
+    from .engine import _hostfast
+    if _hostfast is None:
+        return b"".join(parts)  # one allocation, each part copied once
+    # one allocation, every part copied once by the threaded fa_pack (the GIL
+    # released) into the new bytes object before anyone else sees it
+    bufs = [np.frombuffer(p_, dtype=np.uint8) for p_ in parts]
+    sizes = np.fromiter((b.nbytes for b in bufs), dtype=np.int64, count=len(bufs))
+    offs = np.zeros(len(bufs), dtype=np.int64)
+    np.cumsum(sizes[:-1], out=offs[1:])
+    total = int(sizes.sum())
+    out, addr = _hostfast.alloc_bytes(total)
+    srcs = np.fromiter((b.ctypes.data if b.nbytes else 0 for b in bufs), dtype=np.uint64, count=len(bufs))
+    _lib.check(L.fa_pack(addr, offs.ctypes.data, srcs.ctypes.data, sizes.ctypes.data, len(bufs), 0), "fa_pack")
+    return out
+
+
+class _OffsetStream(io.RawIOBase):
+    """Writable, seekable stream whose positions start at `base` (the bytes
+    before it are the members, assembled separately)."""
+
+    def __init__(self, base: int):
+        super().__init__()
+        self.base = base
+        self.inner = io.BytesIO()
+
+    def writable(self):
+        return True
+
+    def seekable(self):
+        return True
+
+    def write(self, b):
+        return self.inner.write(b)
+
+    def tell(self):
+        return self.base + self.inner.tell()
+
+    def seek(self, pos, whence=io.SEEK_SET):
+        if whence == io.SEEK_SET:
+            if pos < self.base:
+                raise ValueError("seek before the directory")
+            return self.base + self.inner.seek(pos - self.base)
+        return self.base + self.inner.seek(pos, whence)
+
+    def getvalue(self):
+        return self.inner.getvalue()
+
+
+def zlib_crc32(b: bytes) -> int:
+    import zlib
+    return zlib.crc32(b)

@@ -173,6 +173,12 @@ int fa_npz_index(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* co
  * pinned-staging packer of the ingest pipeline (fedlesscan_amd/ingest.py). */
 int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, const int64_t* sizes, int64_t n,
             int nthreads);
+/* [host] zlib-compatible CRC-32 of data[0..n) continuing crc_in (0 to
+ * start), split over up to nthreads threads (0 = hardware concurrency);
+ * *crc_out = zlib.crc32(data, crc_in).  The member checksum of the NPZ writer
+ * (fedlesscan_amd/npz.py write_npz: the saved round+1 model, aggregation.py
+ * :139-147 -> NpzWeightsSerializer.serialize, serialization.py:290-296). */
+int fa_crc32(const void* data, int64_t n, uint32_t crc_in, int nthreads, uint32_t* crc_out);
 
 /* ---- host-side ingest (no GPU): the persisted BSON document -----------------
  * The reference stores each ClientResult as bson.encode(result.dict()) in

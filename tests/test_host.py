@@ -447,6 +447,56 @@ def test_native_npz_index_survives_corruption():
             assert sum(x.nbytes for x in v) <= len(b)
 
 
+def test_fa_crc32_matches_zlib():
+    """The NPZ writer's checksum: zlib.crc32 for any length, alignment,
+    starting value and thread count (threaded ranges joined by the combine)."""
+    import zlib
+    L = _lib.load()
+    out = ctypes.c_uint32()
+    buf = np.random.default_rng(11).integers(0, 256, size=9_000_000, dtype=np.uint8)
+    for n in (0, 1, 7, 15, 16, 17, 63, 4099, (1 << 21) - 1, (1 << 21) + 5, 4_500_001, 8_999_990):
+        for off in (0, 1, 5):
+            for crc_in in (0, 0x9E3779B9):
+                for T in (1, 3, 16):
+                    v = buf[off:off + n]
+                    assert L.fa_crc32(v.ctypes.data if n else None, n, crc_in, T, ctypes.byref(out)) == 0
+                    assert out.value == zlib.crc32(v.tobytes(), crc_in), (n, off, crc_in, T)
+    assert L.fa_crc32(None, 5, 0, 1, ctypes.byref(out)) == _lib.FA_ERR_ARG
+
+
+def test_npz_writer_is_byte_identical_to_savez():
+    """write_npz (and so NpzWeightsSerializer.serialize, uncompressed) returns
+    exactly np.savez's bytes; layouts numpy writes differently fall back."""
+    from fedlesscan_amd.npz import write_npz
+    rng = np.random.default_rng(12)
+
+    def savez(arrs):
+        f = io.BytesIO()
+        np.savez(f, *arrs)
+        return f.getvalue()
+
+    cases = [
+        [],
+        [np.arange(5, dtype=np.float32)],
+        [rng.random((3, 4)).astype(np.float32), np.ones(()), np.zeros((0, 3), np.float32)],
+        [rng.integers(0, 9, (2, 3, 4)), np.array([True, False]), rng.random(7).astype(np.float16),
+         np.array(5, dtype=np.int32), rng.random(3).astype(">f4")],
+        [np.zeros((2, 2), dtype=[("a", "<f4"), ("b", "<i8")])],
+        [rng.random(n).astype(np.float32) for n in (1, 31, 32, 33, 4096, 1_000_003)],
+        [np.asfortranarray(rng.random((2, 3)))[:, :1].copy()],
+    ]
+    for arrs in cases:
+        assert write_npz(arrs) == savez(arrs), [a.shape for a in arrs]
+        assert NpzWeightsSerializer().serialize(arrs) == savez(arrs)
+    for odd in ([rng.random((3, 5)).T], [np.array([1, "a"], dtype=object)], [rng.random(10)[::2]]):
+        assert write_npz(odd) is None
+        assert NpzWeightsSerializer().serialize(odd) == savez(odd)
+    # and it reads back through both readers
+    arrs = cases[3]
+    blob = write_npz(arrs)
+    assert all(np.array_equal(a, b) for a, b in zip(NpzWeightsSerializer().deserialize(blob), arrs))
+
+
 def test_fa_pack_scatters_ranges():
     L = _lib.load()
     rng = np.random.default_rng(3)
