@@ -17,6 +17,7 @@ computed by libfedavg_hip.so on the GPU, or the call raises.
 """
 from __future__ import annotations
 
+import operator
 import os
 import threading
 from typing import List, Optional, Sequence
@@ -295,7 +296,12 @@ def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Te
     A device-resident simulation usually hands over `X[i]` rows of one stacked
     tensor (or equal-size slices of one buffer): then the stacked fold reads
     them with ldx = pitch, with no pointer table to build and upload and with
-    the narrow-model (LDS-staged) kernels the pointer-list fold lacks."""
+    the narrow-model (LDS-staged) kernels the pointer-list fold lacks.
+
+    Only the first and the last row are asked for their storage: when both lie
+    in one storage, every row between them at the constant pitch lies in that
+    storage's contiguous range too, so the view reads exactly the bytes the
+    rows' own pointers name (as_strided re-checks the bounds)."""
     N = len(rows)
     if N < 2 or P == 0:
         return None
@@ -304,11 +310,13 @@ def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Te
         return None
     if (np.diff(host_ptrs) != step).any():
         return None
-    base = rows[0]
-    sp = base.untyped_storage().data_ptr()
-    if any(r.untyped_storage().data_ptr() != sp for r in rows):
+    base, last = rows[0], rows[-1]
+    if last.untyped_storage().data_ptr() != base.untyped_storage().data_ptr():
         return None
     return base.as_strided((N, P), (step // 4, 1))
+
+
+_dtype_of = operator.attrgetter("dtype")
 
 
 class RowSet:
@@ -327,6 +335,7 @@ class RowSet:
     folds, their storage may not (re-create the RowSet after reallocating)."""
 
     def __init__(self, rows: Sequence[torch.Tensor]):
+        rows = list(rows)
         N = len(rows)
         if N == 0:
             _lib.check(_lib.FA_ERR_NO_CLIENTS, "RowSet")
@@ -334,20 +343,27 @@ class RowSet:
         P, dev, dt = r0.numel(), r0.device, r0.dtype
         if not r0.is_cuda:
             raise ValueError("rows must be CUDA (HIP) tensors")
-        for r in rows:
-            if r.numel() != P or r.dtype != dt or not r.is_contiguous() or r.device != dev:
-                raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
-        self.rows = [r.reshape(-1) for r in rows]
+        # one C-level pass per property (a Python loop over 1024 rows with a
+        # reshape per row cost ~1 ms per call, more than the fold of 1024 x 67K)
+        if (set(map(torch.Tensor.numel, rows)) != {P} or set(map(_dtype_of, rows)) != {dt}
+                or not all(map(torch.Tensor.is_contiguous, rows))
+                or set(map(torch.Tensor.get_device, rows)) != {r0.get_device()}):
+            raise InvalidParameterShapeError("all rows must be contiguous with equal size, dtype, device")
+        self.rows = rows
         self.N, self.P, self.device, self.dtype = N, P, dev, dt
         self.view = None
         self.ptrs = None
         self.aligned = False
         if dt == torch.float32 and P > 0:
-            host_ptrs = np.fromiter(map(torch.Tensor.data_ptr, self.rows), dtype=np.int64, count=N)
-            self.view = _equal_stride_view(self.rows, host_ptrs, P)
+            host_ptrs = np.fromiter(map(torch.Tensor.data_ptr, rows), dtype=np.int64, count=N)
+            self.view = _equal_stride_view(rows, host_ptrs, P)
             if self.view is None:
                 self.ptrs = torch.from_numpy(host_ptrs).to(dev)
                 self.aligned = not (host_ptrs % 16).any()
+
+    def stacked(self) -> torch.Tensor:
+        """The rows copied into one [N, P] tensor (the non-fp32 fallbacks)."""
+        return torch.stack([r.reshape(-1) for r in self.rows])
 
 
 def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
@@ -362,10 +378,10 @@ def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
     fw = Factors.weak_f32(weights, scores, total) if rs.dtype == torch.float32 else None
     if fw is None and (rs.dtype != torch.float32
                        or result_dtype(np.dtype(np.float32), weights, scores, total) != np.float32):
-        return fold_stacked(torch.stack(rs.rows), weights, scores, out=out, total=total)
+        return fold_stacked(rs.stacked(), weights, scores, out=out, total=total)
     if rs.view is not None or rs.P == 0:
         # rows of one allocation at a fixed pitch: the stacked fold, no pointer table
-        X = rs.view if rs.view is not None else torch.stack(rs.rows)
+        X = rs.view if rs.view is not None else rs.stacked()
         return fold_stacked(X, weights, scores, out=out, total=total)
     dev = rs.device
     f = fw or Factors(weights, scores, np.dtype(np.float32), total=total)

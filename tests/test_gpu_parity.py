@@ -407,6 +407,31 @@ def test_rowset_rejects_mixed_rows(dev):
     rs = engine.RowSet([torch.zeros(4, device=dev), torch.zeros(4, device=dev)])
     with pytest.raises(InvalidParameterShapeError):
         engine.fold_rows(rs, [1, 2, 3])
+    with pytest.raises(InvalidParameterShapeError):  # a non-contiguous row
+        engine.RowSet([torch.zeros(4, device=dev), torch.zeros(8, device=dev)[::2]])
+    with pytest.raises(InvalidParameterShapeError):  # a row on the host
+        engine.RowSet([torch.zeros(4, device=dev), torch.zeros(4)])
+
+
+@pytest.mark.parametrize("kind", ["views", "separate", "f64"])
+def test_rowset_multidim_rows(dev, kind):
+    """Rows need not be 1-D: X[i] of an [N, a, b] tensor (the equal-stride
+    view), separately allocated [a, b] tensors (the pointer table) and float64
+    rows (stacked first), each bit-equal to the oracle on the flattened rows."""
+    from fedlesscan_amd import engine
+    N, a, b = 37, 61, 101
+    X = synth.clients_f32(601, N, 0, a * b)
+    w = synth.cardinalities(602, N)
+    if kind == "f64":
+        X = X.astype(np.float64)
+    X3 = torch.from_numpy(X.reshape(N, a, b)).to(dev)
+    rows = [X3[i] for i in range(N)] if kind == "views" else [X3[i].clone() for i in range(N)]
+    rs = engine.RowSet(rows)
+    assert (rs.view is not None) == (kind == "views")
+    got = engine.fold_rows(rs, w).cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w))) if kind != "f64" else \
+        OL.fedavg_f64(X, np.array(w, np.float64), float(sum(w)))
+    assert _bits_equal(got, exp)
 
 
 @pytest.mark.parametrize("N,P", [(1, 8), (5, 9), (64, 8 * 1000 + 3), (256, 65536)])
