@@ -23,6 +23,7 @@
 // Kernel families (fold_f32_auto picks one by shape, pick_f32):
 //   k_fold_f32_gs    grid-stride over 16 KiB column tiles, ~1 block per CU,
 //                    balanced passes, launched per column band (large models)
+//   k_fold_f32_tile  one block per tile, same tile body (few clients)
 //   k_fold_f32_lds   LDS-staged: all waves stream client-row chunks of a
 //                    narrow column tile into LDS, wave 0 folds (narrow models)
 // Everything here sits in an anonymous namespace: each library gets its own
@@ -204,6 +205,16 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
     const float* acc_in, float divisor, float* out, int64_t ntiles) {  // acc_in may alias out
     for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
         fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+}
+
+// One block per tile (few clients: more blocks in flight than the grid-stride
+// form, each with a short row run).
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_tile(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out) {  // acc_in may alias out
+    fold_tile<U, C, NT, SCORED, ACC, FIN, NTS>(blockIdx.x, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
 
 // Narrow models: LDS-staged client rows.
@@ -1266,11 +1277,14 @@ int cu_count() {
 //                                      40-quad tiles by how evenly the blocks fill the CUs
 //                                      (pick_lds_tile)
 //   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   tiles4 < CUs, N < 64 or tiles4 <   one block per 4 KiB tile, 4 rows x 1 quad (few clients:
+//     3/4 of the CUs                   4x the blocks of the grid-stride fold)
+//   N < 24, tiles4 >= CUs              one block per 16 KiB tile, 8 rows x 4 quads
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 4 passes x CUs tiles
 // all with non-temporal output stores.
-enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1293,6 +1307,12 @@ inline F32Pick pick_f32(int64_t N, int64_t P) {
     if (nq < (1 << 16)) return pick_lds_tile(P, cus);
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
+    // few clients: each block's rows are short, so the grid-stride fold's ~one
+    // block per CU keeps too few bytes in flight; a block per tile (4x the
+    // blocks for 4 KiB tiles) was 8-30 % faster at 10-128 x 582K and 10-32 x
+    // 1M, 7-10 % at 10 x 4M-10M with 16 KiB tiles (profiles/r02_small_n/)
+    if (tiles4 < cus && (N < 64 || 4 * tiles4 < 3 * cus)) return F32Pick::kTileC1;
+    if (N < 24 && tiles4 >= cus) return F32Pick::kTileC4;
     if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
     return F32Pick::kGsBalC4;
 }
@@ -1325,6 +1345,28 @@ void launch_gs(hipStream_t st, int per_cu, const float* X, int64_t N, int64_t P,
     }
     hipLaunchKernelGGL((k_fold_f32_gs<U, C, NT, SC, ACC, FIN, NTS, B>), dim3((unsigned)grid), dim3(B), 0, st, X,
                        N, P, ldx, a, s, acc_in, d, out, tiles);
+}
+
+// One block per C*kBlock-quad tile (the column-tail lane's tile included),
+// every (scored, accumulate, finalize) combination.
+template <int U, int C, bool NTS>
+int launch_tile_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    if (tiles > 0x7FFFFFFF) return fail(FA_ERR_ARG, "P=%lld too large for a tile launch", (long long)P);
+    const dim3 grid((unsigned)tiles), block(kBlock);
+#define FA_T(SC, ACC, FIN) \
+    hipLaunchKernelGGL((k_fold_f32_tile<U, C, true, SC, ACC, FIN, NTS>), grid, block, 0, st, X, N, P, ldx, a, s, acc_in, d, out)
+    if (sc) {
+        if (acc) { if (fin) FA_T(true, true, true); else FA_T(true, true, false); }
+        else     { if (fin) FA_T(true, false, true); else FA_T(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_T(false, true, true); else FA_T(false, true, false); }
+        else     { if (fin) FA_T(false, false, true); else FA_T(false, false, false); }
+    }
+#undef FA_T
+    return FA_OK;
 }
 
 // ALLF: instantiate every (scored, accumulate, finalize) combination -- only the
@@ -1505,6 +1547,12 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             break;
         case F32Pick::kLdsW8:
             rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileC1:  // plain stores (non-temporal ones cost 3-10 % here)
+            rc = launch_tile_flags<4, 1, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileC4:
+            rc = launch_tile_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kGsBalC2:
             launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

@@ -398,6 +398,39 @@ def test_lds_tile_picks(dev, lib, N, P):
     assert _bits_equal(acc.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("N,P", [(10, 582026), (63, 262147), (1, 300_000), (30, 1_000_003), (100, 582026),
+                                 (10, 4 * 1024 * 1024 + 5), (23, 1024 * 1024 * 2 + 7)])
+def test_few_client_tile_picks(dev, lib, N, P):
+    """The few-client picks (a block per 4 KiB tile below one tile per CU; a
+    block per 16 KiB tile under 24 clients above it) and their neighbours:
+    plain, stall-aware and a two-part continued fold, bit-exact vs the oracle."""
+    from fedlesscan_amd import engine
+    L = lib.load()
+    X = synth.clients_f32(530 + N, N, 0, P)
+    w = synth.cardinalities(530 + P, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(530, N, 10, 2)]
+    ldx = (P + 63) // 64 * 64  # padded pitch: 16-B aligned rows take the vector picks
+    Xd = torch.full((N, ldx), float("nan"), dtype=torch.float32, device=dev)[:, :P]
+    Xd.copy_(torch.from_numpy(X))
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    exp_s = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    assert _bits_equal(engine.fold_stacked(Xd, w, out=_sentinel(P, dev)).cpu().numpy(), exp)
+    assert _bits_equal(engine.fold_stacked(Xd, w, sc, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
+    Xu = torch.from_numpy(X).to(dev)  # unpadded (odd pitch when P % 4 != 0)
+    assert _bits_equal(engine.fold_stacked(Xu, w, sc, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
+    if N > 1:
+        h = N // 2
+        a = torch.tensor(w, dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        div = float(np.float32(sum(w)))
+        acc = _sentinel(P, dev)
+        lib.check(L.fa_fold_f32(Xd.data_ptr(), h, P, ldx, a.data_ptr(), None, None, div, 0, acc.data_ptr(), st),
+                  "f")
+        lib.check(L.fa_fold_f32(Xd[h].data_ptr(), N - h, P, ldx, a[h:].data_ptr(), None, acc.data_ptr(), div, 1,
+                                acc.data_ptr(), st), "f")
+        assert _bits_equal(acc.cpu().numpy(), exp)
+
+
 def test_rowset_rejects_mixed_rows(dev):
     from fedlesscan_amd import InvalidParameterShapeError, engine
     with pytest.raises(InvalidParameterShapeError):
