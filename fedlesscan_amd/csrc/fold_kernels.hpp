@@ -1282,7 +1282,7 @@ int cu_count() {
 //   N < 24, tiles4 >= CUs              one block per 16 KiB tile, 8 rows x 4 quads
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
-//                                      in column bands of <= 4 passes x CUs tiles
+//                                      in column bands of <= 3 passes x CUs tiles
 // all with non-temporal output stores.
 enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
@@ -1557,8 +1557,9 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
         case F32Pick::kGsBalC2:
             launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
-        default:  // one band below 4 x CUs tiles
-            launch_gs_bands<8, 4, true, true>(st, 4, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+        default:  // one band below 3 x CUs tiles; 3-pass bands were 0.3-1 % faster than
+                  // 4-pass ones at 512-1024 clients (profiles/r02_bands/)
+            launch_gs_bands<8, 4, true, true>(st, 3, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
     }
     if (rc) return rc;

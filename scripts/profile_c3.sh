@@ -8,6 +8,7 @@
 set -euo pipefail
 TAG=${1:-r02}
 COMMIT=${2:-unknown}
+# DPC: band dispatches per fold call (C3 with 3-pass bands: 4)
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
@@ -21,7 +22,7 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_
     python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/write.err"
 cd "$ROOT"
 python3 scripts/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" \
-    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --dispatches-per-call 3 \
+    --kernel "k_fold_f32_gs<8, 4, true" --bytes 41000000000 --dispatches-per-call "${DPC:-4}" \
     --provenance "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (C3), round $TAG, commit $COMMIT, $(date -u +%Y-%m-%dT%H:%MZ)" \
     --out "$OUT/pmc_c3.json"
 echo done
