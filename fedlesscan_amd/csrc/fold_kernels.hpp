@@ -1584,9 +1584,11 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
         return check_launch("k_fedavg_bf16_scalar");
     }
     if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
-        // per-GPU C4 buckets (256 x 12.5M): grid-stride, 8 rows x 2 octets,
-        // one block per CU: +7 % over the row-streaming pick
-        launch_bf16_gs<8, 2>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+        // per-GPU C4 buckets (256 x 12.5M) and their multi-GPU round slots
+        // (256 x 3.125M): grid-stride, 8 rows x 2 octets, balanced passes in
+        // column bands of 4 passes: +7 % over the row-streaming pick (DESIGN.md
+        // 5), +1-1.4 % over one block per CU (profiles/r02_slots/)
+        launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
     } else if ((P >> 3) >= ((int64_t)1 << 22)) {
         // whole large models (C4's 100M on one GPU): balanced grid-stride
         // launches over 32 KiB tiles (fewer tile switches per block), in
