@@ -164,8 +164,11 @@ constexpr const char* kVariants[] = {
     // the per-column scalar fold the product used for such input in round 2
     "dw_lds4_w2r32t16", "dw_lds2_w4r32t24", "dw_lds2_w4r16t32", "dw_lds2_w4r32t40", "dw_lds2_w8r32t32",
     "dw_lds2_w4r64t32", "dw_lds3_w8r32t32", "scalar",
+    // one block per tile (the product's few-client form, k_fold_f32_tile), more rows or quads per lane
+    "tile_u8c1", "tile_u16c1", "tile_u8c2", "tile_u4c2", "tile_u8c1_nts", "tile_u4c1",
 };
-constexpr int kFirstAnyAlign = 84;  // variants from here on take any 4-B aligned layout
+constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
+constexpr int kEndAnyAlign = 92;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // Quads per lane of the round-1 row-streaming policy (variant "v4_pickq_nts"):
@@ -261,7 +264,7 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     // unaligned layouts take the product's fold, except the any-alignment variants
-    if (variant < kFirstAnyAlign && (!aligned16(X) || (ldx % 4) || !aligned16(out)))
+    if ((variant < kFirstAnyAlign || variant >= kEndAnyAlign) && (!aligned16(X) || (ldx % 4) || !aligned16(out)))
         return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream);
     hipStream_t st = (hipStream_t)stream;
     const bool sc = s != nullptr, acc = false, fin = true;
@@ -390,6 +393,14 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
             if (sc) launch_scalar<true, false, true>(st, X, N, P, ldx, a, s, acc_in, divisor, out);
             else launch_scalar<false, false, true>(st, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
+#define FA_VT(U, C, NTS) launch_tile_flags<U, C, NTS>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 92: rc = FA_VT(8, 1, false); break;
+        case 93: rc = FA_VT(16, 1, false); break;
+        case 94: rc = FA_VT(8, 2, false); break;
+        case 95: rc = FA_VT(4, 2, false); break;
+        case 96: rc = FA_VT(8, 1, true); break;
+        case 97: rc = FA_VT(4, 1, false); break;
+#undef FA_VT
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
