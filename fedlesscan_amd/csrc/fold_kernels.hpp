@@ -1276,15 +1276,18 @@ int cu_count() {
 //   32K <= P < 256K                    LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
 //                                      40-quad tiles by how evenly the blocks fill the CUs
 //                                      (pick_lds_tile)
-//   N >= 256, tiles4 < 3/4 of the CUs  LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
-//   tiles4 < CUs, N < 64 or tiles4 <   one block per 4 KiB tile, 4 rows x 1 quad (few clients:
-//     3/4 of the CUs                   4x the blocks of the grid-stride fold)
+//   N >= 256, tiles4 < 0.7 x CUs       LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
+//   48 <= N < 112, tiles4 < 3/5 CUs    one lane per column (k_fold_f32_scalar); 48 <= N < 80:
+//                                      up to 0.9 x CUs
+//   tiles4 < 0.7 x CUs (0.9 x CUs for  one block per 4 KiB tile, 4 rows x 1 quad (4x the
+//     N < 112, 1 x CUs for N < 64)     blocks of the grid-stride fold)
+//   N >= 112, 0.7-0.9 x CUs            grid-stride, balanced passes, 8 rows x 2 quads
 //   N < 24, tiles4 >= CUs              one block per 16 KiB tile, 8 rows x 4 quads
 //   CUs < tiles4 < 2 x CUs             grid-stride, balanced passes, 8 rows x 2 quads
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
-// all with non-temporal output stores.
-enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+// with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
+enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1306,12 +1309,27 @@ inline F32Pick pick_f32(int64_t N, int64_t P) {
     if (nq < (1 << 13)) return F32Pick::kLdsW2T16;
     if (nq < (1 << 16)) return pick_lds_tile(P, cus);
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
-    if (N >= 256 && 4 * tiles4 < 3 * cus) return F32Pick::kLdsW8;
-    // few clients: each block's rows are short, so the grid-stride fold's ~one
-    // block per CU keeps too few bytes in flight; a block per tile (4x the
-    // blocks for 4 KiB tiles) was 8-30 % faster at 10-128 x 582K and 10-32 x
-    // 1M, 7-10 % at 10 x 4M-10M with 16 KiB tiles (profiles/r02_small_n/)
-    if (tiles4 < cus && (N < 64 || 4 * tiles4 < 3 * cus)) return F32Pick::kTileC1;
+    // fewer 16 KiB column tiles than ~0.7 (0.9) x CUs: the grid-stride fold
+    // would leave CUs idle; the picks below spread the columns over more blocks
+    const bool under = 10 * tiles4 < 7 * cus, mid = 10 * tiles4 < 9 * cus;
+    if (N >= 256 && under) return F32Pick::kLdsW8;
+    // Between 0.7 and 0.9 tiles per CU every form swings by up to 25 % with the
+    // row pitch (1024 x 700K-1M in 10-40K steps, profiles/r02_small_n/pitch_scan*);
+    // the picks there minimise the mean and worst ratio to the best form over
+    // 32 measured shapes (grid_v4, grid_v5, pitch_scan2).
+    // One lane per column (4x the waves of the tile form): 48-111 clients below
+    // 3/5 of a tile per CU (4-9 % faster at 50-100 x 300K-582K), 48-79 clients
+    // up to 0.9 tiles per CU (64 x 300K-860K: best or tied at every size).
+    if (N >= 48 && N < 112 && (5 * tiles4 < 3 * cus || (N < 80 && mid))) return F32Pick::kColumn;
+    // One block per 4 KiB tile: each block's rows are short with few clients,
+    // so ~one grid-stride block per CU keeps too few bytes in flight (8-30 %
+    // faster at 10-128 x 582K and 10-32 x 1M, profiles/r02_small_n/).
+    if (under || (N < 112 && mid) || (N < 64 && tiles4 < cus)) return F32Pick::kTileC1;
+    // 112+ clients at 0.7-0.9 tiles per CU: balanced passes over 8 KiB tiles
+    // (within 8 % of the best form at every measured pitch)
+    if (mid) return F32Pick::kGsBalC2;
+    // under 24 clients above one tile per CU: one block per 16 KiB tile (7-10 %
+    // at 10 x 4M-10M)
     if (N < 24 && tiles4 >= cus) return F32Pick::kTileC4;
     if (tiles4 > cus && tiles4 < 2 * cus) return F32Pick::kGsBalC2;
     return F32Pick::kGsBalC4;
@@ -1547,6 +1565,17 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             break;
         case F32Pick::kLdsW8:
             rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kColumn:
+#define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
+            if (sc) {
+                if (acc) { if (fin) FA_SC(true, true, true); else FA_SC(true, true, false); }
+                else     { if (fin) FA_SC(true, false, true); else FA_SC(true, false, false); }
+            } else {
+                if (acc) { if (fin) FA_SC(false, true, true); else FA_SC(false, true, false); }
+                else     { if (fin) FA_SC(false, false, true); else FA_SC(false, false, false); }
+            }
+#undef FA_SC
             break;
         case F32Pick::kTileC1:  // plain stores (non-temporal ones cost 3-10 % here)
             rc = launch_tile_flags<4, 1, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

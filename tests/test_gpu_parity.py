@@ -398,12 +398,14 @@ def test_lds_tile_picks(dev, lib, N, P):
     assert _bits_equal(acc.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("N,P", [(10, 582026), (63, 262147), (1, 300_000), (30, 1_000_003), (100, 582026),
+@pytest.mark.parametrize("N,P", [(10, 582026), (47, 262147), (1, 300_000), (30, 1_000_003), (100, 582026),
+                                 (48, 262147), (111, 700_001), (112, 582026), (64, 300_001),
                                  (10, 4 * 1024 * 1024 + 5), (23, 1024 * 1024 * 2 + 7)])
 def test_few_client_tile_picks(dev, lib, N, P):
-    """The few-client picks (a block per 4 KiB tile below one tile per CU; a
-    block per 16 KiB tile under 24 clients above it) and their neighbours:
-    plain, stall-aware and a two-part continued fold, bit-exact vs the oracle."""
+    """The few-client picks (a block per 4 KiB tile below one tile per CU; one
+    lane per column at 48-111 clients below 3/4 of a tile per CU; a block per
+    16 KiB tile under 24 clients above it) and their neighbours: plain,
+    stall-aware and a two-part continued fold, bit-exact vs the oracle."""
     from fedlesscan_amd import engine
     L = lib.load()
     X = synth.clients_f32(530 + N, N, 0, P)
