@@ -1273,9 +1273,10 @@ int cu_count() {
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
 //   P < 32K params                     LDS-staged, 2 waves, 32-row chunks of 16-quad tiles,
 //                                      four chunks in flight per block
-//   32K <= P < 256K                    LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
+//   32K <= P < 80K                     LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
 //                                      40-quad tiles by how evenly the blocks fill the CUs
 //                                      (pick_lds_tile)
+//   80K <= P < 256K                    LDS-staged, 2 waves, two 16-row chunks of 32-quad tiles
 //   N >= 256, tiles4 < 0.7 x CUs       LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   48 <= N < 112, tiles4 < 3/5 CUs    one lane per column (k_fold_f32_scalar); 48 <= N < 80:
 //                                      up to 0.9 x CUs
@@ -1287,7 +1288,7 @@ int cu_count() {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
-enum class F32Pick { kLdsW2T16, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW2T32, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1307,6 +1308,10 @@ inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
 inline F32Pick pick_f32(int64_t N, int64_t P) {
     const int64_t nq = P >> 2, cus = cu_count();
     if (nq < (1 << 13)) return F32Pick::kLdsW2T16;
+    // 80K-256K params: two-wave blocks over 32-quad tiles, 16-row chunks: best
+    // or within 5 % at 100-1024 clients x 82K-246K, where the 4-wave CU-fill
+    // pick lost up to 24 % (131,136 params; profiles/r02_lds/range_32k_256k/)
+    if (nq >= 20480 && nq < (1 << 16)) return F32Pick::kLdsW2T32;
     if (nq < (1 << 16)) return pick_lds_tile(P, cus);
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     // fewer 16 KiB column tiles than ~0.7 (0.9) x CUs: the grid-stride fold
@@ -1553,6 +1558,9 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
             // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
             rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW2T32:
+            rc = launch_lds_flags<2, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW4T24:
             rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

@@ -369,7 +369,7 @@ def test_ptrs_any_alignment(dev, lib, N, P):
     assert _bits_equal(engine.fold_rows(rs, wr, scr, out=_sentinel(P, dev)).cpu().numpy(), exp_s)
 
 
-@pytest.mark.parametrize("P", [67267, 131072, 200001, 40003])  # 24-, 32-, 40-, 40-quad tiles (pick_lds_tile)
+@pytest.mark.parametrize("P", [67267, 32768, 40003, 131072, 200001, 81920])  # 4-wave 24/32/40-quad tiles, 2-wave 32
 @pytest.mark.parametrize("N", [70, 257])
 def test_lds_tile_picks(dev, lib, N, P):
     """Each column tile the auto policy picks for 32K-256K params: stacked and
