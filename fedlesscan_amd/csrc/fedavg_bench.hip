@@ -421,6 +421,10 @@ extern "C" {
 
 const char* fa_bench_last_error(void) { return g_err; }
 int fa_num_variants(void) { return kNumVariants; }
+const char* fa_f32_pick_name(int64_t N, int64_t P, int64_t cus) {
+    if (N < 1 || P < 1) return "";
+    return f32_pick_name(pick_f32(N, P, cus));
+}
 const char* fa_variant_name(int variant) {
     return (variant >= 0 && variant < kNumVariants) ? kVariants[variant] : "";
 }

@@ -1289,6 +1289,22 @@ int cu_count() {
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
 enum class F32Pick { kLdsW2T16, kLdsW2T32, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+inline const char* f32_pick_name(F32Pick p) {
+    switch (p) {
+        case F32Pick::kLdsW2T16: return "lds_w2_t16";
+        case F32Pick::kLdsW2T32: return "lds_w2_t32";
+        case F32Pick::kLdsW4T24: return "lds_w4_t24";
+        case F32Pick::kLdsW4T32: return "lds_w4_t32";
+        case F32Pick::kLdsW4T40: return "lds_w4_t40";
+        case F32Pick::kLdsW8: return "lds_w8_t32";
+        case F32Pick::kColumn: return "column";
+        case F32Pick::kTileC1: return "tile_4k";
+        case F32Pick::kTileC4: return "tile_16k";
+        case F32Pick::kGsBalC2: return "gs_bal_8k";
+        case F32Pick::kGsBalC4: return "gs_bands_16k";
+    }
+    return "";
+}
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1305,8 +1321,8 @@ inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
     return w24 <= w40 ? F32Pick::kLdsW4T24 : F32Pick::kLdsW4T40;
 }
 
-inline F32Pick pick_f32(int64_t N, int64_t P) {
-    const int64_t nq = P >> 2, cus = cu_count();
+inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
+    const int64_t nq = P >> 2, cus = cus_override > 0 ? cus_override : cu_count();
     if (nq < (1 << 13)) return F32Pick::kLdsW2T16;
     // 80K-256K params: two-wave blocks over 32-quad tiles, 16-row chunks: best
     // or within 5 % at 100-1024 clients x 82K-246K, where the 4-wave CU-fill

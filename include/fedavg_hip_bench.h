@@ -40,6 +40,10 @@ int fa_fedavg_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx,
 int fa_num_variants(void);
 /* [host] short name of a variant, e.g. "gsband4_u8c4nt_nts"; "" if out of range. */
 const char* fa_variant_name(int variant);
+/* [host, no GPU needed] the kernel form the product's fp32 auto fold picks for
+ * N clients x P params (16-B aligned rows) on a GPU with `cus` compute units
+ * (<= 0: the current device's), e.g. "tile_4k", "gs_bands_16k"; "" if N or P < 1. */
+const char* fa_f32_pick_name(int64_t N, int64_t P, int64_t cus);
 /* Same for the bf16 fold (variant 0 = fa_fedavg_bf16). */
 int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                            const float* a, const float* s, float divisor,

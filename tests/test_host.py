@@ -63,6 +63,39 @@ def test_library_variant_table():
     assert L.fa_variant_name(n) == b""
 
 
+# The fp32 auto fold's kernel form by shape on a 256-CU MI355X:
+# the BASELINE configs and the shapes whose sweeps set each boundary.
+_PICKS = [
+    ((1024, 10_000_000), "gs_bands_16k"),  # C3 (headline)
+    ((100, 1_000_000), "gs_bands_16k"),    # C2: 245 of 256 CUs get a tile
+    ((512, 25_000_000), "gs_bands_16k"),   # C5
+    ((256, 12_500_000), "gs_bands_16k"),   # a C4 bucket as fp32
+    ((10, 582_026), "tile_4k"),            # C1 (config 1's MNIST CNN)
+    ((32, 1_000_000), "tile_4k"),          # < 64 clients below one tile per CU
+    ((200, 600_000), "tile_4k"),           # < 0.7 tiles per CU
+    ((100, 582_026), "column"),            # 48-111 clients, < 0.6 tiles per CU
+    ((64, 786_000), "column"),             # 48-79 clients, < 0.9 tiles per CU
+    ((100, 786_000), "tile_4k"),           # 80-111 clients at 0.7-0.9
+    ((1024, 786_000), "gs_bal_8k"),        # 112+ clients at 0.7-0.9
+    ((100, 1_500_000), "gs_bal_8k"),       # 1-2 tiles per CU
+    ((1024, 582_026), "lds_w8_t32"),       # 256+ clients below 0.7
+    ((10, 10_000_000), "tile_16k"),        # < 24 clients above one tile per CU
+    ((1024, 16_384), "lds_w2_t16"),        # < 32K params
+    ((1024, 67_267), "lds_w4_t24"),        # 32K-80K: CU-fill tile
+    ((1024, 32_768), "lds_w4_t32"),
+    ((1024, 40_003), "lds_w4_t40"),
+    ((1024, 131_072), "lds_w2_t32"),       # 80K-256K
+]
+
+
+@pytest.mark.parametrize("shape,pick", _PICKS)
+def test_f32_auto_pick_table(shape, pick):
+    B = _lib.load_bench()
+    N, P = shape
+    assert B.fa_f32_pick_name(N, P, 256).decode() == pick
+    assert B.fa_f32_pick_name(0, P, 256) == b""
+
+
 def test_library_argument_errors_need_no_gpu():
     L = _lib.load()
     # validation happens before any HIP call
