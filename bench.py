@@ -416,6 +416,9 @@ def main():
                 "rounds": rounds,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
+                # the kernel form the product's fp32 auto fold takes for one launch of this rank
+                "fold_form": (B.fa_f32_pick_name(wl.N, lay.sub, 0).decode()
+                              if wl.dtype == "f32" and args.variant == 0 and not args.unpadded else None),
             },
             "roofline": {
                 "bound": "hbm",
