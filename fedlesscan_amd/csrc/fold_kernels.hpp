@@ -1273,9 +1273,9 @@ int cu_count() {
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
 //   P < 32K params                     LDS-staged, 2 waves, 32-row chunks of 16-quad tiles,
 //                                      four chunks in flight per block
-//   32K <= P < 80K                     LDS-staged, 4 waves, two chunks in flight, 24-, 32- or
-//                                      40-quad tiles by how evenly the blocks fill the CUs
-//                                      (pick_lds_tile)
+//   32K <= P < 80K                     LDS-staged, two chunks in flight: 4 waves over 24- or
+//                                      40-quad tiles, or 2 waves over 16-quad tiles where
+//                                      32-quad ones would fill the CUs best (pick_lds_tile)
 //   80K <= P < 256K                    LDS-staged, 2 waves, two 16-row chunks of 32-quad tiles
 //   N >= 256, tiles4 < 0.7 x CUs       LDS-staged, 8 waves, 64-row chunks, 32-quad tiles
 //   48 <= N < 112, tiles4 < 3/5 CUs    one lane per column (k_fold_f32_scalar); 48 <= N < 80:
@@ -1288,10 +1288,11 @@ int cu_count() {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
-enum class F32Pick { kLdsW2T16, kLdsW2T32, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
         case F32Pick::kLdsW2T16: return "lds_w2_t16";
+        case F32Pick::kLdsW2T16D2: return "lds_w2_t16_d2";
         case F32Pick::kLdsW2T32: return "lds_w2_t32";
         case F32Pick::kLdsW4T24: return "lds_w4_t24";
         case F32Pick::kLdsW4T32: return "lds_w4_t32";
@@ -1317,7 +1318,10 @@ inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
         return (double)(((b + cus - 1) / cus) * cus) / (double)b;
     };
     const double w24 = waste(24), w32 = waste(32), w40 = waste(40);
-    if (w32 <= w24 && w32 <= w40) return F32Pick::kLdsW4T32;
+    // where 32-quad tiles fill the CUs best, two-wave blocks over 16-quad tiles
+    // (twice the blocks, same waves per CU) instead: the 4-wave 32-quad form
+    // ran 10-60 % behind at 256-1024 x 32K/57K/65K (profiles/r02_lds/range_32k_256k/)
+    if (w32 <= w24 && w32 <= w40) return F32Pick::kLdsW2T16D2;
     return w24 <= w40 ? F32Pick::kLdsW4T24 : F32Pick::kLdsW4T40;
 }
 
@@ -1574,6 +1578,9 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
             // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
             rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW2T16D2:
+            rc = launch_lds_flags<2, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW2T32:
             rc = launch_lds_flags<2, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
