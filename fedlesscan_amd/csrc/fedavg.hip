@@ -180,6 +180,13 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     if (pk == F32Pick::kLdsW2T16)  // as the stacked pick, with the pointer ring (LOPT 4)
         rc = launch_lds_flags<2, 32, 16, 4, false, true, true, 4>(st, s != nullptr, false, true, (const float*)xi, N,
                                                                   P, P, a, s, nullptr, divisor, out);
+    else if (pk == F32Pick::kLdsW2T16D2)  // two-wave 16-quad tiles, as the stacked pick (1.2-1.6x over the
+                                          // 4-wave 32-quad table fold at 32K-65K, profiles/r02_lds/ptrs_two_wave/)
+        rc = launch_lds_flags<2, 32, 16, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
+    else if (pk == F32Pick::kLdsW2T32)  // two-wave 32-quad tiles, as the stacked pick
+        rc = launch_lds_flags<2, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
+                                                         s, nullptr, divisor, out);
     else if (pk == F32Pick::kLdsW4T24)
         rc = launch_lds_flags<4, 32, 24, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
                                                          s, nullptr, divisor, out);

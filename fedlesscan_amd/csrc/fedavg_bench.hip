@@ -196,6 +196,8 @@ constexpr const char* kPtrsVariants[] = {
     "ptrs_o0_w2t16d4", "ptrs_o4_w2t16d4", "ptrs_o0_w8r64t32",
     // any row alignment (4-byte loads / lane = column / the round-2 generic kernel)
     "ptrs_dw_w2t16d4", "ptrs_dw_t40", "ptrs_dw_t32", "ptrs_dw_t24", "ptrs_rows_scalar", "ptrs_generic",
+    // two-wave forms of the stacked fold's 32K-256K picks (16-B aligned rows again)
+    "ptrs_o0_w2t32", "ptrs_o4_w2t32", "ptrs_o0_w2t16d2", "ptrs_o4_w2t16d2",
 };
 constexpr int kNumPtrsVariants = sizeof(kPtrsVariants) / sizeof(kPtrsVariants[0]);
 
@@ -479,7 +481,7 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
     int rc = check_common(N, P, P, xi, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
-    if (variant < 14 && !aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
+    if ((variant < 14 || variant >= 20) && !aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
     hipStream_t st = (hipStream_t)stream;
     const float* X = (const float*)xi;
     const bool sc = s != nullptr;
@@ -522,6 +524,10 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
             else hipLaunchKernelGGL((k_fedavg_f32_ptrs<8, false>), grid_for((P + 3) / 4), dim3(kBlock), 0, st, xi,
                                     N, P, a, s, divisor, out);
             break;
+        case 20: rc = FA_PW(2, 16, 32, 2, 0); break;
+        case 21: rc = FA_PW(2, 16, 32, 2, 4); break;
+        case 22: rc = FA_PW(2, 32, 16, 2, 0); break;
+        case 23: rc = FA_PW(2, 32, 16, 2, 4); break;
         default: return fail(FA_ERR_ARG, "unknown pointer variant %d", variant);
     }
 #undef FA_PV
