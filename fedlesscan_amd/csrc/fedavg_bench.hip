@@ -188,6 +188,7 @@ constexpr const char* kBf16Variants[] = {
     "bf16gs1u8c2", "bf16gs1u8c4", "bf16gsbalu8c2", "bf16gsbalu2c8",
     // column bands of <k> passes
     "bf16band2u2c8", "bf16band4u2c8", "bf16band4u8c2",
+    "bf16band4u16c2", "bf16band4u8c4", "bf16band4u4c4", "bf16band3u8c2", "bf16band4u16c1",
 };
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 constexpr const char* kPtrsVariants[] = {
@@ -468,7 +469,12 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
         case 7: launch_bf16_gs<2, 8>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case 8: launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case 9: launch_bf16_bands<2, 8>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
-        default: launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 10: launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 11: launch_bf16_bands<16, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 12: launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 13: launch_bf16_bands<4, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case 14: launch_bf16_bands<8, 2>(st, 3, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        default: launch_bf16_bands<16, 1>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
     }
 #undef FA_BF
     return check_launch("fedavg_bf16_variant");
