@@ -190,9 +190,6 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     else if (pk == F32Pick::kLdsW4T24)
         rc = launch_lds_flags<4, 32, 24, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
                                                          s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW4T32)
-        rc = launch_lds_flags<4, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
     else if (pk == F32Pick::kLdsW4T40)
         rc = launch_lds_flags<4, 32, 40, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
                                                          s, nullptr, divisor, out);

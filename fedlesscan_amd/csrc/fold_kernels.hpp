@@ -1288,14 +1288,13 @@ int cu_count() {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
-enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T32, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
         case F32Pick::kLdsW2T16: return "lds_w2_t16";
         case F32Pick::kLdsW2T16D2: return "lds_w2_t16_d2";
         case F32Pick::kLdsW2T32: return "lds_w2_t32";
         case F32Pick::kLdsW4T24: return "lds_w4_t24";
-        case F32Pick::kLdsW4T32: return "lds_w4_t32";
         case F32Pick::kLdsW4T40: return "lds_w4_t40";
         case F32Pick::kLdsW8: return "lds_w8_t32";
         case F32Pick::kColumn: return "column";
@@ -1587,9 +1586,6 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             break;
         case F32Pick::kLdsW4T24:
             rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW4T32:
-            rc = launch_lds_flags<4, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kLdsW4T40:
             rc = launch_lds_flags<4, 32, 40, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
