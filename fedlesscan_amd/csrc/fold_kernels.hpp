@@ -1326,7 +1326,9 @@ inline F32Pick pick_lds_tile(int64_t P, int64_t cus) {
 
 inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
     const int64_t nq = P >> 2, cus = cus_override > 0 ? cus_override : cu_count();
-    if (nq < (1 << 13)) return F32Pick::kLdsW2T16;
+    // up to 32K params (32,768 included: 1.23x faster than the CU-fill pick at
+    // 1024 clients, profiles/r02_lds/range_32k_80k_after/)
+    if (nq <= (1 << 13)) return F32Pick::kLdsW2T16;
     // 80K-256K params: two-wave blocks over 32-quad tiles, 16-row chunks: best
     // or within 5 % at 100-1024 clients x 82K-246K, where the 4-wave CU-fill
     // pick lost up to 24 % (131,136 params; profiles/r02_lds/range_32k_256k/)

@@ -82,7 +82,8 @@ _PICKS = [
     ((10, 10_000_000), "tile_16k"),        # < 24 clients above one tile per CU
     ((1024, 16_384), "lds_w2_t16"),        # < 32K params
     ((1024, 67_267), "lds_w4_t24"),        # 32K-80K: CU-fill tile
-    ((1024, 32_768), "lds_w2_t16_d2"),
+    ((1024, 32_768), "lds_w2_t16"),
+    ((1024, 32_772), "lds_w4_t40"),
     ((1024, 65_536), "lds_w2_t16_d2"),
     ((256, 57_344), "lds_w2_t16_d2"),
     ((1024, 40_003), "lds_w4_t40"),
