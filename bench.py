@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--unpadded", action="store_true",
                     help="row pitch = the model size exactly (experiments: odd sizes give rows that are not 16-B "
                          "aligned, as a torch.stack of such a model)")
+    ap.add_argument("--pitch-extra", type=int, default=0,
+                    help="extra row padding in elements on top of the layout's (row-pitch experiments)")
     ap.add_argument("--cpu-cols", type=int, default=1 << 21, help="columns in the CPU baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=8)
     ap.add_argument("--clients", type=int, default=0, help="override the config's client count (experiments)")
@@ -109,7 +111,7 @@ class Workload:
     slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
     With rounds=1 that is one contiguous bucket per rank."""
 
-    def __init__(self, cfg, rank, world, dev, rounds, align=None):
+    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
         self.layout = (SlotLayout(self.P_total, world, rounds) if align is None
@@ -121,12 +123,13 @@ class Workload:
         st = torch.cuda.current_stream(dev).cuda_stream
         tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
         sub, W = self.layout.sub, self.layout.local_width
-        self.X = torch.zeros((self.N, W), dtype=tdt, device=dev)
+        self.ldx = W + pitch_extra  # row pitch (elements): the slots side by side, plus any extra padding
+        self.X = torch.zeros((self.N, self.ldx), dtype=tdt, device=dev)
         gen = B.fa_synth_f32 if self.dtype == "f32" else B.fa_synth_bf16
         esz = self.X.element_size()
         for k, (lo, hi) in enumerate(self.slots):
             if hi > lo:
-                _lib.check(gen(self.X.data_ptr() + k * sub * esz, self.N, hi - lo, W, self.seed, 0, lo, st),
+                _lib.check(gen(self.X.data_ptr() + k * sub * esz, self.N, hi - lo, self.ldx, self.seed, 0, lo, st),
                            "synth", bench=True)
         self.col0 = self.slots[0][0]
         self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
@@ -158,16 +161,16 @@ class Workload:
         ob = None if self.out_bf16 is None else self.out_bf16.data_ptr() + k * sub * 2
         bench = variant > 0
         if self.dtype == "f32" and variant < 0:  # opt-in split-client fold
-            rc = L.fa_fedavg_f32_splitn(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st)
+            rc = L.fa_fedavg_f32_splitn(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o, st)
         elif self.dtype == "f32" and variant == 0:
-            rc = L.fa_fedavg_f32(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st)
+            rc = L.fa_fedavg_f32(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o, st)
         elif self.dtype == "f32":
-            rc = _lib.load_bench().fa_fedavg_f32_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, st,
+            rc = _lib.load_bench().fa_fedavg_f32_variant(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o, st,
                                                          variant)
         elif variant == 0:
-            rc = L.fa_fedavg_bf16(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o, ob, st)
+            rc = L.fa_fedavg_bf16(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o, ob, st)
         else:
-            rc = _lib.load_bench().fa_fedavg_bf16_variant(x, self.N, sub, W, self.a.data_ptr(), s, self.div, o,
+            rc = _lib.load_bench().fa_fedavg_bf16_variant(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o,
                                                           ob, st, variant)
         if rc:
             _lib.check(rc, "fold", bench=bench)
@@ -251,7 +254,7 @@ def main():
     rounds = args.rounds or (1 if world == 1 else 4)
     if args.splitn:
         args.variant = -1
-    wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None)
+    wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra)
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
@@ -411,6 +414,7 @@ def main():
                 "params_per_gpu": wl.P,
                 "params_total": wl.P_total,
                 "layout": f"row-stacked [clients][params] {'fp32' if wl.dtype == 'f32' else 'bf16'} in HBM",
+                "row_pitch": wl.ldx,
                 "parallelism": f"param-bucket x{world}" + (
                     f" + RCCL all_gather in {rounds} rounds overlapped with the fold" if world > 1 else ""),
                 "rounds": rounds,
