@@ -1340,7 +1340,8 @@ inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
     const bool under = 10 * tiles4 < 7 * cus, mid = 10 * tiles4 < 9 * cus;
     if (N >= 256 && under) return F32Pick::kLdsW8;
     // Between 0.7 and 0.9 tiles per CU every form swings by up to 25 % with the
-    // row pitch (1024 x 700K-1M in 10-40K steps, profiles/r02_small_n/pitch_scan*);
+    // model size (1024 x 700K-1M in 10-40K steps, profiles/r02_small_n/pitch_scan*;
+    // extra row padding changes nothing, pitch_pad/);
     // the picks there minimise the mean and worst ratio to the best form over
     // 32 measured shapes (grid_v4, grid_v5, pitch_scan2).
     // One lane per column (4x the waves of the tile form): 48-111 clients below
@@ -1352,7 +1353,7 @@ inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
     // faster at 10-128 x 582K and 10-32 x 1M, profiles/r02_small_n/).
     if (under || (N < 112 && mid) || (N < 64 && tiles4 < cus)) return F32Pick::kTileC1;
     // 112+ clients at 0.7-0.9 tiles per CU: balanced passes over 8 KiB tiles
-    // (within 8 % of the best form at every measured pitch)
+    // (within 8 % of the best form at every measured size)
     if (mid) return F32Pick::kGsBalC2;
     // under 24 clients above one tile per CU: one block per 16 KiB tile (7-10 %
     // at 10 x 4M-10M)
