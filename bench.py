@@ -10,9 +10,15 @@ c4), plus, at world size > 1, the RCCL all-gather of every rank's output
 bucket over xGMI (the one real exchange step of the path: SURVEY 8e).
 
 Default workload = BASELINE config 3: 1024 clients x 10,000,000 fp32 params on
-ONE GPU.  With --gpus N (torch.distributed.run, one process per GPU) every rank
-owns its own 10M-param bucket of a 10M*N-param model (weak scaling) and the
-global model is reassembled by all_gather_into_tensor.
+ONE GPU.  With --gpus N (one process per GPU) every rank owns its own
+10M-param bucket of a 10M*N-param model (weak scaling) and the global model is
+reassembled by all_gather_into_tensor (RCCL over xGMI).  `python bench.py
+--gpus N` with N > 1 outside torch.distributed.run starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a
+child process (before anything touches the GPU), passes its output through and
+exits with its status; under torch.distributed.run, --gpus must equal
+WORLD_SIZE.  Under torch.distributed.run the process group is initialised even
+at WORLD_SIZE 1 (nccl = RCCL), so the gather path runs on real RCCL streams.
 
 Inputs: integer-exact synthetic generator (fedlesscan_amd/synth.py), generated
 directly in HBM by fa_synth_*; random-init, no dataset.  Rank 0 at N=1 also
@@ -24,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -86,22 +94,75 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N > 1 run without torch.distributed.run: start it as a CHILD
+    process with one rank per GPU and return its exit status (None: this
+    process is a rank itself).  Runs before anything initialises the GPU (no
+    exec from a process that has: the child is a separate process), so the
+    N-GPU line is always N real ranks, never a relabelled 1-GPU run."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    if os.environ.get("FEDAVG_BENCH_BACKEND") != "gloo":
+        # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if args.gpus > have:
+            log(f"error: --gpus {args.gpus} but only {have} GPU(s) visible "
+                "(FEDAVG_BENCH_BACKEND=gloo rehearses more ranks than GPUs)")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    log("launching " + " ".join(cmd))
+    return subprocess.call(cmd)  # rank 0's JSON line reaches our stdout unchanged
+
+
 def setup_dist(args):
+    """(world, rank, device, backend).  Under torch.distributed.run the process
+    group is initialised at any world size, WORLD_SIZE 1 included, so the
+    all-gather path always runs (nccl = RCCL over xGMI)."""
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: the line would not measure "
+                         f"{args.gpus} GPUs")
+    backend = None
+    if launched:
         if os.environ.get("FEDAVG_BENCH_BACKEND") == "gloo":
             # rehearsal on a box with fewer GPUs than ranks: ranks share devices,
             # the gather goes through gloo (host memory); never a headline number
             torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group("gloo")
+            backend = "gloo"
+            dist.init_process_group(backend)
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            backend = "nccl"
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    return world, rank, torch.device("cuda", torch.cuda.current_device())
+    return world, rank, torch.device("cuda", torch.cuda.current_device()), backend
+
+
+def rank_devices(dev) -> list:
+    """Every rank's GPU (rank order): ordinal and PCI bus id."""
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": dist.get_rank() if dist.is_initialized() else 0, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "device": dev.index, "pci_bus_id": getattr(props, "pci_bus_id", None),
+          "pci_device_id": getattr(props, "pci_device_id", None), "name": props.name}
+    if not dist.is_initialized():
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
 
 
 class Workload:
@@ -177,10 +238,12 @@ class Workload:
 
 
 def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
-    """Oracle on host cores over a bounded column sample of the same workload."""
+    """Oracle on host cores over a bounded column sample of the same workload
+    (rank 0's first slot: the GPU output of those columns is checked bit for
+    bit against it)."""
     from oracle import fedavg_oracle as O  # checker / CPU baseline only
     from oracle import oracle_lib as OL
-    ncols = min(ncols, wl.P)
+    ncols = min(ncols, wl.slots[0][1] - wl.slots[0][0])
     t0 = time.time()
     Xh = OL.synth_f32(wl.seed, wl.N, ncols, col0=wl.col0) if wl.dtype == "f32" else \
         synth.bf16_bits_to_f32(OL.synth_bf16(wl.seed, wl.N, ncols, col0=wl.col0))
@@ -211,17 +274,23 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
     gpu = wl.out[:ncols].cpu().numpy()
     exact = bool(np.array_equal(gpu.view(np.uint32), ref.view(np.uint32)) and
                  np.array_equal(ref_omp.view(np.uint32), ref.view(np.uint32)))
+    visible = len(os.sched_getaffinity(0))
     return {
         "value": round(sample_bytes / t_np / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-        "sample": f"{wl.N} clients x first {ncols} params of the same workload; numpy literal restatement "
-                  f"of fed_avg_aggregator.py:24-42 (1 core, numpy ufuncs single-threaded), median of {len(t_np_all)} runs {t_np:.2f} s "
+        "sample": f"{wl.N} clients x first {ncols} params of the same workload (rank 0's first slot, columns "
+                  f"{wl.col0}..{wl.col0 + ncols}); numpy literal restatement of fed_avg_aggregator.py:24-42 "
+                  f"(1 core, numpy ufuncs single-threaded), median of {len(t_np_all)} runs {t_np:.2f} s "
                   f"(total {sum(t_np_all):.1f} s)",
+        "sample_temporaries": f"each `layer * n` product is a fresh {ncols * 4 / 1e6:.1f} MB float32 array "
+                              f"(the full workload's rows are {wl.P * 4 / 1e6:.1f} MB): the sample is friendlier "
+                              "to the caches than the whole job, so this rate is an upper bound for the "
+                              "reference on the full workload",
         "omp": {"value": round(sample_bytes / min(t_omp) / 1e9, 3), "unit": "GB/s", "cores": threads,
                 "kind": "port", "impl": "oracle/fedavg_ref.c (bit-identical, OpenMP)",
-                "cores_note": f"OpenMP threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS', 'unset')}), "
-                              "the host CPU share of one GPU on the GPU box; the other visible CPUs "
-                              "belong to the node's other GPUs"},
-        "host_cpus_visible": len(os.sched_getaffinity(0)),
+                "cores_note": f"{threads} OpenMP threads of the {visible} CPUs visible: OMP_NUM_THREADS "
+                              f"({os.environ.get('OMP_NUM_THREADS', 'unset')}) is the host CPU share of one GPU "
+                              "on the GPU box; the other visible CPUs belong to the node's other GPUs"},
+        "host_cpus_visible": visible,
         "sample_bit_exact_vs_gpu": exact,
         "gen_s": round(gen_s, 2),
     }
@@ -244,21 +313,23 @@ def read_traffic(config: str):
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist(args)
-    if args.gpus != world and world > 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    world, rank, dev, backend = setup_dist(args)
+    dist_on = dist.is_initialized()  # every rank-collective branch below keys on this, not on world > 1
     cfg = CONFIGS[args.config]
     if args.clients or args.params:
         cfg = (args.clients or cfg[0], args.params or cfg[1], *cfg[2:7],
                cfg[7] + f" [override: {args.clients or cfg[0]} clients x {args.params or cfg[1]} params]")
-    rounds = args.rounds or (1 if world == 1 else 4)
+    rounds = args.rounds or (4 if dist_on else 1)
     if args.splitn:
         args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra)
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
-                       device=dev) if world > 1 else None
+                       device=dev) if dist_on else None
     stream = torch.cuda.current_stream(dev)
 
     if args.sweep and rank == 0:
@@ -304,7 +375,7 @@ def main():
             wl.launch(args.variant, k)
             if ev is not None:
                 ev[0][k][1].record(stream)
-            if world > 1:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
+            if dist_on:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
                 lo, hi = lay.round_range(k)
                 w = gather_into(full[lo:hi], send[k * sub:(k + 1) * sub], None, async_op=True)
                 if w is not None:
@@ -318,7 +389,7 @@ def main():
         step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(rounds)], torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     # One GPU: the folds run back to back and two events bracket the whole timed
@@ -329,18 +400,18 @@ def main():
     t0 = time.perf_counter()
     region[0].record(stream)
     for k in range(args.steps):
-        step(evs[k] if world > 1 else None)
+        step(evs[k] if dist_on else None)
     region[1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gather_ok = None
-    if world > 1:  # my slots inside the reassembled model must be my fold output, bit for bit
+    if dist_on:  # my slots inside the reassembled model must be my fold output, bit for bit
         ok = True
         iv = torch.int32 if wl.dtype == "f32" else torch.int16
         for k, (lo, hi) in enumerate(wl.slots):
@@ -349,7 +420,7 @@ def main():
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
-    if world > 1:
+    if dist_on:
         kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in folds) for folds, _ in evs]
         # the exchange left exposed: from the last fold's end to the end of the step
         exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
@@ -358,7 +429,7 @@ def main():
     else:
         kern_avg = region[0].elapsed_time(region[1]) / args.steps  # per fold call, launch gaps included
         exposed_avg = 0.0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([kern_avg, exposed_avg], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
@@ -380,7 +451,7 @@ def main():
     ceiling = (nfl - nfl % 4) * 4 / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9
 
     tb = torch.tensor([float(wl.bytes)], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(tb)  # units all ranks processed
     total_bytes = float(tb.item()) * args.steps
     value = total_bytes / elapsed / 1e9
@@ -388,12 +459,18 @@ def main():
     # the committed PMC pass measured exactly this launch: the unmodified config, one fold per step
     traffic, traffic_src = (read_traffic(args.config) if not (args.clients or args.params) and rounds == 1
                             else (None, None))
+    devices = rank_devices(dev)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baseline runs on rank 0 at every world size, after the timed
+    # region (the other ranks wait at the barrier below), so every line -- the
+    # N-GPU ones included -- carries the reference timed on the same host
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(wl, args.cpu_cols, args.cpu_reps)
         except Exception as e:  # the baseline must never hide the GPU result
             cpu = {"error": repr(e)}
+    if dist_on:
+        dist.barrier()
     if rank == 0:
         line = {
             "metric": "aggregated GB/s (device-resident) — N-client FedAvg fp32 reduction",
@@ -416,7 +493,8 @@ def main():
                 "layout": f"row-stacked [clients][params] {'fp32' if wl.dtype == 'f32' else 'bf16'} in HBM",
                 "row_pitch": wl.ldx,
                 "parallelism": f"param-bucket x{world}" + (
-                    f" + RCCL all_gather in {rounds} rounds overlapped with the fold" if world > 1 else ""),
+                    f" + {'RCCL' if backend == 'nccl' else backend} all_gather in {rounds} rounds overlapped with "
+                    "the fold" if dist_on else ""),
                 "rounds": rounds,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
@@ -439,15 +517,19 @@ def main():
             },
             "cpu_baseline": cpu,
             "gather_check": gather_ok,
+            # the ranks that actually ran: torch.distributed's world and each rank's GPU
+            "dist": {"backend": backend, "world_size": dist.get_world_size() if dist_on else 1,
+                     "launcher": "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none (single process)",
+                     "devices": devices},
             # per-rank split of a step at N > 1 (max over ranks): the fold kernels,
             # and the all-gather left exposed after the last fold of the step
             "fold_ms": round(kern_avg, 4),
-            "gather_exposed_ms": round(exposed_avg, 4) if world > 1 else None,
+            "gather_exposed_ms": round(exposed_avg, 4) if dist_on else None,
             "gather_bytes_per_rank": (lay.padded_total * (4 if wl.dtype == "f32" else 2)
-                                      * (world - 1) // world) if world > 1 else 0,
+                                      * (world - 1) // world) if dist_on else 0,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

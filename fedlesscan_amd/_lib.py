@@ -64,6 +64,7 @@ _PROTOS = {
     "fa_host_alloc": (_int, [_vp, _i64]),
     "fa_host_free": (_int, [_vp]),
     "fa_copy_h2d": (_int, [_vp, _vp, _i64, _vp]),
+    "fa_copy_peer": (_int, [_vp, _int, _vp, _int, _i64, _vp]),
 }
 
 # libfedavg_hip_bench.so (include/fedavg_hip_bench.h)

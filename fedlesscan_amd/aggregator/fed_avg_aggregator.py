@@ -81,13 +81,20 @@ def chunked(items: Iterable, n: int) -> Iterator[list]:
 
 
 class FedAvgAggregator(ParameterAggregator):
-    """Cardinality-weighted FedAvg; the fold runs in libfedavg_hip.so."""
+    """Cardinality-weighted FedAvg; the fold runs in libfedavg_hip.so.
 
-    def __init__(self, device=None):
+    device:  the GPU to fold on (default: the current one).
+    devices: several GPUs of this process (a list of ints / torch.device, or
+             "all"): the model's columns are split into one bucket per GPU,
+             each GPU ingests and folds its own bucket (multigpu.py), and the
+             model is reassembled on the host; bit-identical to one GPU."""
+
+    def __init__(self, device=None, devices=None):
         self.device = device
+        self.devices = devices
 
     def _aggregate(self, parameters: List[List[np.ndarray]], weights: List[float]) -> List[np.ndarray]:
-        return engine.aggregate_layers(parameters, weights, None, device=self.device)
+        return engine.aggregate_layers(parameters, weights, None, device=self.device, devices=self.devices)
 
     def select_aggregation_candidates(self, store, session_id, round_id):
         dicts, candidates = store.load_results_for_round(session_id=session_id, round_id=round_id)
@@ -108,7 +115,7 @@ class FedAvgAggregator(ParameterAggregator):
             return self._aggregate(params, cards), (metrics or None)
         metrics: list = []
         out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
-                                       None, device=self.device)
+                                       None, device=self.device, devices=self.devices)
         return out, (metrics or None)
 
 
@@ -118,8 +125,8 @@ class StreamFedAvgAggregator(FedAvgAggregator):
     Reproduces the reference's running re-weighting exactly (it is not
     bit-equal to batch FedAvg)."""
 
-    def __init__(self, chunk_size: int = 25, device=None):
-        super().__init__(device)
+    def __init__(self, chunk_size: int = 25, device=None, devices=None):
+        super().__init__(device, devices)
         self.chunk_size = chunk_size
 
     def chunks(self, iterator: Iterator, n) -> Iterator[List]:

@@ -26,10 +26,12 @@ from .parameter_aggregator import ParameterAggregator
 
 
 class StallAwareAggregator(ParameterAggregator):
-    def __init__(self, current_round, aggregation_hyper_params: Optional[AggregationHyperParams], device=None):
+    def __init__(self, current_round, aggregation_hyper_params: Optional[AggregationHyperParams], device=None,
+                 devices=None):
         self.current_round = current_round
         self.tolerance = aggregation_hyper_params.tolerance if aggregation_hyper_params is not None else 0
         self.device = device
+        self.devices = devices  # several GPUs, one column bucket each (see FedAvgAggregator)
         super().__init__()
 
     def _score_clients(self, client_result: List[dict]) -> List[float]:
@@ -39,7 +41,7 @@ class StallAwareAggregator(ParameterAggregator):
     def _aggregate(self, client_feats: List[dict], parameters: List[List[np.ndarray]],
                    weights: List[float]) -> List[np.ndarray]:
         return engine.aggregate_layers(parameters, weights, self._score_clients(client_feats),
-                                       device=self.device)
+                                       device=self.device, devices=self.devices)
 
     def select_aggregation_candidates(self, store, session_id, round_id):
         dicts, candidates = store.load_results_for_session(session_id=session_id, round_id=round_id,
@@ -57,14 +59,15 @@ class StallAwareAggregator(ParameterAggregator):
             return self._aggregate(client_feats, params, cards), (metrics or None)
         metrics: list = []
         out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
-                                       self._score_clients(client_feats), device=self.device)
+                                       self._score_clients(client_feats), device=self.device,
+                                       devices=self.devices)
         return out, (metrics or None)
 
 
 class StreamStallAwareAggregator(StallAwareAggregator):
     def __init__(self, current_round: int, aggregation_hyper_params: Optional[AggregationHyperParams],
-                 chunk_size: int = 25, device=None):
-        super().__init__(current_round, aggregation_hyper_params, device)
+                 chunk_size: int = 25, device=None, devices=None):
+        super().__init__(current_round, aggregation_hyper_params, device, devices)
         self.chunk_size = chunk_size
 
     def chunks(self, iterator: Iterator, n) -> Iterator[List]:

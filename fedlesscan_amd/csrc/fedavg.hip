@@ -42,6 +42,9 @@ template <class Launch>
 int with_host_factors(const float* a, const float* s, int64_t N, void* stream, Launch launch) {
     if (N <= 0) return launch((const float*)nullptr, (const float*)nullptr);  // the entry's own checks report
     if (!a) return fail(FA_ERR_ARG, "null host factor pointer");
+    // the slot (and its device buffer) of the GPU that owns the stream, not of
+    // the calling thread's current device
+    StreamDevice on_stream_device(stream);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return fail(FA_ERR_HIP, "hipGetDevice");
     FactorRing& R = g_factor_rings[dev];
@@ -102,6 +105,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate_f32(float* acc, const flo
 
 }  // namespace
 
+// error text for the host entries of ingest_host.cpp (another TU)
+__attribute__((visibility("hidden"))) int fa_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
+
 // ===========================================================================
 // C-ABI
 // ===========================================================================
@@ -121,6 +127,7 @@ int fa_fold_f32(const float* X, int64_t N, int64_t P, int64_t ldx, const float* 
 }
 
 int fa_accumulate_f32(float* acc, const float* x, float a, float s, int first, int64_t P, void* stream) {
+    StreamDevice on_stream_device(stream);
     if (P < 0 || (P > 0 && (!acc || !x))) return fail(FA_ERR_ARG, "null acc/x or negative P");
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipLaunchKernelGGL(k_accumulate_f32, grid_for((P + 3) / 4), dim3(kBlock), 0, (hipStream_t)stream, acc, x, a, s,
@@ -143,6 +150,7 @@ int fa_fedavg_f32_splitn(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     const int64_t blocks = (((P + 3) >> 2) + 15) / 16;
     if (blocks > 0x7FFFFFFF / (NW * 64)) return fail(FA_ERR_ARG, "P too large for fa_fedavg_f32_splitn");
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     if (s)
         hipLaunchKernelGGL((k_fold_f32_splitn<NW, true>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, X, N, P,
                            ldx, a, s, divisor, out);
@@ -159,6 +167,7 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     if (!aligned16(out)) return fail(FA_ERR_ARG, "fa_fedavg_f32_ptrs_aligned needs a 16-B aligned out");
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
 #define FA_R(U, C, GRIDCAP)                                                                                    \
     {                                                                                                          \
@@ -216,6 +225,7 @@ int fa_fedavg_f32_ptrs(const float* const* xi, int64_t N, int64_t P, const float
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     // rows at any 4-B offset.  Narrow models: the LDS-staged fold with 4-byte
     // loads and row bases from the table; otherwise one lane per column, row
     // bases wave-uniform.  (The round-2 kernel, a lane per 4 columns with a
@@ -251,6 +261,7 @@ int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const doub
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     if (aligned16(X) && aligned16(out) && (ldx % 2 == 0)) {
         if (s)
             hipLaunchKernelGGL((k_fedavg_f64_v2<8, true>), grid_for((P >> 1) + 1), dim3(kBlock), 0, st, X, N, P,
@@ -274,6 +285,7 @@ int fa_fedavg_i32(const int32_t* X, int64_t N, int64_t P, int64_t ldx, const int
     int rc = check_common(N, P, ldx, X, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
+    StreamDevice on_stream_device(stream);
     hipLaunchKernelGGL((k_fedavg_int<int32_t, uint32_t>), grid_for(P), dim3(kBlock), 0, (hipStream_t)stream,
                        X, N, P, ldx, a, divisor, out);
     return check_launch("k_fedavg_int<int32>");
@@ -284,6 +296,7 @@ int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx, const int
     int rc = check_common(N, P, ldx, X, a, out);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
+    StreamDevice on_stream_device(stream);
     hipLaunchKernelGGL((k_fedavg_int<int64_t, uint64_t>), grid_for(P), dim3(kBlock), 0, (hipStream_t)stream,
                        X, N, P, ldx, a, divisor, out);
     return check_launch("k_fedavg_int<int64>");
@@ -354,6 +367,42 @@ int fa_copy_h2d(void* dst, const void* src, int64_t n, void* stream) {
     if (n == 0) return FA_OK;
     hipError_t e = hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyHostToDevice, (hipStream_t)stream);
     if (e != hipSuccess) return fail(FA_ERR_HIP, "hipMemcpyAsync H2D: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+// ---- single-process multi-GPU: reassembling the model over xGMI -------------
+int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int64_t n, void* stream) {
+    if (n < 0 || (n && (!dst || !src)) || dst_device < 0 || src_device < 0 || dst_device >= 16 ||
+        src_device >= 16)
+        return fail(FA_ERR_ARG, "fa_copy_peer: bad arguments");
+    if (n == 0) { g_err[0] = 0; return FA_OK; }
+    StreamDevice on_stream_device(stream);
+    if (dst_device != src_device) {
+        // peer access both ways, once per pair (without it the runtime stages
+        // the copy through host memory)
+        static std::mutex mu;
+        static bool tried[16][16] = {};
+        std::lock_guard<std::mutex> lk(mu);
+        if (!tried[src_device][dst_device]) {
+            tried[src_device][dst_device] = tried[dst_device][src_device] = true;
+            int prev = 0;
+            (void)hipGetDevice(&prev);
+            const int pair[2][2] = {{src_device, dst_device}, {dst_device, src_device}};
+            for (const auto& pr : pair) {
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, pr[0], pr[1]) == hipSuccess && can && hipSetDevice(pr[0]) == hipSuccess) {
+                    const hipError_t pe = hipDeviceEnablePeerAccess(pr[1], 0);
+                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                        (void)hipGetLastError();  // the copy below still works, staged
+                }
+            }
+            (void)hipGetLastError();  // clear any failed enable: the copy reports its own status
+            (void)hipSetDevice(prev);
+        }
+    }
+    hipError_t e = hipMemcpyPeerAsync(dst, dst_device, src, src_device, (size_t)n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipMemcpyPeerAsync: %s", hipGetErrorString(e));
+    g_err[0] = 0;
     return FA_OK;
 }
 

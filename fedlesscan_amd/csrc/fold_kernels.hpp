@@ -25,7 +25,8 @@
 //                    balanced passes, launched per column band (large models)
 //   k_fold_f32_tile  one block per tile, same tile body (few clients)
 //   k_fold_f32_lds   LDS-staged: all waves stream client-row chunks of a
-//                    narrow column tile into LDS, wave 0 folds (narrow models)
+//                    narrow column tile into LDS, then every wave folds its
+//                    share of the tile's columns from LDS (narrow models)
 // Everything here sits in an anonymous namespace: each library gets its own
 // copy, and templates are instantiated only where a TU launches them.
 #pragma once
@@ -582,12 +583,17 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
 }
 
 // ---------------------------------------------------------------------------
+// TUNING VARIANT ONLY (measured and rejected, DESIGN.md 5 "LDS-DMA ring"):
+// the product never launches it; it stays in libfedavg_hip_bench.so as the
+// measured answer to the "deeper LDS ring" idea.
 // Narrow models, deep ring: LDS-DMA (global_load_lds) into an S-slot ring.
-//   Same tile and fold as k_fold_f32_lds (a block owns TQ quads of every row;
-//   wave 0 folds each R-row chunk from LDS in client order, one lane per quad),
+//   Same tile as k_fold_f32_lds with the round-1 quad fold (a block owns TQ
+//   quads of every row; wave 0 folds each R-row chunk from LDS in client
+//   order, one lane per quad),
 //   but the chunks are copied HBM -> LDS by global_load_lds_dwordx4, which
 //   needs no VGPRs: S - 1 chunks stay in flight per block (the register-staged
-//   fold holds two), which is what a narrow model is short of.  Counters on
+//   fold holds two), which was the hypothesis for narrow models (it measured
+//   slower everywhere).  Counters on
 //   1024 x 16K / 67K (profiles/r02_narrow/SUMMARY.md): SQ_WAIT_ANY = 72-80 %
 //   of the wave cycles with at most two chunks in flight, i.e. latency-bound.
 //   Synchronisation per chunk: each wave's counted `s_waitcnt vmcnt` retires
@@ -1256,6 +1262,32 @@ int check_common(int64_t N, int64_t P, int64_t ldx, const void* X, const void* a
     return FA_OK;
 }
 
+// Make the device that owns `stream` current for the duration of one C-ABI
+// call, and restore the caller's device afterwards.  Every allocation (the
+// host-factor ring's device slots), every CU-count lookup (the fold policy) and
+// every launch then belongs to the stream's GPU, whatever device the calling
+// thread has current: a fold of tensors on cuda:1 issued from a thread whose
+// current device is 0 reads its factors from cuda:1's memory and is picked for
+// cuda:1's CU count.  A NULL stream means the caller's current device.
+struct StreamDevice {
+    int prev = -1;
+    explicit StreamDevice(void* stream) {
+        if (!stream) return;
+        int cur = 0;
+        hipDevice_t d = 0;
+        if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice((hipStream_t)stream, &d) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        if ((int)d != cur && hipSetDevice((int)d) == hipSuccess) prev = cur;
+    }
+    ~StreamDevice() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    StreamDevice(const StreamDevice&) = delete;
+    StreamDevice& operator=(const StreamDevice&) = delete;
+};
+
 // Compute units of the current device (cached per device).
 int cu_count() {
     static thread_local int cache[16] = {0};
@@ -1542,6 +1574,7 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     }
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     const bool sc = s != nullptr, acc = acc_in != nullptr, fin = finalize != 0;
     const bool vec = (N == 0 || aligned16(X)) && (ldx % 4 == 0) && aligned16(out) &&
                      (!acc || aligned16(acc_in));
@@ -1632,6 +1665,7 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
+    StreamDevice on_stream_device(stream);
     const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && (!out_bf16 || aligned16(out_bf16));
     if (!vec) {
         if (s)

@@ -236,6 +236,10 @@ const CrcTables& crc_tables() {
 
 }  // namespace
 
+// fa_last_error() text for the host entries (defined in fedavg.hip, hidden:
+// not part of the exported ABI)
+__attribute__((visibility("hidden"))) int fa_internal_fail(int code, const char* msg);
+
 extern "C" {
 
 static int npz_index_impl(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* counts, int32_t* dtypes,
@@ -320,11 +324,12 @@ int fa_npz_index(const uint8_t* blob, int64_t len, int64_t* offsets, int64_t* co
 
 int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, const int64_t* sizes, int64_t n,
             int nthreads) {
-    if (n < 0 || (n > 0 && (!dst || !dst_offsets || !srcs || !sizes))) return FA_ERR_ARG;
+    if (n < 0 || (n > 0 && (!dst || !dst_offsets || !srcs || !sizes)))
+        return fa_internal_fail(FA_ERR_ARG, "fa_pack: bad arguments");
     // prefix sums of the source sizes: the work is split by bytes, not ranges
     std::vector<int64_t> off(n + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
-        if (sizes[i] < 0 || dst_offsets[i] < 0) return FA_ERR_ARG;
+        if (sizes[i] < 0 || dst_offsets[i] < 0) return fa_internal_fail(FA_ERR_ARG, "fa_pack: negative size or offset");
         off[i + 1] = off[i] + sizes[i];
     }
     const int64_t total = off[n];
@@ -355,7 +360,7 @@ int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, cons
 }
 
 int fa_crc32(const void* data, int64_t n, uint32_t crc_in, int nthreads, uint32_t* crc_out) {
-    if (n < 0 || (n > 0 && !data) || !crc_out) return FA_ERR_ARG;
+    if (n < 0 || (n > 0 && !data) || !crc_out) return fa_internal_fail(FA_ERR_ARG, "fa_crc32: bad arguments");
     const CrcTables& K = crc_tables();
     const uint8_t* p = (const uint8_t*)data;
     int T = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());

@@ -414,15 +414,34 @@ def _layer_meta(parameters, n_eff):
     return L, shapes, dtypes
 
 
+def _multi(devices) -> Optional[list]:
+    """The device list of a multi-GPU call, or None for a one-GPU call."""
+    if devices is None:
+        return None
+    from .multigpu import resolve_devices
+    devs = resolve_devices(devices)
+    return devs if len(devs) > 1 else None
+
+
 def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: Optional[Sequence] = None,
-                     device: Optional[torch.device] = None) -> List:
+                     device: Optional[torch.device] = None, devices=None) -> List:
     """Reference-shaped FedAvg / stall-aware aggregation.
 
     parameters: N clients x L layers (numpy arrays, or CUDA tensors).  Returns
     L outputs (numpy in -> numpy out, tensors in -> CUDA tensors out).  zip()
     truncation over clients/weights/scores and over layers is kept
     (fed_avg_aggregator.py:32-41); the divisor is the sum of ALL weights.
+
+    devices: several GPUs of this process (multigpu.py): host float32 layers
+    are folded one column bucket per GPU, bit-identical to one GPU.  Other
+    layer groups (device tensors, other dtypes) run on the first of them.
     """
+    multi = _multi(devices)
+    if multi is not None and device is None:
+        device = multi[0]
+    elif devices is not None and multi is None and device is None:
+        from .multigpu import resolve_devices
+        device = resolve_devices(devices)[0]
     n_eff = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
     if n_eff == 0:
         return []
@@ -444,6 +463,13 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
         fp32_result = result_dtype(np.dtype(np.float32), total_weights, sc) == np.float32
         if (not on_device and P > 0 and dtypes[lis[0]] == np.float32 and fp32_result):
             # host fp32 rows: pipelined pinned-chunk H2D + in-order chunked fold (bit-identical)
+            if multi is not None:  # one column bucket per GPU, result assembled in pinned host memory
+                flat = _stream_group_multi(parameters, n_eff, lis, P, w, sc, sum(total_weights), multi)
+                off = 0
+                for li, n in zip(lis, sizes):
+                    outs[li] = flat[off:off + n].reshape(shapes[li])
+                    off += n
+                continue
             res = _stream_group(parameters, n_eff, lis, P, w, sc, sum(total_weights), dev)
         elif on_device and dtypes[lis[0]] == torch.float32 and fp32_result and all(
                 parameters[i][li].is_contiguous() for i in range(n_eff) for li in lis):
@@ -484,7 +510,8 @@ def _fast_row(layers, shapes) -> bool:
                 for x, shp in zip(layers, shapes)))
 
 
-def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional[torch.device] = None) -> List:
+def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional[torch.device] = None,
+                      devices=None) -> List:
     """aggregate_layers over an iterator of decoded (layers, weight) rows, with
     the fold overlapping the decode.
 
@@ -497,7 +524,14 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
     drains the iterator and runs aggregate_layers over every row, which is
     exactly the materialised path.  zip() truncation is kept: rows beyond
     len(scores) are not folded, their weights still count in the divisor.
+
+    devices: several GPUs (multigpu.MultiStreamingFold): every GPU ingests and
+    folds its own column bucket of each row, so the rows cross G PCIe links.
     """
+    multi = _multi(devices)
+    if devices is not None and device is None:
+        from .multigpu import resolve_devices
+        device = resolve_devices(devices)[0]
     it = iter(items)
     first = next(it, None)
     if first is None:
@@ -509,9 +543,13 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
             (scores is None or (len(scores) > 0 and all(_py_scalar(x) for x in scores))))
     P = sum(int(np.prod(shp)) if len(shp) else 1 for shp in shapes) if fast else 0
     if fast and P > 0:
-        from .ingest import StreamingFold
-        sf = StreamingFold(P, chunk_rows=max(1, STREAM_CHUNK_BYTES // (4 * P)),
-                           device=device or default_device(), direct=DIRECT_DMA)
+        if multi is not None:
+            from .multigpu import MultiStreamingFold
+            sf = MultiStreamingFold(P, multi, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
+        else:
+            from .ingest import StreamingFold
+            sf = StreamingFold(P, chunk_rows=max(1, STREAM_CHUNK_BYTES // (4 * P)),
+                               device=device or default_device(), direct=DIRECT_DMA)
         sf.add(list(first[0]), first[1], None if scores is None else scores[0])
         for layers, w in it:
             rows.append(layers)
@@ -525,7 +563,8 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
                 break
             sf.add(list(layers), w, None if scores is None else scores[i])
         else:
-            flat = to_host(sf.finish(total=sum(weights)))
+            res = sf.finish(total=sum(weights))
+            flat = res if multi is not None else to_host(res)
             outs, off = [], 0
             for shp in shapes:
                 n = int(np.prod(shp)) if len(shp) else 1
@@ -535,7 +574,7 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
     for layers, w in it:
         rows.append(layers)
         weights.append(w)
-    return aggregate_layers(rows, weights, scores, device=device)
+    return aggregate_layers(rows, weights, scores, device=device, devices=devices)
 
 
 def to_host(t: torch.Tensor) -> np.ndarray:
@@ -552,6 +591,14 @@ def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
     from .ingest import StreamingFold
     rows = max(1, min(n, STREAM_CHUNK_BYTES // (4 * P)))
     sf = StreamingFold(P, chunk_rows=rows, device=dev, direct=DIRECT_DMA)
+    for i in range(n):
+        sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
+    return sf.finish(total=total)
+
+
+def _stream_group_multi(parameters, n, lis, P, w, sc, total, devices) -> np.ndarray:
+    from .multigpu import MultiStreamingFold
+    sf = MultiStreamingFold(P, devices, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
     for i in range(n):
         sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
     return sf.finish(total=total)

@@ -52,24 +52,25 @@ def create_http_user_error_response(exception: Exception, status: int = 400) -> 
     return {"statusCode": status, "body": json.dumps(format_exception_for_user(exception)), "headers": dict(_JSON)}
 
 
-def _run(config: AggregatorFunctionParams, result_store, parameter_store, device) -> str:
+def _run(config: AggregatorFunctionParams, result_store, parameter_store, device, devices=None) -> str:
     result = default_aggregation_handler(
         session_id=config.session_id, round_id=config.round_id, result_store=result_store,
         parameter_store=parameter_store, serializer=config.serializer, test_data=config.test_data,
         aggregation_strategy=config.aggregation_strategy,
-        aggregation_hyper_params=config.aggregation_hyper_params, device=device)
+        aggregation_hyper_params=config.aggregation_hyper_params, device=device, devices=devices)
     return json.dumps(result.model_dump(mode="json"))  # pydantic-v1 .json() layout (providers.py:172)
 
 
 def make_openfaas_handler(result_store: InMemoryClientResultStore, parameter_store: InMemoryParameterStore,
-                          device=None) -> Callable:
+                          device=None, devices=None) -> Callable:
     """handle(event, context) of the OpenFaaS aggregator (handler.py:16-28):
-    event.body is the AggregatorFunctionParams JSON."""
+    event.body is the AggregatorFunctionParams JSON.  devices: fold on several
+    GPUs of the function's process (one column bucket each)."""
 
     def handle(event, context=None) -> Dict:
         try:
             config = AggregatorFunctionParams.model_validate_json(event.body)
-            return create_http_success_response(_run(config, result_store, parameter_store, device))
+            return create_http_success_response(_run(config, result_store, parameter_store, device, devices))
         except (ValidationError, AggregationError) as e:
             return create_http_user_error_response(e)
 
@@ -77,7 +78,7 @@ def make_openfaas_handler(result_store: InMemoryClientResultStore, parameter_sto
 
 
 def make_openwhisk_main(result_store: InMemoryClientResultStore, parameter_store: InMemoryParameterStore,
-                        device=None) -> Callable:
+                        device=None, devices=None) -> Callable:
     """main(request) of the OpenWhisk aggregator (main.py:12-24) with the
     openwhisk_action_handler parameter handling (providers.py:180-218)."""
 
@@ -94,7 +95,7 @@ def make_openwhisk_main(result_store: InMemoryClientResultStore, parameter_store
                 except JSONDecodeError:
                     body = json.loads(base64.b64decode(body))
             config = AggregatorFunctionParams.model_validate(body)
-            return create_http_success_response(_run(config, result_store, parameter_store, device))
+            return create_http_success_response(_run(config, result_store, parameter_store, device, devices))
         except (ValidationError, AggregationError, JSONDecodeError, binascii.Error) as e:
             return create_http_user_error_response(e)
 

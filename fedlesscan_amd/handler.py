@@ -49,17 +49,19 @@ def default_aggregation_handler(session_id: str, round_id: int, result_store: In
                                 test_data=None, delete_results_after_finish: bool = True,
                                 aggregation_strategy: AggregationStrategy = AggregationStrategy.PER_ROUND,
                                 aggregation_hyper_params: Optional[AggregationHyperParams] = None,
-                                device=None) -> AggregatorFunctionResult:
+                                device=None, devices=None) -> AggregatorFunctionResult:
+    """device / devices: the GPU, or several GPUs of this process (one column
+    bucket each, fedlesscan_amd.multigpu), the strategy folds on."""
     hp = aggregation_hyper_params if aggregation_hyper_params is not None else AggregationHyperParams()
     per_session = aggregation_strategy == AggregationStrategy.PER_SESSION
     logger.info(f"Aggregator invoked for session {session_id} and round {round_id}")
     try:
-        aggregator = (StallAwareAggregator(round_id, hp, device=device) if per_session
-                      else FedAvgAggregator(device=device))
+        aggregator = (StallAwareAggregator(round_id, hp, device=device, devices=devices) if per_session
+                      else FedAvgAggregator(device=device, devices=devices))
         feats, results = aggregator.select_aggregation_candidates(result_store, session_id, round_id)
         if hp.aggregate_online:
-            aggregator = (StreamStallAwareAggregator(round_id, hp, device=device) if per_session
-                          else StreamFedAvgAggregator(device=device))
+            aggregator = (StreamStallAwareAggregator(round_id, hp, device=device, devices=devices) if per_session
+                          else StreamFedAvgAggregator(device=device, devices=devices))
         else:
             results = results if isinstance(results, list) else list(results)
         new_parameters, test_results = aggregator.aggregate(results, feats)
@@ -89,8 +91,10 @@ class MockAggregator:
     """In-process aggregator (mock_aggregation.py:6-31) over the in-memory stores."""
 
     def __init__(self, params: AggregatorFunctionParams, result_store: InMemoryClientResultStore,
-                 parameter_store: InMemoryParameterStore, delete_results_after_finish: bool = True, device=None):
+                 parameter_store: InMemoryParameterStore, delete_results_after_finish: bool = True, device=None,
+                 devices=None):
         self.params = params
+        self.devices = devices
         self.result_store = result_store
         self.parameter_store = parameter_store
         self.delete_results_after_finish = delete_results_after_finish
@@ -100,4 +104,5 @@ class MockAggregator:
         p = self.params
         return default_aggregation_handler(p.session_id, p.round_id, self.result_store, self.parameter_store,
                                            p.serializer, None, self.delete_results_after_finish,
-                                           p.aggregation_strategy, p.aggregation_hyper_params, self.device)
+                                           p.aggregation_strategy, p.aggregation_hyper_params, self.device,
+                                           self.devices)

@@ -173,7 +173,7 @@ def write_npz(arrays) -> Optional[bytes]:
 
     Returns None (the caller runs np.savez) for anything numpy writes another
     way: object dtypes (pickled), arrays that are not C-contiguous, members of
-    4 GiB or more.
+    4 GiB or more; and when libfedavg_hip.so cannot be loaded.
     """
     from numpy.lib import format as npformat
     from . import _lib
@@ -182,7 +182,12 @@ def write_npz(arrays) -> Optional[bytes]:
     for a in arrs:
         if a.dtype.hasobject or not a.flags.c_contiguous or a.nbytes >= zipfile.ZIP64_LIMIT:
             return None
-    L = _lib.load()
+    try:
+        # host-only helpers of the HIP library (CRC-32, threaded copies); a
+        # process that only saves a model must still save it without them
+        L = _lib.load()
+    except (_lib.AggregationError, OSError):
+        return None  # the caller runs np.savez: the same bytes
     import ctypes
     crc = ctypes.c_uint32()
     parts: list = []  # local header, .npy header, payload for each member; then the directory

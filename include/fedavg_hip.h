@@ -155,6 +155,19 @@ int fa_host_alloc(void** p, int64_t n);
 int fa_host_free(void* p);
 int fa_copy_h2d(void* dst, const void* src, int64_t n, void* stream);
 
+/* ---- single-process multi-GPU ------------------------------------------------
+ * The reference calls the strategy in-process, once per round
+ * (aggregation.py:71-97).  The multi-GPU drop-in (fedlesscan_amd/multigpu.py)
+ * folds one column bucket per GPU in that same process and reassembles the
+ * model on one of them:
+ *   fa_copy_peer: n bytes from src (on src_device) to dst (on dst_device),
+ *     hipMemcpyPeerAsync over xGMI, enqueued on `stream` (normally the source
+ *     GPU's stream that produced src, so it runs after that fold).  Peer
+ *     access is enabled both ways the first time a pair is used.
+ * Every compute entry above runs on the GPU that owns its stream, whatever
+ * device the calling thread has current. */
+int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int64_t n, void* stream);
+
 /* ---- host-side ingest (no GPU): NPZ wire format -> pinned staging ----------
  * Client blobs are uncompressed NPZ archives (NpzWeightsSerializer,
  * serialization.py:280-306, written by the client, client.py:186-199). */

@@ -1,0 +1,96 @@
+"""The RCCL (torch.distributed "nccl") exchange on the MI355X.
+
+The 8-GPU run belongs to the driver; a one-GPU box cannot hold two RCCL ranks
+(RCCL refuses two ranks on one device), so this runs the nccl backend at world
+size 1 on cuda:0, in ONE spawned process (RCCL state stays out of the pytest
+process): the per-round async all_gather_into_tensor on RCCL's streams, its
+overlap with the next round's fold, the bf16-as-uint8 exchange, and the
+reference-shaped per-layer entry, all bit-exact against the oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+from fedlesscan_amd import synth
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+N, SEED = 41, 21
+CASES = [("f32", 10007, 4), ("f32", 262144 + 5, 4), ("bf16", 8 * 1000 + 3, 4), ("bf16", 65536, 3)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scores(seed, n):
+    return [(r + 1) / 11 for r in synth.round_ids(seed, n, 10, 2)]
+
+
+def _rccl_worker(port, q):
+    import torch as T
+    import torch.distributed as dist
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    T.cuda.set_device(0)
+    dev = T.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        out = {"backend": dist.get_backend()}
+        agg = ShardedAggregator()
+        w = synth.cardinalities(SEED, N)
+        sc = _scores(SEED, N)
+        for dt, P, rounds in CASES:
+            lay = SlotLayout(P, 1, rounds)
+            bf16 = dt == "bf16"
+            X = T.zeros((N, lay.local_width), dtype=T.int16 if bf16 else T.float32, device=dev)
+            for k, (lo, hi) in enumerate(lay.slots(0)):
+                if hi > lo:
+                    part = (synth.clients_bf16(SEED, N, lo, hi - lo).view(np.int16) if bf16
+                            else synth.clients_f32(SEED, N, lo, hi - lo))
+                    X[:, k * lay.sub:k * lay.sub + hi - lo] = T.from_numpy(part).to(dev)
+            for scored in (False, True):
+                full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
+                out[(dt, P, scored)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
+        m = G.manifest()["f32_small"]
+        layers = agg.aggregate_layers(G.parameters("f32_small"), m["weights"])
+        out["layers"] = [np.array(a) for a in layers]
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_slots_and_layers_bit_exact():
+    import torch.multiprocessing as mp
+    from oracle import fedavg_oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    got = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert got["backend"] == "nccl"
+    w = synth.cardinalities(SEED, N)
+    sc = _scores(SEED, N)
+    for dt, P, _ in CASES:
+        for scored in (False, True):
+            s = sc if scored else None
+            if dt == "bf16":
+                _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(SEED, N, 0, P), w, s)
+                assert np.array_equal(np.frombuffer(got[(dt, P, scored)], dtype=np.uint16), exp), (dt, P, scored)
+            else:
+                exp = O.fedavg_stacked(synth.clients_f32(SEED, N, 0, P), w, s)
+                assert np.array_equal(np.frombuffer(got[(dt, P, scored)], dtype=np.uint32),
+                                      exp.view(np.uint32)), (dt, P, scored)
+    exp_layers = G.expected("f32_small", "fedavg")
+    assert len(got["layers"]) == len(exp_layers)
+    assert all(a.shape == b.shape and G.same_bits(a, b) for a, b in zip(got["layers"], exp_layers))

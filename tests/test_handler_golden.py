@@ -49,12 +49,13 @@ def _build_store(entry):
     return st
 
 
-def _run(entry, device=None):
+def _run(entry, device=None, devices=None):
     from fedlesscan_amd.handler import default_aggregation_handler
     st, ps = _build_store(entry), InMemoryParameterStore()
     res = default_aggregation_handler("s", entry["round_id"], st, ps, SER, None, entry["delete"],
                                       AggregationStrategy(entry["strategy"]),
-                                      AggregationHyperParams(**entry["hyperparams"]), device=device)
+                                      AggregationHyperParams(**entry["hyperparams"]), device=device,
+                                      devices=devices)
     return res, st, ps
 
 
@@ -83,7 +84,7 @@ def _check(name, entry, res, st, ps):
 
 @pytest.fixture
 def oracle_fold(monkeypatch):
-    def fake(parameters, weights, scores=None, device=None):
+    def fake(parameters, weights, scores=None, device=None, devices=None):
         n = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
         if scores is None:
             return O.fedavg_literal(parameters[:n], list(weights))
@@ -91,7 +92,7 @@ def oracle_fold(monkeypatch):
         prods = [[np.multiply(np.multiply(l, w), s) for l in p] for p, w, s in zip(parameters, weights, scores)]
         return [reduce(np.add, ls) / total for ls in zip(*prods)]
 
-    def fake_decoded(items, scores=None, device=None):
+    def fake_decoded(items, scores=None, device=None, devices=None):
         rows, ws = [], []
         for layers, w in items:
             rows.append(layers)
@@ -145,3 +146,17 @@ def test_handler_on_gpu_vs_reference(name):
         assert type(ei.value).__name__ == entry["raises"]
         return
     _check(name, entry, *_run(entry, dev))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", _scenarios())
+def test_handler_on_two_gpu_buckets_vs_reference(name):
+    """The same scenarios with the strategy folding one column bucket per GPU
+    (devices=[0, 0]: two buckets on the one GPU of a test box)."""
+    entry = G.manifest()[CASE]["scenarios"][name]
+    if "raises" in entry:
+        with pytest.raises(Exception) as ei:
+            _run(entry, devices=[0, 0])
+        assert type(ei.value).__name__ == entry["raises"]
+        return
+    _check(name, entry, *_run(entry, devices=[0, 0]))

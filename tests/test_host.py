@@ -276,12 +276,12 @@ def test_store_returns_fresh_objects():
 # ---------------------------------------------------------------------------
 @pytest.fixture
 def oracle_fold(monkeypatch):
-    def fake(parameters, weights, scores=None, device=None):
+    def fake(parameters, weights, scores=None, device=None, devices=None):
         n = min(len(parameters), len(weights), len(scores) if scores is not None else len(weights))
         if scores is None:
             return O.fedavg_literal(parameters[:n], list(weights))
         return _stall(parameters[:n], list(weights), list(scores))
-    def fake_decoded(items, scores=None, device=None):
+    def fake_decoded(items, scores=None, device=None, devices=None):
         rows, ws = [], []
         for layers, w in items:
             rows.append(layers)
