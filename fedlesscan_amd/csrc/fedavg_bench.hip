@@ -166,6 +166,10 @@ constexpr const char* kVariants[] = {
     "dw_lds2_w4r64t32", "dw_lds3_w8r32t32", "scalar",
     // one block per tile (the product's few-client form, k_fold_f32_tile), more rows or quads per lane
     "tile_u8c1", "tile_u16c1", "tile_u8c2", "tile_u4c2", "tile_u8c1_nts", "tile_u4c1",
+    // even split: one block per CU (g2: two) owning ceil(nq / blocks) contiguous quads,
+    // auto = quads per lane from the range (k_fold_f32_even, round 3)
+    "even_auto", "even_g2_auto", "even_u16c2", "even_u32c1", "even_u8c4", "even_u4c4", "even_g2_u8c2",
+    "even_g4_auto",
 };
 constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
 constexpr int kEndAnyAlign = 92;
@@ -404,6 +408,16 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 96: rc = FA_VT(8, 1, true); break;
         case 97: rc = FA_VT(4, 1, false); break;
 #undef FA_VT
+#define FA_VE(G, U, C) launch_even_flags<U, C>(st, G, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 98: launch_even_auto(st, cu_count(), sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out); break;
+        case 99: launch_even_auto(st, 2 * cu_count(), sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out); break;
+        case 100: FA_VE(cu_count(), 16, 2); break;
+        case 101: FA_VE(cu_count(), 32, 1); break;
+        case 102: FA_VE(cu_count(), 8, 4); break;
+        case 103: FA_VE(cu_count(), 4, 4); break;
+        case 104: FA_VE(2 * cu_count(), 8, 2); break;
+        case 105: launch_even_auto(st, 4 * cu_count(), sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out); break;
+#undef FA_VE
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF

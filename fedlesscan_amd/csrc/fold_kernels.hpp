@@ -887,6 +887,93 @@ __global__ __launch_bounds__(kBlock) void k_fold_f32_scalar(
     out[c] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// Even split: a persistent grid of G blocks (one per CU) where block b owns
+// the contiguous quad range [b*per, min((b+1)*per, nq)), per = ceil(nq / G).
+// Every block streams the same bytes (to one quad per row), so the launch
+// ends when every CU ends: no partly-filled last round of blocks, no idle CUs
+// (the tile launches leave 20-30 % of the CUs idle at 0.7-0.9 tiles per CU).
+// Inside its range a block walks chunks of C*kBlock quads, lane l taking quads
+// chunk + l + kBlock*c (every wave-load one contiguous 1 KiB run).  A lane
+// whose quad lies past the range loads the range's last quad instead (a valid
+// address the wave's other lanes already read: one merged cache line) and
+// never stores it, so the loads carry no branch.  Rows go U at a time with
+// every row index clamped to N-1 and the adds of rows past N skipped (a
+// wave-uniform test after the loads), so the client tail is pipelined too.
+// Same per-column in-order fold as every other kernel (bit-identical).
+// The P%4 tail columns are folded by the last lane of the last block.
+// ---------------------------------------------------------------------------
+template <int U, int C, bool SCORED, bool ACC, bool FIN>
+__global__ __launch_bounds__(kBlock) void k_fold_f32_even(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t per) {  // acc_in may alias out
+    const int64_t nq = P >> 2, ldq = ldx >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < nq ? lo + per : nq;
+    for (int64_t base = lo; base < hi; base += (int64_t)C * kBlock) {
+        int64_t q[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int64_t qq = base + threadIdx.x + (int64_t)c * kBlock;
+            q[c] = qq < hi ? qq : hi - 1;
+        }
+        f32x4 acc[C];
+        int64_t i0;
+        if constexpr (ACC) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = reinterpret_cast<const f32x4*>(acc_in)[q[c]];
+            i0 = 0;
+        } else {
+            const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = term4<SCORED>(__builtin_nontemporal_load(X4 + q[c]), a0, s0);
+            i0 = 1;
+        }
+        for (int64_t i = i0; i < N; i += U) {
+            f32x4 v[U][C];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = i + u < N ? i + u : N - 1;
+#pragma unroll
+                for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(X4 + r * ldq + q[c]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (i + u < N) {  // wave-uniform
+                    const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(v[u][c], ai, si));
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (base + threadIdx.x + (int64_t)c * kBlock < hi) {
+                const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
+                __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(out) + q[c]);
+            }
+        }
+    }
+    if ((P & 3) && blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) {
+        for (int64_t col = nq * 4; col < P; ++col) {
+            float acc;
+            int64_t i = 0;
+            if constexpr (ACC) {
+                acc = acc_in[col];
+            } else {
+                acc = term1<SCORED>(X[col], a[0], SCORED ? s[0] : 1.0f);
+                i = 1;
+            }
+#pragma unroll 8
+            for (; i < N; ++i) acc = acc + term1<SCORED>(X[i * ldx + col], a[i], SCORED ? s[i] : 1.0f);
+            if constexpr (FIN) acc = acc / divisor;
+            out[col] = acc;
+        }
+    }
+}
+
 // List-of-rows form: xi[i] = device pointer to client i's P floats.  A lane
 // owns 4 columns; U rows are loaded ahead of the ordered adds.  The row
 // alignment test is wave-uniform (every lane reads the same pointer).
@@ -1495,6 +1582,50 @@ void launch_scalar(hipStream_t st, const float* X, int64_t N, int64_t P, int64_t
                    const float* s, const float* acc_in, float d, float* out) {
     hipLaunchKernelGGL((k_fold_f32_scalar<SC, ACC, FIN>), grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx,
                        a, s, acc_in, d, out);
+}
+
+// Even-split fold (k_fold_f32_even): G blocks, per = ceil(nq / G) quads each.
+template <int U, int C, bool ALLF = false>
+void launch_even_flags(hipStream_t st, int64_t G, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                       int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t nq = P >> 2;
+    if (G < 1) G = 1;
+    int64_t per = (nq + G - 1) / G;
+    if (per < 1) per = 1;
+    const int64_t grid = nq > 0 ? (nq + per - 1) / per : 1;  // no empty trailing blocks
+#define FA_E(SC, ACC, FIN)                                                                                   \
+    hipLaunchKernelGGL((k_fold_f32_even<U, C, SC, ACC, FIN>), dim3((unsigned)grid), dim3(kBlock), 0, st, X, N, P, \
+                       ldx, a, s, acc_in, d, out, per)
+    if constexpr (!ALLF) {
+        if (sc) FA_E(true, false, true); else FA_E(false, false, true);
+    } else if (sc) {
+        if (acc) { if (fin) FA_E(true, true, true); else FA_E(true, true, false); }
+        else     { if (fin) FA_E(true, false, true); else FA_E(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_E(false, true, true); else FA_E(false, true, false); }
+        else     { if (fin) FA_E(false, false, true); else FA_E(false, false, false); }
+    }
+#undef FA_E
+}
+
+// Quads per lane of the even split: the fewest that cover a block's range in
+// one chunk (up to 4); rows in flight so that a lane keeps >= 16 quad loads
+// (U*C) ahead of its adds whatever C is.
+inline int even_quads_per_lane(int64_t P, int64_t G) {
+    const int64_t nq = P >> 2;
+    const int64_t per = (nq + G - 1) / (G > 0 ? G : 1);
+    const int64_t c = (per + kBlock - 1) / kBlock;
+    return c < 1 ? 1 : (c > 4 ? 4 : (int)c);
+}
+template <bool ALLF = false>
+void launch_even_auto(hipStream_t st, int64_t G, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    switch (even_quads_per_lane(P, G)) {
+        case 1: launch_even_flags<16, 1, ALLF>(st, G, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out); break;
+        case 2: launch_even_flags<8, 2, ALLF>(st, G, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out); break;
+        case 3: launch_even_flags<8, 3, ALLF>(st, G, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out); break;
+        default: launch_even_flags<8, 4, ALLF>(st, G, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out); break;
+    }
 }
 
 // LDS-staged narrow fold: one block per TQ quads (the partial tail quad included).

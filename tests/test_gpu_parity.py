@@ -1059,3 +1059,32 @@ def test_band_variants_multi_band(dev, lib, P):
     lib.check(L.fa_fold_f32(X[2].data_ptr(), 1, P, P, a[2:].data_ptr(), None, acc.data_ptr(), div, 1,
                             acc.data_ptr(), st), "f")
     assert _bits_equal(acc.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("N", [1, 2, 7, 8, 9, 15, 16, 17, 33, 100])
+@pytest.mark.parametrize("P", [4, 7, 260, 1028, 4 * 256 * 256 + 3, 300001, 800000])
+def test_even_split_client_and_column_edges(dev, lib, N, P):
+    """k_fold_f32_even (the even-split fold): client counts around its U rows
+    in flight (row indices clamped, adds of rows past N skipped) and column
+    ranges that end inside a lane's C quads (clamped quads never stored),
+    stall-aware and plain, bit-exact against the C oracle."""
+    B = lib.load_bench()
+    names = [B.fa_variant_name(v).decode() for v in range(B.fa_num_variants())]
+    evens = [v for v, n in enumerate(names) if n.startswith("even_")]
+    assert len(evens) >= 8
+    X = torch.from_numpy(synth.clients_f32(500 + N, N, 0, P)).to(dev)
+    w = synth.cardinalities(500 + N, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(500 + N, N, 10, 2)]
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Xh = X.cpu().numpy()
+    for sp in (None, s):
+        exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)),
+                            s=None if sp is None else np.array(sc, np.float32))
+        for v in evens:
+            o = _sentinel(P, dev)
+            _bcheck(B.fa_fedavg_f32_variant(X.data_ptr(), N, P, P, a.data_ptr(), None if sp is None else sp.data_ptr(),
+                                            div, o.data_ptr(), st, v), "variant")
+            assert _bits_equal(o.cpu().numpy(), exp), (names[v], N, P, sp is None)
