@@ -1407,7 +1407,8 @@ int cu_count() {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
-enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4, kGsBalC2, kGsBalC4 };
+enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
+                     kTileC4Plain, kGsBalC2, kGsBalC4 };
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
         case F32Pick::kLdsW2T16: return "lds_w2_t16";
@@ -1419,6 +1420,7 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kColumn: return "column";
         case F32Pick::kTileC1: return "tile_4k";
         case F32Pick::kTileC4: return "tile_16k";
+        case F32Pick::kTileC4Plain: return "tile_16k_ps";
         case F32Pick::kGsBalC2: return "gs_bal_8k";
         case F32Pick::kGsBalC4: return "gs_bands_16k";
     }
@@ -1458,6 +1460,12 @@ inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
     // would leave CUs idle; the picks below spread the columns over more blocks
     const bool under = 10 * tiles4 < 7 * cus, mid = 10 * tiles4 < 9 * cus;
     if (N >= 256 && under) return F32Pick::kLdsW8;
+    // 48+ clients at 0.7-1 tiles per CU: one block per 16 KiB tile, 8 rows x 4
+    // quads ahead, plain stores (round-3 sweep of 15 forms over 42 shapes,
+    // profiles/r03_even/: best or within 2 % at 740K-1M params for 64-1024
+    // clients, where the 4 KiB tile and 8 KiB balanced picks were 5-20 %
+    // behind; the even split over all CUs, k_fold_f32_even, was 10-60 % behind)
+    if (N >= 48 && !under && tiles4 < cus) return F32Pick::kTileC4Plain;
     // Between 0.7 and 0.9 tiles per CU every form swings by up to 25 % with the
     // model size (1024 x 700K-1M in 10-40K steps, profiles/r02_small_n/pitch_scan*;
     // extra row padding changes nothing, pitch_pad/);
@@ -1776,6 +1784,9 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
             break;
         case F32Pick::kTileC4:
             rc = launch_tile_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileC4Plain:
+            rc = launch_tile_flags<8, 4, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
         case F32Pick::kGsBalC2:
             launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

@@ -18,8 +18,11 @@ by default: on MI355X hosts the 16-thread pack fully overlaps the DMA, and one
 copy per chunk beat one copy per layer; it pays where host memcpy
 bandwidth, not PCIe, is the limit.
 
-Memory: 2 pinned + 2 device chunks of chunk_rows x P floats and one [P]
-accumulator, independent of the number of clients.
+Memory: `slots` pinned + `slots` device chunks of chunk_rows x P floats (2 by
+default; FEDAVG_STREAM_SLOTS overrides) and one [P] accumulator, independent of
+the number of clients.  More, smaller chunks shorten the exposed tail of a
+round (the last chunk's DMA and fold run after the last row arrives) at the
+cost of more copies and launches.
 """
 from __future__ import annotations
 
@@ -47,38 +50,39 @@ class StreamingFold:
     stats = {"direct_rows": 0, "packed_rows": 0}
 
     def __init__(self, P: int, chunk_rows: int = 16, device: Optional[torch.device] = None,
-                 pitch_align: int = 64, direct: bool = False):
+                 pitch_align: int = 64, direct: bool = False, slots: Optional[int] = None):
         if P <= 0:
             raise InvalidParameterShapeError("StreamingFold needs P > 0")
         self.P = P
         self.dev = device or torch.device("cuda", torch.cuda.current_device())
         self.ldx = ((P + pitch_align - 1) // pitch_align) * pitch_align
         self.R = max(1, chunk_rows)
-        self.host = [torch.empty((self.R, self.ldx), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        K = self.K = max(2, slots if slots is not None else int(os.environ.get("FEDAVG_STREAM_SLOTS", "2")))
+        self.host = [torch.empty((self.R, self.ldx), dtype=torch.float32, pin_memory=True) for _ in range(K)]
         # per-chunk factors [a; s] travel with the chunk's rows on the copy
         # stream, from pinned memory (a pageable H2D could stall the producer)
-        self.fac_host = [torch.empty((2, self.R), dtype=torch.float32, pin_memory=True) for _ in range(2)]
-        self.fac_dev = [torch.empty((2, self.R), dtype=torch.float32, device=self.dev) for _ in range(2)]
-        self.devbuf = [torch.empty((self.R, self.ldx), dtype=torch.float32, device=self.dev) for _ in range(2)]
+        self.fac_host = [torch.empty((2, self.R), dtype=torch.float32, pin_memory=True) for _ in range(K)]
+        self.fac_dev = [torch.empty((2, self.R), dtype=torch.float32, device=self.dev) for _ in range(K)]
+        self.devbuf = [torch.empty((self.R, self.ldx), dtype=torch.float32, device=self.dev) for _ in range(K)]
         self.acc = torch.empty(P, dtype=torch.float32, device=self.dev)
         self.copy_stream = torch.cuda.Stream(device=self.dev)
         self.compute = torch.cuda.current_stream(self.dev)
-        self.h2d_done = [torch.cuda.Event() for _ in range(2)]
-        self.fold_done = [torch.cuda.Event() for _ in range(2)]
-        self.fold_pending = [False, False]
+        self.h2d_done = [torch.cuda.Event() for _ in range(K)]
+        self.fold_done = [torch.cuda.Event() for _ in range(K)]
+        self.fold_pending = [False] * K
         self.buf = 0
         self.fill = 0
         self.weights: List = []
         self.scored: Optional[bool] = None
-        self.chunk_a: List = [[], []]
-        self.chunk_s: List = [[], []]
+        self.chunk_a: List = [[] for _ in range(K)]
+        self.chunk_s: List = [[] for _ in range(K)]
         self.started = False
         self.rows = 0
         # per chunk: source layers and their byte offsets inside the pinned chunk
-        self.srcs: List = [[], []]
+        self.srcs: List = [[] for _ in range(K)]
         # per chunk: which rows were DMA'd directly, and the arrays those copies read
-        self.row_direct: List = [[], []]
-        self.keep: List = [[], []]
+        self.row_direct: List = [[] for _ in range(K)]
+        self.keep: List = [[] for _ in range(K)]
         self.direct = direct
         self.direct_rows = 0
         self.threads = int(os.environ.get("FEDAVG_COPY_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -190,18 +194,18 @@ class StreamingFold:
         self.chunk_a[b], self.chunk_s[b] = [], []
         self.row_direct[b] = []
         self.fill = 0
-        self.buf ^= 1
+        self.buf = (self.buf + 1) % self.K
 
     def finish(self, total=None) -> torch.Tensor:
         """Fold the last partial chunk and divide by fl32(total or sum(weights))."""
         if self.rows == 0:
             _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
         self._flush(finalize=True, total=total)
-        if self.keep[0] or self.keep[1]:
+        if any(self.keep):
             # direct copies read the callers' arrays: they must be done before
             # the caller may free them
             self.copy_stream.synchronize()
-            self.keep = [[], []]
+            self.keep = [[] for _ in range(self.K)]
         return self.acc
 
 

@@ -400,7 +400,9 @@ def test_lds_tile_picks(dev, lib, N, P):
 
 @pytest.mark.parametrize("N,P", [(10, 582026), (47, 262147), (1, 300_000), (30, 1_000_003), (100, 582026),
                                  (48, 262147), (111, 700_001), (112, 582026), (64, 300_001),
-                                 (10, 4 * 1024 * 1024 + 5), (23, 1024 * 1024 * 2 + 7)])
+                                 (10, 4 * 1024 * 1024 + 5), (23, 1024 * 1024 * 2 + 7),
+                                 # the round-3 16 KiB plain-store tile pick (48+ clients, 0.7-1 tiles per CU)
+                                 (48, 786_001), (64, 800_002), (100, 1_000_003), (130, 740_001)])
 def test_few_client_tile_picks(dev, lib, N, P):
     """The few-client picks (a block per 4 KiB tile below one tile per CU; one
     lane per column at 48-111 clients below 3/4 of a tile per CU; a block per

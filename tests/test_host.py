@@ -67,16 +67,19 @@ def test_library_variant_table():
 # the BASELINE configs and the shapes whose sweeps set each boundary.
 _PICKS = [
     ((1024, 10_000_000), "gs_bands_16k"),  # C3 (headline)
-    ((100, 1_000_000), "gs_bands_16k"),    # C2: 245 of 256 CUs get a tile
+    ((100, 1_000_000), "tile_16k_ps"),     # C2: 245 tiles, 48+ clients at 0.7-1 tiles per CU
     ((512, 25_000_000), "gs_bands_16k"),   # C5
     ((256, 12_500_000), "gs_bands_16k"),   # a C4 bucket as fp32
     ((10, 582_026), "tile_4k"),            # C1 (config 1's MNIST CNN)
     ((32, 1_000_000), "tile_4k"),          # < 64 clients below one tile per CU
     ((200, 600_000), "tile_4k"),           # < 0.7 tiles per CU
     ((100, 582_026), "column"),            # 48-111 clients, < 0.6 tiles per CU
-    ((64, 786_000), "column"),             # 48-79 clients, < 0.9 tiles per CU
-    ((100, 786_000), "tile_4k"),           # 80-111 clients at 0.7-0.9
-    ((1024, 786_000), "gs_bal_8k"),        # 112+ clients at 0.7-0.9
+    ((64, 786_000), "tile_16k_ps"),        # 48+ clients at 0.7-1 tiles per CU (round 3)
+    ((100, 786_000), "tile_16k_ps"),
+    ((1024, 786_000), "tile_16k_ps"),
+    ((40, 786_000), "tile_4k"),            # < 48 clients at 0.7-0.9
+    ((64, 600_000), "column"),             # 48-79 clients below 0.7 tiles per CU
+    ((1024, 1_000_000), "tile_16k_ps"),
     ((100, 1_500_000), "gs_bal_8k"),       # 1-2 tiles per CU
     ((1024, 582_026), "lds_w8_t32"),       # 256+ clients below 0.7
     ((10, 10_000_000), "tile_16k"),        # < 24 clients above one tile per CU
