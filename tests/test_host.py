@@ -501,6 +501,9 @@ def test_fa_crc32_matches_zlib():
                     assert L.fa_crc32(v.ctypes.data if n else None, n, crc_in, T, ctypes.byref(out)) == 0
                     assert out.value == zlib.crc32(v.tobytes(), crc_in), (n, off, crc_in, T)
     assert L.fa_crc32(None, 5, 0, 1, ctypes.byref(out)) == _lib.FA_ERR_ARG
+    assert "fa_crc32" in _lib.last_error()  # the host entries set the error text too
+    assert L.fa_pack(None, None, None, None, 3, 1) == _lib.FA_ERR_ARG
+    assert "fa_pack" in _lib.last_error()
 
 
 def test_npz_writer_is_byte_identical_to_savez():
@@ -669,3 +672,23 @@ def test_openwhisk_entry_point(oracle_fold):
     # a body that is neither JSON nor base64 -> binascii.Error -> 400
     resp = main({"__ow_body": "abc", "__ow_method": "post"})
     assert resp["statusCode"] == 400 and json.loads(resp["body"])["errorType"] == "Error"
+
+
+def test_serialize_without_the_native_library(monkeypatch):
+    """A process that only saves a model needs no HIP library: write_npz
+    declines and NpzWeightsSerializer.serialize falls back to np.savez (the
+    same bytes)."""
+    import io
+    from fedlesscan_amd import npz
+    from fedlesscan_amd.aggregator.exceptions import AggregationError
+    from fedlesscan_amd.common.serialization import NpzWeightsSerializer
+
+    def missing(*a, **k):
+        raise AggregationError("HIP extension not built")
+
+    monkeypatch.setattr(_lib, "load", missing)
+    arrs = [np.arange(12, dtype=np.float32).reshape(3, 4), np.ones(5, np.float64)]
+    assert npz.write_npz(arrs) is None
+    f = io.BytesIO()
+    np.savez(f, *arrs)
+    assert NpzWeightsSerializer().serialize(arrs) == f.getvalue()
