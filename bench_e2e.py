@@ -117,8 +117,9 @@ def main():
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     t_gpu = sorted(ts)[len(ts) // 2]
-    from fedlesscan_amd.ingest import StreamingFold
+    from fedlesscan_amd.ingest import NATIVE_INGEST, NativeStreamingFold, StreamingFold
     routes = dict(StreamingFold.stats)
+    routes["native_pipe_rows"] = NativeStreamingFold.stats["rows"]
 
     # decode-only (zero-copy views) and pinned H2D of the same bytes
     from fedlesscan_amd.npz import read_layers
@@ -143,8 +144,9 @@ def main():
         "clients": N, "params": P, "input_bytes": in_bytes, "gen_s": round(gen_s, 1),
         "gpu_e2e_s": round(t_gpu, 4), "gpu_e2e_gbs": round(in_bytes / t_gpu / 1e9, 2),
         "gpu_e2e_min_s": round(min(ts), 4), "gpu_e2e_max_s": round(max(ts), 4),
-        "stream_chunk_mb": int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "64")),
-        "stream_slots": int(os.environ.get("FEDAVG_STREAM_SLOTS", "2")),
+        "stream_chunk_mb": int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "16")),
+        "stream_slots": int(os.environ.get("FEDAVG_STREAM_SLOTS", "0")) or None,
+        "ingest": "native pipe (fa_ingest_*)" if NATIVE_INGEST and not a.pinned_store else "python StreamingFold",
         "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),
         "ingest_rows": routes,
     }

@@ -1,0 +1,416 @@
+// ingest_pipe.cpp — native streaming ingest for libfedavg_hip.so:
+// client rows in host memory -> packed into page-locked slots by a persistent
+// worker pool -> one DMA per slot on a copy stream -> the in-order chunked fold
+// (fa_fold_f32) on the caller's compute stream.
+//
+// Reference path replaced: the strategies' aggregate() materialises every
+// decoded client (fed_avg_aggregator.py:64-92, stall_aware_aggregation.py:
+// 82-117) and then folds on one core.  Here the caller hands over each
+// decoded row as soon as it has it (fa_ingest_add returns once the row's copy
+// tasks are queued): decoding row i+1 (caller), packing rows i, i-1, ...
+// (workers), the DMA of the previous slot (copy engine) and the fold of the
+// one before (GPU) all overlap.  Slots are filled and folded strictly in row
+// order with the accumulator carried across them, so the result is
+// bit-identical to one fa_fedavg_f32 over all rows (the property fa_fold_f32
+// documents).
+//
+// Threads: the caller's thread (add / finish, which block only for
+// backpressure: a slot is refilled after its fold has completed), one issuer
+// thread per pipe (waits for a full slot's packs, then enqueues its DMA and
+// fold: the HIP calls stay in slot order) and a process-wide pool of copy
+// workers shared by every pipe (one pipe per GPU for the multi-GPU drop-in).
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fedavg_hip.h"
+
+__attribute__((visibility("hidden"))) int fa_internal_fail(int code, const char* msg);
+
+namespace {
+
+// ---- process-wide copy workers ------------------------------------------------
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool pool;
+        return pool;
+    }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (workers_.empty()) start();
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void start() {  // under mu_
+        int n = 16;  // the GPU box's CPU share of one GPU; FEDAVG_COPY_THREADS overrides
+        if (const char* e = getenv("FEDAVG_COPY_THREADS")) n = std::max(1, atoi(e));
+        n = std::min<int>(n, std::max(1u, std::thread::hardware_concurrency()));
+        for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;  // stop_
+            std::function<void()> f = std::move(q_.front());
+            q_.pop_front();
+            lk.unlock();
+            f();
+            lk.lock();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> workers_;
+    bool stop_ = false;
+};
+
+constexpr int64_t kTaskBytes = 1 << 20;  // one copy task: >= 1 MiB keeps the pool's overhead small
+
+enum class SlotState { kFree, kFilling, kQueued, kIssued };
+
+struct Slot {
+    float* host = nullptr;      // [R][ldx] page-locked
+    float* dev = nullptr;       // [R][ldx]
+    float* fac_host = nullptr;  // [2][R] page-locked: a, then s
+    float* fac_dev = nullptr;   // [2][R]
+    hipEvent_t h2d_done = nullptr, fold_done = nullptr;
+    SlotState state = SlotState::kFree;
+    int64_t rows = 0;
+    bool has_s = false;
+    std::atomic<int64_t> outstanding{0};  // copy tasks not yet finished
+};
+
+struct QueueItem {
+    int slot;  // -1: finalize only (every row already folded)
+    bool final_chunk;
+};
+
+}  // namespace
+
+struct fa_ingest {
+    int64_t P = 0, ldx = 0, R = 0;
+    int K = 0, device = 0;
+    std::vector<Slot> slots;
+    hipStream_t copy = nullptr;
+    // per round
+    float* acc = nullptr;
+    hipStream_t compute = nullptr;
+    int cur = 0;
+    int64_t rows = 0;
+    bool started = false;  // acc holds a partial fold (issuer side)
+    int scored = -1;       // -1 unknown, 0 FedAvg, 1 stall-aware
+    float divisor = 0.f;
+    // issuer
+    std::thread issuer;
+    std::mutex mu;
+    std::condition_variable cv;       // issuer wake-up, slot state changes, pack completion
+    std::deque<QueueItem> queue;
+    int in_flight = 0;                // queue items not yet issued
+    bool stop = false;
+    int err = FA_OK;
+    std::string errmsg;
+};
+
+namespace {
+
+int set_err(fa_ingest* p, int code, const std::string& msg) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->err == FA_OK) {
+        p->err = code;
+        p->errmsg = msg;
+    }
+    p->cv.notify_all();
+    return code;
+}
+
+int hip_err(fa_ingest* p, const char* what, hipError_t e) {
+    return set_err(p, FA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Issue one full slot (or the finalize-only step) on the streams.  Runs on the
+// issuer thread, in queue (= row) order.
+int issue(fa_ingest* p, const QueueItem& it) {
+    if (it.slot < 0) {  // every row was in earlier slots: divide only
+        return fa_fold_f32(nullptr, 0, p->P, p->ldx, nullptr, nullptr, p->acc, p->divisor, 1, p->acc, p->compute);
+    }
+    Slot& S = p->slots[it.slot];
+    {
+        std::unique_lock<std::mutex> lk(p->mu);
+        p->cv.wait(lk, [&] { return S.outstanding.load() == 0 || p->err != FA_OK; });
+        if (p->err != FA_OK) return p->err;
+    }
+    hipError_t e = hipMemcpyAsync(S.dev, S.host, (size_t)(S.rows * p->ldx) * sizeof(float), hipMemcpyHostToDevice,
+                                  p->copy);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(S.fac_dev, S.fac_host, (size_t)(2 * p->R) * sizeof(float), hipMemcpyHostToDevice, p->copy);
+    if (e == hipSuccess) e = hipEventRecord(S.h2d_done, p->copy);
+    if (e == hipSuccess) e = hipStreamWaitEvent(p->compute, S.h2d_done, 0);
+    if (e != hipSuccess) return hip_err(p, "ingest H2D", e);
+    const int rc = fa_fold_f32(S.dev, S.rows, p->P, p->ldx, S.fac_dev, S.has_s ? S.fac_dev + p->R : nullptr,
+                               p->started ? p->acc : nullptr, it.final_chunk ? p->divisor : 0.f,
+                               it.final_chunk ? 1 : 0, p->acc, p->compute);
+    if (rc != FA_OK) return set_err(p, rc, std::string("ingest fold: ") + fa_last_error());
+    p->started = true;
+    e = hipEventRecord(S.fold_done, p->compute);
+    if (e != hipSuccess) return hip_err(p, "ingest event", e);
+    return FA_OK;
+}
+
+void issuer_loop(fa_ingest* p) {
+    (void)hipSetDevice(p->device);
+    std::unique_lock<std::mutex> lk(p->mu);
+    for (;;) {
+        p->cv.wait(lk, [&] { return p->stop || !p->queue.empty(); });
+        if (p->queue.empty()) return;  // stop
+        const QueueItem it = p->queue.front();
+        p->queue.pop_front();
+        const bool ok = p->err == FA_OK;  // after a failure the rest of the round is drained, not issued
+        lk.unlock();
+        const int rc = ok ? issue(p, it) : FA_OK;
+        lk.lock();
+        if (it.slot >= 0) p->slots[it.slot].state = SlotState::kIssued;
+        if (rc != FA_OK && p->err == FA_OK) {
+            p->err = rc;
+            p->errmsg = fa_last_error();
+        }
+        --p->in_flight;
+        p->cv.notify_all();
+    }
+}
+
+void enqueue(fa_ingest* p, int slot, bool final_chunk) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (slot >= 0) p->slots[slot].state = SlotState::kQueued;
+    p->queue.push_back({slot, final_chunk});
+    ++p->in_flight;
+    p->cv.notify_all();
+}
+
+// Wait until slot k may be refilled: its previous contents were issued and
+// their fold has completed.
+int claim(fa_ingest* p, int k) {
+    Slot& S = p->slots[k];
+    {
+        std::unique_lock<std::mutex> lk(p->mu);
+        p->cv.wait(lk, [&] { return S.state != SlotState::kQueued || p->err != FA_OK; });
+        if (p->err != FA_OK) return p->err;
+    }
+    if (S.state == SlotState::kIssued) {
+        hipError_t e = hipEventSynchronize(S.fold_done);
+        if (e != hipSuccess) return hip_err(p, "ingest slot wait", e);
+    }
+    S.state = SlotState::kFilling;
+    S.rows = 0;
+    return FA_OK;
+}
+
+void free_slots(fa_ingest* p) {
+    for (Slot& S : p->slots) {
+        if (S.fold_done) (void)hipEventSynchronize(S.fold_done);
+        if (S.h2d_done) (void)hipEventDestroy(S.h2d_done);
+        if (S.fold_done) (void)hipEventDestroy(S.fold_done);
+        if (S.host) (void)hipHostFree(S.host);
+        if (S.fac_host) (void)hipHostFree(S.fac_host);
+        if (S.dev) (void)hipFree(S.dev);
+        if (S.fac_dev) (void)hipFree(S.fac_dev);
+    }
+    if (p->copy) (void)hipStreamDestroy(p->copy);
+}
+
+int report(fa_ingest* p) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->err == FA_OK) return FA_OK;
+    return fa_internal_fail(p->err, p->errmsg.c_str());
+}
+
+}  // namespace
+
+extern "C" {
+
+int fa_ingest_create(fa_ingest** out, int64_t P, int64_t chunk_bytes, int slots, int device) {
+    if (!out || P <= 0 || chunk_bytes <= 0 || slots < 2 || slots > 64 || device < 0)
+        return fa_internal_fail(FA_ERR_ARG, "fa_ingest_create: bad arguments");
+    *out = nullptr;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fa_internal_fail(FA_ERR_HIP, "fa_ingest_create: cannot select the device");
+    }
+    fa_ingest* p = new fa_ingest();
+    p->P = P;
+    p->ldx = (P + 63) / 64 * 64;  // 256-B row pitch: the vector folds
+    p->R = std::max<int64_t>(1, chunk_bytes / (p->ldx * (int64_t)sizeof(float)));
+    p->K = slots;
+    p->device = device;
+    p->slots = std::vector<Slot>(slots);
+    hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
+    for (Slot& S : p->slots) {
+        const size_t rowbytes = (size_t)(p->R * p->ldx) * sizeof(float), facbytes = (size_t)(2 * p->R) * sizeof(float);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&S.host, rowbytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&S.fac_host, facbytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void**)&S.dev, rowbytes);
+        if (e == hipSuccess) e = hipMalloc((void**)&S.fac_dev, facbytes);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.h2d_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.fold_done, hipEventDisableTiming);
+        if (e == hipSuccess) memset(S.fac_host, 0, facbytes);
+    }
+    if (e != hipSuccess) {
+        const std::string msg = std::string("fa_ingest_create: ") + hipGetErrorString(e);
+        free_slots(p);
+        delete p;
+        (void)hipSetDevice(prev);
+        return fa_internal_fail(FA_ERR_HIP, msg.c_str());
+    }
+    p->issuer = std::thread(issuer_loop, p);
+    (void)hipSetDevice(prev);
+    *out = p;
+    return FA_OK;
+}
+
+int fa_ingest_rows_per_chunk(const fa_ingest* p) { return p ? (int)p->R : 0; }
+
+int fa_ingest_begin(fa_ingest* p, float* acc, void* stream) {
+    if (!p || !acc) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: bad arguments");
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (p->in_flight) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: previous round not finished");
+        p->err = FA_OK;
+        p->errmsg.clear();
+    }
+    p->acc = acc;
+    p->compute = (hipStream_t)stream;
+    p->cur = 0;
+    p->rows = 0;
+    p->started = false;
+    p->scored = -1;
+    return FA_OK;
+}
+
+int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, int64_t n, float a, float s,
+                  int has_s) {
+    if (!p || n < 0 || (n > 0 && (!srcs || !sizes))) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_add: bad arguments");
+    if (p->scored >= 0 && p->scored != (has_s ? 1 : 0))
+        return fa_internal_fail(FA_ERR_SHAPE, "either every row has a score or none does");
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (sizes[i] < 0 || (sizes[i] && !srcs[i])) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_add: bad piece");
+        total += sizes[i];
+    }
+    if (total != p->P * (int64_t)sizeof(float))
+        return fa_internal_fail(FA_ERR_SHAPE, "fa_ingest_add: row bytes != P * 4");
+    if (int rc = report(p)) return rc;
+    p->scored = has_s ? 1 : 0;
+    Slot& S = p->slots[p->cur];
+    if (S.state != SlotState::kFilling && claim(p, p->cur) != FA_OK) return report(p);
+    const int64_t r = S.rows++;
+    S.has_s = has_s != 0;
+    S.fac_host[r] = a;
+    S.fac_host[p->R + r] = has_s ? s : 1.0f;
+    // copy tasks of >= 1 MiB, split across pieces and inside large pieces
+    uint8_t* dst = reinterpret_cast<uint8_t*>(S.host + r * p->ldx);
+    int64_t off = 0;
+    struct Part { const uint8_t* src; uint8_t* dst; int64_t n; };
+    std::vector<Part> batch;
+    int64_t batch_bytes = 0;
+    auto flush = [&] {
+        if (batch.empty()) return;
+        S.outstanding.fetch_add(1);
+        CopyPool::get().submit([p, &S, parts = std::move(batch)] {
+            for (const Part& q : parts) memcpy(q.dst, q.src, (size_t)q.n);
+            // decrement under the pipe's lock: once a waiter sees 0 this task no longer touches the pipe
+            std::lock_guard<std::mutex> lk(p->mu);
+            if (S.outstanding.fetch_sub(1) == 1) p->cv.notify_all();
+        });
+        batch = std::vector<Part>();
+        batch_bytes = 0;
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* src = (const uint8_t*)srcs[i];
+        for (int64_t done = 0; done < sizes[i];) {
+            const int64_t take = std::min(sizes[i] - done, kTaskBytes - batch_bytes);
+            batch.push_back({src + done, dst + off, take});
+            batch_bytes += take;
+            done += take;
+            off += take;
+            if (batch_bytes >= kTaskBytes) flush();
+        }
+    }
+    flush();
+    ++p->rows;
+    if (S.rows == p->R) {
+        enqueue(p, p->cur, false);
+        p->cur = (p->cur + 1) % p->K;
+    }
+    return FA_OK;
+}
+
+int fa_ingest_finish(fa_ingest* p, float divisor) {
+    if (!p) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_finish: bad arguments");
+    if (p->rows == 0) return fa_internal_fail(FA_ERR_NO_CLIENTS, "no client results to aggregate (N == 0)");
+    p->divisor = divisor;  // read by the issuer for the final item, which is queued below
+    Slot& S = p->slots[p->cur];
+    if (S.state == SlotState::kFilling && S.rows > 0) {
+        enqueue(p, p->cur, true);
+        p->cur = (p->cur + 1) % p->K;
+    } else {
+        enqueue(p, -1, true);
+    }
+    {
+        std::unique_lock<std::mutex> lk(p->mu);
+        p->cv.wait(lk, [&] { return p->in_flight == 0; });  // every pack done, every DMA and fold enqueued
+    }
+    return report(p);
+}
+
+int fa_ingest_destroy(fa_ingest* p) {
+    if (!p) return FA_OK;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->stop = true;
+    }
+    p->cv.notify_all();
+    if (p->issuer.joinable()) p->issuer.join();
+    {  // copy tasks still running read from the caller's rows and write the slots
+        std::unique_lock<std::mutex> lk(p->mu);
+        p->cv.wait(lk, [&] {
+            for (const Slot& S : p->slots)
+                if (S.outstanding.load() != 0) return false;
+            return true;
+        });
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(p->device);
+    free_slots(p);
+    (void)hipSetDevice(prev);
+    delete p;
+    return FA_OK;
+}
+
+}  // extern "C"

@@ -490,10 +490,10 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
     return outs
 
 
-# pinned staging per chunk (two chunks in flight); FEDAVG_STREAM_CHUNK_MB overrides.
-# 64 MB measured best on MI355X: 100x1M 9.6 ms (41 GB/s) against
-# 15.3 ms at 256 MB (too few chunks to overlap); 100x10M 76 ms (52.5 GB/s).
-STREAM_CHUNK_BYTES = int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "64")) << 20
+# pinned staging per chunk; FEDAVG_STREAM_CHUNK_MB overrides.  The native pipe
+# (ingest.NativeStreamingFold, round 3) keeps 4 chunks in flight; the
+# Python-driven StreamingFold (direct DMA) keeps 2 of 64 MB.
+STREAM_CHUNK_BYTES = int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "16")) << 20
 # DMA layers straight from page-locked documents instead of packing them
 # (StreamingFold direct=True); FEDAVG_DIRECT_DMA=1 turns it on.
 DIRECT_DMA = os.environ.get("FEDAVG_DIRECT_DMA", "0") == "1"
@@ -547,9 +547,8 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
             from .multigpu import MultiStreamingFold
             sf = MultiStreamingFold(P, multi, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
         else:
-            from .ingest import StreamingFold
-            sf = StreamingFold(P, chunk_rows=max(1, STREAM_CHUNK_BYTES // (4 * P)),
-                               device=device or default_device(), direct=DIRECT_DMA)
+            from .ingest import make_streaming_fold
+            sf = make_streaming_fold(P, device or default_device(), STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
         sf.add(list(first[0]), first[1], None if scores is None else scores[0])
         for layers, w in it:
             rows.append(layers)
@@ -588,9 +587,8 @@ def to_host(t: torch.Tensor) -> np.ndarray:
 
 
 def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
-    from .ingest import StreamingFold
-    rows = max(1, min(n, STREAM_CHUNK_BYTES // (4 * P)))
-    sf = StreamingFold(P, chunk_rows=rows, device=dev, direct=DIRECT_DMA)
+    from .ingest import make_streaming_fold
+    sf = make_streaming_fold(P, dev, min(STREAM_CHUNK_BYTES, max(1, n) * 4 * P), direct=DIRECT_DMA)
     for i in range(n):
         sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
     return sf.finish(total=total)

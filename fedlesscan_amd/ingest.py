@@ -26,7 +26,10 @@ cost of more copies and launches.
 """
 from __future__ import annotations
 
+import collections
+import ctypes
 import os
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -207,6 +210,159 @@ class StreamingFold:
             self.copy_stream.synchronize()
             self.keep = [[] for _ in range(self.K)]
         return self.acc
+
+
+class _PipeCache:
+    """Native ingest pipes (fa_ingest_*) kept across rounds: a pipe owns
+    page-locked and device chunks and an issuer thread, so it is created once
+    per (device, P, chunk size, slots) and reused; a pipe serves one round at a
+    time (a concurrent round gets its own), and at most MAX idle pipes are
+    kept per process."""
+
+    MAX = 4
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.idle: "collections.OrderedDict" = collections.OrderedDict()  # key -> [pipe, ...]
+
+    def get(self, key):
+        with self.lock:
+            pipes = self.idle.get(key)
+            if pipes:
+                p = pipes.pop()
+                if not pipes:
+                    del self.idle[key]
+                return p
+        dev, P, chunk_bytes, slots = key
+        h = ctypes.c_void_p()
+        _lib.call("fa_ingest_create", ctypes.byref(h), P, chunk_bytes, slots, dev)
+        return h
+
+    def put(self, key, pipe):
+        with self.lock:
+            self.idle.setdefault(key, []).append(pipe)
+            self.idle.move_to_end(key)
+            n = sum(len(v) for v in self.idle.values())
+            while n > self.MAX:
+                k, v = next(iter(self.idle.items()))
+                _lib.load().fa_ingest_destroy(v.pop())
+                if not v:
+                    del self.idle[k]
+                n -= 1
+
+    @staticmethod
+    def drop(pipe):
+        _lib.load().fa_ingest_destroy(pipe)
+
+
+_pipes = _PipeCache()
+
+
+class NativeStreamingFold:
+    """StreamingFold on the native pipe (libfedavg_hip.so fa_ingest_*): the
+    same add(row, weight, score) / finish(total) contract and bit-identical
+    result, with the packing done by the library's copy workers and the DMA and
+    fold issued by its own thread, so add() returns as soon as the row's copies
+    are queued and decoding the next row overlaps everything else.  The rows'
+    arrays are kept alive until finish() (the workers read them)."""
+
+    stats = {"rows": 0}
+
+    def __init__(self, P: int, device: Optional[torch.device] = None, chunk_bytes: int = 16 << 20,
+                 slots: int = 4):
+        if P <= 0:
+            raise InvalidParameterShapeError("StreamingFold needs P > 0")
+        self.P = P
+        self.dev = device or torch.device("cuda", torch.cuda.current_device())
+        if self.dev.index is None:
+            self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.key = (self.dev.index, P, int(chunk_bytes), int(slots))
+        self.pipe = _pipes.get(self.key)
+        self.acc = torch.empty(P, dtype=torch.float32, device=self.dev)
+        self.L = _lib.load()
+        try:
+            _lib.check(self.L.fa_ingest_begin(self.pipe, self.acc.data_ptr(),
+                                              torch.cuda.current_stream(self.dev).cuda_stream), "fa_ingest_begin")
+        except BaseException:
+            _pipes.drop(self.pipe)
+            self.pipe = None
+            raise
+        self.keep: List = []
+        self.weights: List = []
+        self.rows = 0
+
+    def _fail(self):
+        if self.pipe is not None:  # a round that failed half-way is not reused
+            _pipes.drop(self.pipe)
+            self.pipe = None
+        self.keep = []
+
+    def add(self, row, weight, score: Optional[float] = None):
+        if self.pipe is None:
+            raise InvalidParameterShapeError("this StreamingFold failed earlier")
+        pieces = row if isinstance(row, (list, tuple)) else [row]
+        arrs = []
+        for layer in pieces:
+            arr = np.ascontiguousarray(layer)
+            if arr.dtype != np.float32:
+                self._fail()
+                raise InvalidParameterShapeError(f"StreamingFold takes float32 rows, got {arr.dtype}")
+            arrs.append(arr)
+        n = len(arrs)
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        sizes = (ctypes.c_int64 * n)(*[a.nbytes for a in arrs])
+        a = float(np.float32(weight))  # fl32(n_i): numpy's rounding of the Python scalar
+        s = 1.0 if score is None else float(np.float32(score))
+        rc = self.L.fa_ingest_add(self.pipe, ptrs, sizes, n, a, s, 0 if score is None else 1)
+        if rc:
+            err = _lib.last_error()
+            self._fail()
+            if rc == _lib.FA_ERR_SHAPE:
+                raise InvalidParameterShapeError(f"fa_ingest_add: {err}")
+            _lib.check(rc, "fa_ingest_add")
+        self.keep.append(arrs)
+        self.weights.append(weight)
+        self.rows += 1
+        NativeStreamingFold.stats["rows"] += 1
+
+    def finish(self, total=None) -> torch.Tensor:
+        if self.pipe is None:
+            raise InvalidParameterShapeError("this StreamingFold failed earlier")
+        if self.rows == 0:
+            self._fail()
+            _lib.check(_lib.FA_ERR_NO_CLIENTS, "StreamingFold.finish")
+        div = float(np.float32(sum(self.weights) if total is None else total))
+        rc = self.L.fa_ingest_finish(self.pipe, div)
+        if rc:
+            err = _lib.last_error()
+            self._fail()
+            _lib.check(rc, f"fa_ingest_finish ({err})")
+        _pipes.put(self.key, self.pipe)  # every copy is done: the rows are no longer read
+        self.pipe = None
+        self.keep = []
+        return self.acc
+
+    def __del__(self):
+        if getattr(self, "pipe", None) is not None:  # abandoned mid-round
+            try:
+                _pipes.drop(self.pipe)
+            except Exception:
+                pass
+
+
+# native pipe by default; FEDAVG_NATIVE_INGEST=0 selects the Python-driven StreamingFold
+NATIVE_INGEST = os.environ.get("FEDAVG_NATIVE_INGEST", "1") == "1"
+STREAM_SLOTS = int(os.environ.get("FEDAVG_STREAM_SLOTS", "0"))  # 0: the form's default
+
+
+def make_streaming_fold(P: int, device, chunk_bytes: int, direct: bool = False):
+    """The ingest for P-float rows on `device`: the native pipe, or the
+    Python-driven StreamingFold for the direct-DMA route (page-locked
+    documents) or when FEDAVG_NATIVE_INGEST=0."""
+    if NATIVE_INGEST and not direct:
+        return NativeStreamingFold(P, device, chunk_bytes, STREAM_SLOTS or 4)
+    return StreamingFold(P, chunk_rows=max(1, chunk_bytes // (4 * P)), device=device, direct=direct,
+                         slots=STREAM_SLOTS or None)
 
 
 def stream_layers(rows_iter, shapes: Sequence[tuple], chunk_rows: int = 16, device=None):

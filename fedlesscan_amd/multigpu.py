@@ -89,7 +89,7 @@ class MultiStreamingFold:
     """
 
     def __init__(self, P: int, devices: Sequence, chunk_bytes: int = 64 << 20, direct: bool = False):
-        from .ingest import StreamingFold
+        from .ingest import make_streaming_fold
         if P <= 0:
             raise InvalidParameterShapeError("MultiStreamingFold needs P > 0")
         self.P = P
@@ -98,8 +98,7 @@ class MultiStreamingFold:
         self.folds = []
         for dev, (lo, hi) in zip(self.devices, self.bounds):
             w = hi - lo
-            self.folds.append(StreamingFold(w, chunk_rows=max(1, chunk_bytes // (4 * w)), device=dev, direct=direct)
-                              if w > 0 else None)
+            self.folds.append(make_streaming_fold(w, dev, chunk_bytes, direct=direct) if w > 0 else None)
         self.rows = 0
 
     def add(self, layers, weight, score: Optional[float] = None):

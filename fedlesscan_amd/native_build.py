@@ -26,7 +26,7 @@ CSRC = os.path.join(PKG, "csrc")
 SRC = os.path.join(CSRC, "fedavg.hip")
 BENCH_SRC = os.path.join(CSRC, "fedavg_bench.hip")
 KERNELS = os.path.join(CSRC, "fold_kernels.hpp")
-HOST_SRCS = [os.path.join(CSRC, f) for f in ("ingest_host.cpp", "bson_host.cpp")]
+HOST_SRCS = [os.path.join(CSRC, f) for f in ("ingest_host.cpp", "bson_host.cpp", "ingest_pipe.cpp")]
 HDR = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HDR = os.path.join(REPO, "include", "fedavg_hip_bench.h")
 OUT_DIR = os.path.join(PKG, "_native")

@@ -168,6 +168,36 @@ int fa_copy_h2d(void* dst, const void* src, int64_t n, void* stream);
  * device the calling thread has current. */
 int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int64_t n, void* stream);
 
+/* ---- native streaming ingest: host rows -> pinned slots -> DMA -> chunked fold --
+ * The strategies' aggregate() (fed_avg_aggregator.py:57-92,
+ * stall_aware_aggregation.py:82-117) decodes every client and then folds; here
+ * each decoded row is handed over as it is decoded.  A process-wide pool of
+ * copy workers packs rows into `slots` page-locked chunks of about chunk_bytes
+ * (whole rows, pitch P rounded up to 64 floats); one issuer thread per pipe
+ * sends each full chunk with one DMA on the pipe's copy stream and folds it on
+ * the round's compute stream with fa_fold_f32, chunks in row order, the
+ * accumulator carried across them: bit-identical to fa_fedavg_f32 over all
+ * rows.  A chunk slot is refilled only after its fold has completed.
+ *   fa_ingest_create:  allocate a pipe for models of P floats on `device`
+ *   fa_ingest_begin:   start a round folding into acc [device, P] on `stream`
+ *   fa_ingest_add:     one client row [host]: n pieces (srcs[i], sizes[i] bytes)
+ *                      that concatenate to P floats, its factors a = fl32(n_i)
+ *                      and s = fl32(score) when has_s (every row or none).  The
+ *                      pieces must stay valid until fa_ingest_finish returns.
+ *   fa_ingest_finish:  fold the last chunk and divide by `divisor`; returns when
+ *                      every copy is done and every DMA and fold is enqueued
+ *                      (the caller waits on `stream` for the result)
+ *   fa_ingest_destroy: wait for outstanding copies, free everything.
+ * The pipe is reusable round after round (begin ... finish). */
+typedef struct fa_ingest fa_ingest;
+int fa_ingest_create(fa_ingest** pipe, int64_t P, int64_t chunk_bytes, int slots, int device);
+int fa_ingest_rows_per_chunk(const fa_ingest* pipe);
+int fa_ingest_begin(fa_ingest* pipe, float* acc, void* stream);
+int fa_ingest_add(fa_ingest* pipe, const void* const* srcs, const int64_t* sizes, int64_t n, float a, float s,
+                  int has_s);
+int fa_ingest_finish(fa_ingest* pipe, float divisor);
+int fa_ingest_destroy(fa_ingest* pipe);
+
 /* ---- host-side ingest (no GPU): NPZ wire format -> pinned staging ----------
  * Client blobs are uncompressed NPZ archives (NpzWeightsSerializer,
  * serialization.py:280-306, written by the client, client.py:186-199). */

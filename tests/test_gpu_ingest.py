@@ -169,3 +169,91 @@ def test_aggregate_decoded_equals_materialised(dev, case):
     exp = engine.aggregate_layers(rows, w, scores, device=dev)
     got = engine.aggregate_decoded(iter(list(zip(rows, w))), scores, device=dev)
     assert _same_outputs(got, exp)
+
+
+# ---------------------------------------------------------------------------
+# the native pipe (fa_ingest_*, csrc/ingest_pipe.cpp): worker-pool packs, an
+# issuer thread per pipe, K chunk slots, the fold carried across them
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("chunk_rows", [1, 2, 5, 64])
+@pytest.mark.parametrize("slots", [2, 3, 7])
+@pytest.mark.parametrize("scored", [False, True])
+def test_native_pipe_bit_exact(dev, chunk_rows, slots, scored):
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    N, P = 37, 70001
+    X = synth.clients_f32(61, N, 0, P)
+    w = synth.cardinalities(61, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(61, N, 10, 2)] if scored else None
+    ldx = (P + 63) // 64 * 64
+    sf = NativeStreamingFold(P, dev, chunk_bytes=chunk_rows * ldx * 4, slots=slots)
+    sf.acc.fill_(float("nan"))
+    for i in range(N):
+        r = X[i]
+        # pieces that cross the 1 MiB copy-task boundary and tiny ones
+        sf.add([r[:3].reshape(3), r[3:29903].reshape(100, 299), r[29903:]], w[i], None if sc is None else sc[i])
+    got = sf.finish().cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    assert G.same_bits(got, exp)
+
+
+def test_native_pipe_rounds_reuse_and_concurrency(dev):
+    """A pipe serves round after round (the cache hands it back), two rounds in
+    flight at once get two pipes, the divisor override (zip truncation) and a
+    round whose rows fill the last slot exactly (finalize-only step)."""
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    N, P = 12, 4099
+    X = synth.clients_f32(62, N, 0, P)
+    w = synth.cardinalities(62, N)
+    ldx = (P + 63) // 64 * 64
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    for _ in range(3):
+        a = NativeStreamingFold(P, dev, chunk_bytes=3 * ldx * 4, slots=2)  # 12 rows = 4 full slots
+        b = NativeStreamingFold(P, dev, chunk_bytes=3 * ldx * 4, slots=2)
+        assert a.pipe.value != b.pipe.value
+        for i in range(N):
+            a.add(X[i], w[i])
+            b.add(X[N - 1 - i], w[N - 1 - i])
+        assert G.same_bits(a.finish().cpu().numpy(), exp)
+        got_b = b.finish(total=sum(w) + 5).cpu().numpy()
+        exp_b = OL.fedavg_f32(X[::-1].copy(), np.array(w[::-1], np.float32), np.float32(sum(w) + 5))
+        assert G.same_bits(got_b, exp_b)
+
+
+def test_native_pipe_errors(dev):
+    from fedlesscan_amd.aggregator.exceptions import InsufficientClientResults, InvalidParameterShapeError
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    P = 1000
+    sf = NativeStreamingFold(P, dev, chunk_bytes=1 << 20, slots=2)
+    with pytest.raises(InvalidParameterShapeError):
+        sf.add(np.zeros(999, np.float32), 1)
+    with pytest.raises(InvalidParameterShapeError):  # a failed round is not reused
+        sf.add(np.zeros(1000, np.float32), 1)
+    sf = NativeStreamingFold(P, dev, chunk_bytes=1 << 20, slots=2)
+    with pytest.raises(InvalidParameterShapeError):
+        sf.add(np.zeros(1000, np.float64), 1)
+    sf = NativeStreamingFold(P, dev, chunk_bytes=1 << 20, slots=2)
+    sf.add(np.ones(1000, np.float32), 2)
+    with pytest.raises(InvalidParameterShapeError):  # scores on some rows only
+        sf.add(np.ones(1000, np.float32), 2, 0.5)
+    sf = NativeStreamingFold(P, dev, chunk_bytes=1 << 20, slots=2)
+    with pytest.raises(InsufficientClientResults):
+        sf.finish()
+    # the next round on a fresh pipe works
+    sf = NativeStreamingFold(P, dev, chunk_bytes=1 << 20, slots=2)
+    sf.add(np.full(1000, 3, np.float32), 2)
+    assert np.all(sf.finish().cpu().numpy() == 3)
+
+
+def test_native_pipe_is_the_default_aggregate_route(dev):
+    """FedAvgAggregator.aggregate on host NPZ blobs goes through the native
+    pipe and stays bit-exact against the reference goldens."""
+    from fedlesscan_amd import FedAvgAggregator
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    from test_gpu_multigpu import _npz_results
+    case = "f32_n60"
+    m = G.manifest()[case]
+    before = NativeStreamingFold.stats["rows"]
+    out = FedAvgAggregator().aggregate(_npz_results(G.parameters(case), m["weights"]), None)[0]
+    assert NativeStreamingFold.stats["rows"] - before == len(m["weights"])
+    assert all(G.same_bits(a, b) for a, b in zip(out, G.expected(case, "aggregate")))

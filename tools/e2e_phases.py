@@ -36,8 +36,9 @@ def main():
     from fedlesscan_amd import FedAvgAggregator, synth
     from fedlesscan_amd.aggregator.fed_avg_aggregator import decode_results
     from fedlesscan_amd.engine import STREAM_CHUNK_BYTES
-    from fedlesscan_amd.ingest import StreamingFold
+    from fedlesscan_amd.ingest import make_streaming_fold
     from fedlesscan_amd.store import InMemoryClientResultStore
+    from fedlesscan_amd.engine import to_host as engine_to_host
     N, P = a.clients, a.params
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -55,7 +56,7 @@ def main():
         params, w, _ = decode_results(list(it), None)
         t.append(time.perf_counter())
         rows = max(1, min(N, STREAM_CHUNK_BYTES // (4 * P)))
-        sf = StreamingFold(P, chunk_rows=rows, device=dev)
+        sf = make_streaming_fold(P, dev, STREAM_CHUNK_BYTES)
         torch.cuda.synchronize()
         t.append(time.perf_counter())
         for i in range(N):
@@ -65,7 +66,7 @@ def main():
         t.append(time.perf_counter())
         torch.cuda.synchronize()
         t.append(time.perf_counter())
-        acc.cpu().numpy()
+        engine_to_host(acc)
         t.append(time.perf_counter())
         names = ["decode", "setup", "adds", "finish", "device_wait", "d2h"]
         out.append({k: round((t[j + 1] - t[j]) * 1e3, 2) for j, k in enumerate(names)})
