@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "fedavg_hip.h"
+#include "host_copy.hpp"
 
 namespace {
 
@@ -342,8 +343,8 @@ int fa_pack(void* dst, const int64_t* dst_offsets, const void* const* srcs, cons
         for (int64_t b = b0; b < b1 && i < n; ++i) {
             const int64_t s0 = std::max(b, off[i]), s1 = std::min(b1, off[i + 1]);
             if (s1 > s0)
-                memcpy((uint8_t*)dst + dst_offsets[i] + (s0 - off[i]), (const uint8_t*)srcs[i] + (s0 - off[i]),
-                       (size_t)(s1 - s0));
+                fa_host::pack_copy((uint8_t*)dst + dst_offsets[i] + (s0 - off[i]),
+                                   (const uint8_t*)srcs[i] + (s0 - off[i]), (size_t)(s1 - s0));
             b = s1;
         }
     };

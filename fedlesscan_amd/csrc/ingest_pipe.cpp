@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "fedavg_hip.h"
+#include "host_copy.hpp"
 
 __attribute__((visibility("hidden"))) int fa_internal_fail(int code, const char* msg);
 
@@ -342,7 +343,7 @@ int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, i
         if (batch.empty()) return;
         S.outstanding.fetch_add(1);
         CopyPool::get().submit([p, &S, parts = std::move(batch)] {
-            for (const Part& q : parts) memcpy(q.dst, q.src, (size_t)q.n);
+            for (const Part& q : parts) fa_host::pack_copy(q.dst, q.src, (size_t)q.n);
             // decrement under the pipe's lock: once a waiter sees 0 this task no longer touches the pipe
             std::lock_guard<std::mutex> lk(p->mu);
             if (S.outstanding.fetch_sub(1) == 1) p->cv.notify_all();

@@ -1,0 +1,8 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+exec scripts/gpu_steps.sh \
+  "ingest_tests:300:$PYT -m gpu tests/test_gpu_ingest.py tests/test_gpu_multigpu.py" \
+  "pack_bw:120:FEDAVG_PACK_NT=1 python3 tools/pack_bw.py && FEDAVG_PACK_NT=0 python3 tools/pack_bw.py && FEDAVG_PACK_NT=1 python3 tools/pack_bw.py && FEDAVG_PACK_NT=0 python3 tools/pack_bw.py" \
+  "e2e_nt:700:OUT=gpurun_out/e2e_nt CONFIGS='py:64:2 nat:16:4 nat:32:3 nat:64:3' scripts/e2e_native.sh" \
+  "c4_budget:600:scripts/c4_budget.sh"
