@@ -67,7 +67,7 @@ _PROTOS = {
     "fa_copy_peer": (_int, [_vp, _int, _vp, _int, _i64, _vp]),
     "fa_ingest_create": (_int, [_vp, _i64, _i64, _int, _int]),
     "fa_ingest_rows_per_chunk": (_int, [_vp]),
-    "fa_ingest_begin": (_int, [_vp, _vp, _vp]),
+    "fa_ingest_begin": (_int, [_vp, _vp, _vp, _i64]),
     "fa_ingest_add": (_int, [_vp, _vp, _vp, _i64, _f32, _f32, _int]),
     "fa_ingest_finish": (_int, [_vp, _f32]),
     "fa_ingest_destroy": (_int, [_vp]),

@@ -114,8 +114,9 @@ class FedAvgAggregator(ParameterAggregator):
             params, cards, metrics = decode_results(client_results, default_cardinality)
             return self._aggregate(params, cards), (metrics or None)
         metrics: list = []
+        n = len(client_results) if hasattr(client_results, "__len__") else 0
         out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
-                                       None, device=self.device, devices=self.devices)
+                                       None, device=self.device, devices=self.devices, expected_rows=n)
         return out, (metrics or None)
 
 

@@ -58,9 +58,10 @@ class StallAwareAggregator(ParameterAggregator):
             params, cards, metrics = decode_results(client_results, default_cardinality)
             return self._aggregate(client_feats, params, cards), (metrics or None)
         metrics: list = []
+        n = len(client_results) if hasattr(client_results, "__len__") else 0
         out = engine.aggregate_decoded(decoded_rows(client_results, default_cardinality, metrics),
                                        self._score_clients(client_feats), device=self.device,
-                                       devices=self.devices)
+                                       devices=self.devices, expected_rows=n)
         return out, (metrics or None)
 
 

@@ -103,6 +103,7 @@ struct Slot {
     hipEvent_t h2d_done = nullptr, fold_done = nullptr;
     SlotState state = SlotState::kFree;
     int64_t rows = 0;
+    int64_t cap = 0;  // rows this use of the slot takes before it is sent (<= R: the ramps)
     bool has_s = false;
     std::atomic<int64_t> outstanding{0};  // copy tasks not yet finished
 };
@@ -124,6 +125,8 @@ struct fa_ingest {
     hipStream_t compute = nullptr;
     int cur = 0;
     int64_t rows = 0;
+    int64_t expected = 0;  // rows the caller announced for the round (0: unknown)
+    int64_t chunks = 0;    // slots started this round
     bool started = false;  // acc holds a partial fold (issuer side)
     int scored = -1;       // -1 unknown, 0 FedAvg, 1 stall-aware
     float divisor = 0.f;
@@ -296,8 +299,8 @@ int fa_ingest_create(fa_ingest** out, int64_t P, int64_t chunk_bytes, int slots,
 
 int fa_ingest_rows_per_chunk(const fa_ingest* p) { return p ? (int)p->R : 0; }
 
-int fa_ingest_begin(fa_ingest* p, float* acc, void* stream) {
-    if (!p || !acc) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: bad arguments");
+int fa_ingest_begin(fa_ingest* p, float* acc, void* stream, int64_t expected_rows) {
+    if (!p || !acc || expected_rows < 0) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: bad arguments");
     {
         std::lock_guard<std::mutex> lk(p->mu);
         if (p->in_flight) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: previous round not finished");
@@ -308,6 +311,8 @@ int fa_ingest_begin(fa_ingest* p, float* acc, void* stream) {
     p->compute = (hipStream_t)stream;
     p->cur = 0;
     p->rows = 0;
+    p->expected = expected_rows;
+    p->chunks = 0;
     p->started = false;
     p->scored = -1;
     return FA_OK;
@@ -328,7 +333,18 @@ int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, i
     if (int rc = report(p)) return rc;
     p->scored = has_s ? 1 : 0;
     Slot& S = p->slots[p->cur];
-    if (S.state != SlotState::kFilling && claim(p, p->cur) != FA_OK) return report(p);
+    if (S.state != SlotState::kFilling) {
+        if (claim(p, p->cur) != FA_OK) return report(p);
+        // Ramps: the round's first chunks hold 1, 2, 4, ... rows, so the first
+        // DMA starts after one row instead of a full chunk; with the row count
+        // announced, the last ones shrink the same way (at most half of what
+        // is left), so the tail the round waits for after its last row is
+        // about one row's DMA and fold instead of a chunk's.
+        int64_t cap = p->chunks < 62 ? std::min<int64_t>(p->R, (int64_t)1 << p->chunks) : p->R;
+        if (p->expected > p->rows) cap = std::min(cap, std::max<int64_t>(1, (p->expected - p->rows + 1) / 2));
+        S.cap = cap;
+        ++p->chunks;
+    }
     const int64_t r = S.rows++;
     S.has_s = has_s != 0;
     S.fac_host[r] = a;
@@ -364,7 +380,7 @@ int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, i
     }
     flush();
     ++p->rows;
-    if (S.rows == p->R) {
+    if (S.rows == S.cap) {
         enqueue(p, p->cur, false);
         p->cur = (p->cur + 1) % p->K;
     }

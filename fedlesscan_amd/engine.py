@@ -511,7 +511,7 @@ def _fast_row(layers, shapes) -> bool:
 
 
 def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional[torch.device] = None,
-                      devices=None) -> List:
+                      devices=None, expected_rows: int = 0) -> List:
     """aggregate_layers over an iterator of decoded (layers, weight) rows, with
     the fold overlapping the decode.
 
@@ -527,6 +527,8 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
 
     devices: several GPUs (multigpu.MultiStreamingFold): every GPU ingests and
     folds its own column bucket of each row, so the rows cross G PCIe links.
+    expected_rows: the number of rows when the caller knows it (a list of
+    results); the native pipe then shrinks its last chunks (a shorter tail).
     """
     multi = _multi(devices)
     if devices is not None and device is None:
@@ -543,12 +545,15 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
             (scores is None or (len(scores) > 0 and all(_py_scalar(x) for x in scores))))
     P = sum(int(np.prod(shp)) if len(shp) else 1 for shp in shapes) if fast else 0
     if fast and P > 0:
+        n_exp = min(expected_rows, n_fold) if n_fold is not None else expected_rows
         if multi is not None:
             from .multigpu import MultiStreamingFold
-            sf = MultiStreamingFold(P, multi, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
+            sf = MultiStreamingFold(P, multi, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA,
+                                    expected_rows=n_exp)
         else:
             from .ingest import make_streaming_fold
-            sf = make_streaming_fold(P, device or default_device(), STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
+            sf = make_streaming_fold(P, device or default_device(), STREAM_CHUNK_BYTES, direct=DIRECT_DMA,
+                                     expected_rows=n_exp)
         sf.add(list(first[0]), first[1], None if scores is None else scores[0])
         for layers, w in it:
             rows.append(layers)
@@ -588,7 +593,7 @@ def to_host(t: torch.Tensor) -> np.ndarray:
 
 def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
     from .ingest import make_streaming_fold
-    sf = make_streaming_fold(P, dev, min(STREAM_CHUNK_BYTES, max(1, n) * 4 * P), direct=DIRECT_DMA)
+    sf = make_streaming_fold(P, dev, min(STREAM_CHUNK_BYTES, max(1, n) * 4 * P), direct=DIRECT_DMA, expected_rows=n)
     for i in range(n):
         sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
     return sf.finish(total=total)
@@ -596,7 +601,7 @@ def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
 
 def _stream_group_multi(parameters, n, lis, P, w, sc, total, devices) -> np.ndarray:
     from .multigpu import MultiStreamingFold
-    sf = MultiStreamingFold(P, devices, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA)
+    sf = MultiStreamingFold(P, devices, chunk_bytes=STREAM_CHUNK_BYTES, direct=DIRECT_DMA, expected_rows=n)
     for i in range(n):
         sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
     return sf.finish(total=total)

@@ -269,7 +269,7 @@ class NativeStreamingFold:
     stats = {"rows": 0}
 
     def __init__(self, P: int, device: Optional[torch.device] = None, chunk_bytes: int = 16 << 20,
-                 slots: int = 4):
+                 slots: int = 4, expected_rows: int = 0):
         if P <= 0:
             raise InvalidParameterShapeError("StreamingFold needs P > 0")
         self.P = P
@@ -282,7 +282,8 @@ class NativeStreamingFold:
         self.L = _lib.load()
         try:
             _lib.check(self.L.fa_ingest_begin(self.pipe, self.acc.data_ptr(),
-                                              torch.cuda.current_stream(self.dev).cuda_stream), "fa_ingest_begin")
+                                              torch.cuda.current_stream(self.dev).cuda_stream,
+                                              max(0, int(expected_rows))), "fa_ingest_begin")
         except BaseException:
             _pipes.drop(self.pipe)
             self.pipe = None
@@ -355,12 +356,14 @@ NATIVE_INGEST = os.environ.get("FEDAVG_NATIVE_INGEST", "1") == "1"
 STREAM_SLOTS = int(os.environ.get("FEDAVG_STREAM_SLOTS", "0"))  # 0: the form's default
 
 
-def make_streaming_fold(P: int, device, chunk_bytes: int, direct: bool = False):
+def make_streaming_fold(P: int, device, chunk_bytes: int, direct: bool = False, expected_rows: int = 0):
     """The ingest for P-float rows on `device`: the native pipe, or the
     Python-driven StreamingFold for the direct-DMA route (page-locked
-    documents) or when FEDAVG_NATIVE_INGEST=0."""
+    documents) or when FEDAVG_NATIVE_INGEST=0.  expected_rows: the round's row
+    count when the caller knows it (the native pipe then shrinks its last
+    chunks)."""
     if NATIVE_INGEST and not direct:
-        return NativeStreamingFold(P, device, chunk_bytes, STREAM_SLOTS or 4)
+        return NativeStreamingFold(P, device, chunk_bytes, STREAM_SLOTS or 4, expected_rows)
     return StreamingFold(P, chunk_rows=max(1, chunk_bytes // (4 * P)), device=device, direct=direct,
                          slots=STREAM_SLOTS or None)
 

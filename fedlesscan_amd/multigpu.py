@@ -88,7 +88,8 @@ class MultiStreamingFold:
     [P] model in page-locked host memory, each bucket copied D2H on its own GPU.
     """
 
-    def __init__(self, P: int, devices: Sequence, chunk_bytes: int = 64 << 20, direct: bool = False):
+    def __init__(self, P: int, devices: Sequence, chunk_bytes: int = 64 << 20, direct: bool = False,
+                 expected_rows: int = 0):
         from .ingest import make_streaming_fold
         if P <= 0:
             raise InvalidParameterShapeError("MultiStreamingFold needs P > 0")
@@ -98,7 +99,8 @@ class MultiStreamingFold:
         self.folds = []
         for dev, (lo, hi) in zip(self.devices, self.bounds):
             w = hi - lo
-            self.folds.append(make_streaming_fold(w, dev, chunk_bytes, direct=direct) if w > 0 else None)
+            self.folds.append(make_streaming_fold(w, dev, chunk_bytes, direct=direct, expected_rows=expected_rows)
+                              if w > 0 else None)
         self.rows = 0
 
     def add(self, layers, weight, score: Optional[float] = None):

@@ -179,7 +179,11 @@ int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int
  * accumulator carried across them: bit-identical to fa_fedavg_f32 over all
  * rows.  A chunk slot is refilled only after its fold has completed.
  *   fa_ingest_create:  allocate a pipe for models of P floats on `device`
- *   fa_ingest_begin:   start a round folding into acc [device, P] on `stream`
+ *   fa_ingest_begin:   start a round folding into acc [device, P] on `stream`;
+ *                      expected_rows = the round's row count if known (0: not):
+ *                      the first chunks hold 1, 2, 4, ... rows and, with the
+ *                      count known, the last ones at most half of what is left,
+ *                      so neither the start nor the tail waits for a full chunk
  *   fa_ingest_add:     one client row [host]: n pieces (srcs[i], sizes[i] bytes)
  *                      that concatenate to P floats, its factors a = fl32(n_i)
  *                      and s = fl32(score) when has_s (every row or none).  The
@@ -192,7 +196,7 @@ int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int
 typedef struct fa_ingest fa_ingest;
 int fa_ingest_create(fa_ingest** pipe, int64_t P, int64_t chunk_bytes, int slots, int device);
 int fa_ingest_rows_per_chunk(const fa_ingest* pipe);
-int fa_ingest_begin(fa_ingest* pipe, float* acc, void* stream);
+int fa_ingest_begin(fa_ingest* pipe, float* acc, void* stream, int64_t expected_rows);
 int fa_ingest_add(fa_ingest* pipe, const void* const* srcs, const int64_t* sizes, int64_t n, float a, float s,
                   int has_s);
 int fa_ingest_finish(fa_ingest* pipe, float divisor);

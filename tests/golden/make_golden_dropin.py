@@ -67,7 +67,7 @@ def _oracle_fold(monkeypatch_target):
         prods = [[np.multiply(np.multiply(l, w), s) for l in p] for p, w, s in zip(parameters, weights, scores)]
         return [reduce(np.add, ls) / total for ls in zip(*prods)]
 
-    def fake_decoded(items, scores=None, device=None, devices=None):
+    def fake_decoded(items, scores=None, device=None, devices=None, expected_rows=0):
         rows, ws = [], []
         for layers, w in items:
             rows.append(layers)

@@ -257,3 +257,24 @@ def test_native_pipe_is_the_default_aggregate_route(dev):
     out = FedAvgAggregator().aggregate(_npz_results(G.parameters(case), m["weights"]), None)[0]
     assert NativeStreamingFold.stats["rows"] - before == len(m["weights"])
     assert all(G.same_bits(a, b) for a, b in zip(out, G.expected(case, "aggregate")))
+
+
+@pytest.mark.parametrize("expected", ["none", "exact", "high", "low"])
+@pytest.mark.parametrize("chunk_rows", [1, 4, 16])
+def test_native_pipe_chunk_ramps(dev, expected, chunk_rows):
+    """The ramps (first chunks of 1, 2, 4, ... rows; with the row count
+    announced, last chunks of at most half of what is left) change only where
+    the chunks end: bit-exact whatever count is announced."""
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    N, P = 29, 20011
+    X = synth.clients_f32(63, N, 0, P)
+    w = synth.cardinalities(63, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(63, N, 10, 2)]
+    ldx = (P + 63) // 64 * 64
+    exp_rows = {"none": 0, "exact": N, "high": N + 5, "low": N - 7}[expected]
+    sf = NativeStreamingFold(P, dev, chunk_bytes=chunk_rows * ldx * 4, slots=3, expected_rows=exp_rows)
+    for i in range(N):
+        sf.add(X[i], w[i], sc[i])
+    got = sf.finish().cpu().numpy()
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
+    assert G.same_bits(got, exp)

@@ -284,7 +284,7 @@ def oracle_fold(monkeypatch):
         if scores is None:
             return O.fedavg_literal(parameters[:n], list(weights))
         return _stall(parameters[:n], list(weights), list(scores))
-    def fake_decoded(items, scores=None, device=None, devices=None):
+    def fake_decoded(items, scores=None, device=None, devices=None, expected_rows=0):
         rows, ws = [], []
         for layers, w in items:
             rows.append(layers)

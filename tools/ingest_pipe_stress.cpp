@@ -80,7 +80,9 @@ static void worker(int tid, int rounds) {
         check(fa_ingest_create(&pipe, P, chunk, slots, 0) == FA_OK, "create");
         std::vector<float> acc(P, -1.f);
         for (int rep = 0; rep < 2; ++rep) {  // the pipe is reused
-            check(fa_ingest_begin(pipe, acc.data(), nullptr) == FA_OK, "begin");
+            // the announced row count: unknown, exact, too high, too low (only the chunk sizes change)
+            const int64_t guess[4] = {0, N, N + 3, N > 2 ? N - 2 : 1};
+            check(fa_ingest_begin(pipe, acc.data(), nullptr, guess[rng() % 4]) == FA_OK, "begin");
             for (int64_t i = 0; i < N; ++i) {
                 // the row in 1-4 pieces
                 std::vector<const void*> src;
@@ -105,7 +107,7 @@ static void worker(int tid, int rounds) {
             check(memcmp(exp.data(), acc.data(), P * 4) == 0, "bit-exact");
         }
         // errors mid-round, then destroy with copies possibly in flight
-        check(fa_ingest_begin(pipe, acc.data(), nullptr) == FA_OK, "begin 2");
+        check(fa_ingest_begin(pipe, acc.data(), nullptr, 0) == FA_OK, "begin 2");
         const void* src0 = X.data();
         int64_t full = P * 4, shortb = (P - 1) * 4;
         check(fa_ingest_add(pipe, &src0, &full, 1, 1.f, 1.f, 0) == FA_OK, "add ok");
@@ -114,7 +116,7 @@ static void worker(int tid, int rounds) {
         fa_ingest_destroy(pipe);
         fa_ingest* empty = nullptr;
         check(fa_ingest_create(&empty, P, chunk, slots, 0) == FA_OK, "create 2");
-        check(fa_ingest_begin(empty, acc.data(), nullptr) == FA_OK, "begin 3");
+        check(fa_ingest_begin(empty, acc.data(), nullptr, 5) == FA_OK, "begin 3");
         check(fa_ingest_finish(empty, 1.f) == FA_ERR_NO_CLIENTS, "empty round");
         fa_ingest_destroy(empty);
     }
