@@ -152,6 +152,17 @@ def setup_dist(args):
     return world, rank, torch.device("cuda", torch.cuda.current_device()), backend
 
 
+def json_stdout():
+    """A writer on the real stdout for the one JSON line; fd 1 itself is
+    pointed at stderr for the rest of the run, because RCCL prints its version
+    banner (and the HIP runtime its notices) on stdout, which would put extra
+    lines before the JSON line of a multi-GPU run."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(real, "w")
+
+
 def rank_devices(dev) -> list:
     """Every rank's GPU (rank order): ordinal and PCI bus id."""
     props = torch.cuda.get_device_properties(dev)
@@ -316,6 +327,7 @@ def main():
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
+    out = json_stdout()
     world, rank, dev, backend = setup_dist(args)
     dist_on = dist.is_initialized()  # every rank-collective branch below keys on this, not on world > 1
     cfg = CONFIGS[args.config]
@@ -528,7 +540,7 @@ def main():
             "gather_bytes_per_rank": (lay.padded_total * (4 if wl.dtype == "f32" else 2)
                                       * (world - 1) // world) if dist_on else 0,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if dist_on:
         dist.destroy_process_group()
 

@@ -1818,7 +1818,14 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
                                divisor, out_f32, out_bf16);
         return check_launch("k_fedavg_bf16_scalar");
     }
-    if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
+    if (N >= 128 && (P >> 3) >= 368000 && (P >> 3) < 700000) {
+        // 2.9M-5.6M params, 128+ clients (the 3.125M-param round slot of an 8-GPU C4 bucket):
+        // four octets per lane (8 rows x 4 x 16 B in flight per lane), column bands of 4
+        // passes: 0.238 against 0.260 ms at 256 x 3.125M (profiles/r03_c4_budget/), 5-11 %
+        // faster at 3.1M-5M and 128-256 clients, but 2-8 % slower at 2.5M-3M and 6.25M-8M
+        // (profiles/r02_slots/bf16_octets_scan/), hence the narrow range
+        launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+    } else if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
         // per-GPU C4 buckets (256 x 12.5M) and their multi-GPU round slots
         // (256 x 3.125M): grid-stride, 8 rows x 2 octets, balanced passes in
         // column bands of 4 passes: +7 % over the row-streaming pick (DESIGN.md

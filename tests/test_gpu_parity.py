@@ -655,6 +655,15 @@ def test_config4_full_size_bf16_256x100M(dev, lib):
     _full_size_check(dev, lib, 256, 100_000_000, 4, "bf16", scored=False)
 
 
+@pytest.mark.parametrize("N,P,scored", [(256, 12_500_000, False),   # an 8-GPU rank's C4 bucket
+                                        (256, 3_125_000, True),     # its round slot (4 rounds): 4 octets per lane
+                                        (128, 4_000_011, False),    # same pick, P % 8 tail
+                                        (256, 2_944_003, True),     # the pick's lower edge
+                                        (256, 5_599_997, False)])   # its upper edge
+def test_config4_rank_bucket_and_slots_bf16(dev, lib, N, P, scored):
+    _full_size_check(dev, lib, N, P, 40 + N, "bf16", scored=scored)
+
+
 @pytest.mark.parametrize("chunk_rows", [1, 3, 7, 64])
 @pytest.mark.parametrize("scored", [False, True])
 def test_streaming_fold_equals_batch(dev, chunk_rows, scored):
