@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=8)
     ap.add_argument("--clients", type=int, default=0, help="override the config's client count (experiments)")
     ap.add_argument("--params", type=int, default=0, help="override the config's parameter count (experiments)")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="initialise a one-rank nccl (RCCL) process group in this process, without a launcher, so the "
+                         "all-gather path runs under a profiler that must start the program itself (one GPU)")
     ap.add_argument("--rounds", type=int, default=0,
                     help="exchange rounds per step (fold of round k+1 overlaps the all-gather of round k); "
                          "default 1 on one GPU, 4 on several")
@@ -128,6 +131,11 @@ def setup_dist(args):
     """(world, rank, device, backend).  Under torch.distributed.run the process
     group is initialised at any world size, WORLD_SIZE 1 included, so the
     all-gather path always runs (nccl = RCCL over xGMI)."""
+    if getattr(args, "rccl_world1", False) and "WORLD_SIZE" not in os.environ:
+        if args.gpus != 1:
+            raise SystemExit("bench.py: --rccl-world1 runs one rank (--gpus 1)")
+        os.environ.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(_free_port()))
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -531,7 +539,10 @@ def main():
             "gather_check": gather_ok,
             # the ranks that actually ran: torch.distributed's world and each rank's GPU
             "dist": {"backend": backend, "world_size": dist.get_world_size() if dist_on else 1,
-                     "launcher": "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none (single process)",
+                     "launcher": ("in-process one-rank group (--rccl-world1)" if args.rccl_world1 else
+                                  "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ or
+                                  "GROUP_RANK" in os.environ else
+                                  "environment (WORLD_SIZE set)" if dist_on else "none (single process)"),
                      "devices": devices},
             # per-rank split of a step at N > 1 (max over ranks): the fold kernels,
             # and the all-gather left exposed after the last fold of the step

@@ -144,7 +144,7 @@ def main():
         "clients": N, "params": P, "input_bytes": in_bytes, "gen_s": round(gen_s, 1),
         "gpu_e2e_s": round(t_gpu, 4), "gpu_e2e_gbs": round(in_bytes / t_gpu / 1e9, 2),
         "gpu_e2e_min_s": round(min(ts), 4), "gpu_e2e_max_s": round(max(ts), 4),
-        "stream_chunk_mb": int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "16")),
+        "stream_chunk_mb": int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "32")),
         "stream_slots": int(os.environ.get("FEDAVG_STREAM_SLOTS", "0")) or None,
         "ingest": "native pipe (fa_ingest_*)" if NATIVE_INGEST and not a.pinned_store else "python StreamingFold",
         "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),

@@ -491,9 +491,11 @@ def aggregate_layers(parameters: Sequence[Sequence], weights: Sequence, scores: 
 
 
 # pinned staging per chunk; FEDAVG_STREAM_CHUNK_MB overrides.  The native pipe
-# (ingest.NativeStreamingFold, round 3) keeps 4 chunks in flight; the
-# Python-driven StreamingFold (direct DMA) keeps 2 of 64 MB.
-STREAM_CHUNK_BYTES = int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "16")) << 20
+# (ingest.NativeStreamingFold, round 3) keeps 3 chunks of 32 MB in flight: best
+# or within the run-to-run spread of 16-64 MB x 3-6 slots on 10 x 582K, 100 x 1M,
+# 100 x 10M and 1024 x 1M (profiles/r03_e2e_ramp/); the Python-driven
+# StreamingFold (the direct-DMA route) keeps 2.
+STREAM_CHUNK_BYTES = int(os.environ.get("FEDAVG_STREAM_CHUNK_MB", "32")) << 20
 # DMA layers straight from page-locked documents instead of packing them
 # (StreamingFold direct=True); FEDAVG_DIRECT_DMA=1 turns it on.
 DIRECT_DMA = os.environ.get("FEDAVG_DIRECT_DMA", "0") == "1"

@@ -363,7 +363,7 @@ def make_streaming_fold(P: int, device, chunk_bytes: int, direct: bool = False, 
     count when the caller knows it (the native pipe then shrinks its last
     chunks)."""
     if NATIVE_INGEST and not direct:
-        return NativeStreamingFold(P, device, chunk_bytes, STREAM_SLOTS or 4, expected_rows)
+        return NativeStreamingFold(P, device, chunk_bytes, STREAM_SLOTS or 3, expected_rows)
     return StreamingFold(P, chunk_rows=max(1, chunk_bytes // (4 * P)), device=device, direct=direct,
                          slots=STREAM_SLOTS or None)
 
