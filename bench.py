@@ -45,6 +45,7 @@ sys.path.insert(0, REPO)
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
 from fedlesscan_amd.sharding import SlotLayout, gather_into  # noqa: E402
+from fedlesscan_amd.sharding import fold_stream as sharding_fold_stream  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -351,6 +352,14 @@ def main():
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
                        device=dev) if dist_on else None
     stream = torch.cuda.current_stream(dev)
+    if dist_on:
+        # the folds on a high-priority stream: HIP maps streams onto a few
+        # hardware queues, and a fold sharing one with RCCL's stream queues
+        # behind the previous round's collective instead of overlapping it
+        # (profiles/r03_c4_trace/: fold k+1 started ~35 us after fold k, behind
+        # the all-gather's copy, when both sat on one queue)
+        stream = sharding_fold_stream(dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
 
     if args.sweep and rank == 0:
         nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()
@@ -405,6 +414,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
 
+    torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
     for _ in range(args.warmup):
         step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -516,6 +526,7 @@ def main():
                     f" + {'RCCL' if backend == 'nccl' else backend} all_gather in {rounds} rounds overlapped with "
                     "the fold" if dist_on else ""),
                 "rounds": rounds,
+                "fold_stream": "high priority" if dist_on else "default",
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
                 # the kernel form the product's fp32 auto fold takes for one launch of this rank

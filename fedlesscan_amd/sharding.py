@@ -71,6 +71,23 @@ class SlotLayout:
         return k * self.world * self.sub, (k + 1) * self.world * self.sub
 
 
+_fold_streams: dict = {}
+
+
+def fold_stream(device) -> torch.cuda.Stream:
+    """A high-priority stream per GPU for the folds that overlap the exchange.
+
+    HIP maps streams onto a few hardware queues per device; a fold sharing a
+    queue with RCCL's stream waits behind the previous round's collective
+    instead of running beside it (profiles/r03_c4_trace/).  A high-priority
+    stream sits on its own queue."""
+    dev = torch.device(device)
+    s = _fold_streams.get(dev)
+    if s is None:
+        s = _fold_streams[dev] = torch.cuda.Stream(device=dev, priority=-1)
+    return s
+
+
 def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
     """all_gather_into_tensor of `piece` into `full`.  16-bit payloads travel
     as bytes (bit-identical; an all-gather moves bytes, and gloo takes neither
@@ -162,6 +179,20 @@ class ShardedAggregator:
         want_bf16= for bf16 input), as engine.fold_stacked does."""
         if X_local.shape[1] != layout.local_width:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
+        if not X_local.is_cuda or layout.rounds == 1:
+            return self._aggregate_slots(X_local, weights, scores, layout, out, total)
+        # the rounds' folds on a high-priority stream of their own (fold_stream), ordered after
+        # the caller's work and before the caller's later work
+        caller = torch.cuda.current_stream(X_local.device)
+        fs = fold_stream(X_local.device)
+        fs.wait_stream(caller)
+        with torch.cuda.stream(fs):
+            full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
+        caller.wait_stream(fs)
+        full.record_stream(caller)
+        return full
+
+    def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
         sub = layout.sub
         bf16 = X_local.dtype == torch.bfloat16
         odt = torch.bfloat16 if bf16 else torch.float32
