@@ -14,5 +14,5 @@ for r in 4 2; do
       --no-cpu-baseline > "$OUT/r$r.json" 2> "$OUT/r$r.err"
 done
 cd "$ROOT"
-python3 scripts/trace_gaps.py "$OUT/r4" "$OUT/r2" > "$OUT/SUMMARY.md"
+ROUNDS=4 python3 scripts/trace_gaps.py "$OUT/r4" > "$OUT/SUMMARY.md"; ROUNDS=2 python3 scripts/trace_gaps.py "$OUT/r2" >> "$OUT/SUMMARY.md"
 echo done
