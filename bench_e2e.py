@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--bson", action="store_true", help="start from BSON documents in the result store")
     ap.add_argument("--pinned-store", action="store_true", help="with --bson: documents in page-locked memory")
+    ap.add_argument("--devices", default="",
+                    help="comma-separated GPU ordinals for the multi-GPU drop-in (FedAvgAggregator(devices=...)); "
+                         "'all' = every visible GPU; a GPU may repeat (buckets sharing one GPU)")
     a = ap.parse_args()
     from oracle import fedavg_oracle as O  # checker + CPU reference timing only
     N, P = a.clients, a.params
@@ -99,15 +102,19 @@ def main():
         for i, cr in enumerate(results(blobs, cards)):
             store.save("bench", 1, f"client-{i}", cr)
 
+    devices = None
+    if a.devices:
+        devices = "all" if a.devices == "all" else [int(x) for x in a.devices.split(",")]
+
     def one_round(crs):
         if store is not None:
-            agg = FedAvgAggregator()
+            agg = FedAvgAggregator(devices=devices)
             feats, it = agg.select_aggregation_candidates(store, "bench", 1)
             return agg.aggregate(list(it), feats)
-        return FedAvgAggregator().aggregate(crs, None)
+        return FedAvgAggregator(devices=devices).aggregate(crs, None)
 
     # warm up the pipeline (pinned allocations, library load)
-    FedAvgAggregator().aggregate(results(blobs[: min(N, 4)], cards[: min(N, 4)]), None)
+    FedAvgAggregator(devices=devices).aggregate(results(blobs[: min(N, 4)], cards[: min(N, 4)]), None)
     torch.cuda.synchronize()
     ts, out = [], None
     for _ in range(a.reps):
@@ -149,6 +156,7 @@ def main():
         "ingest": "native pipe (fa_ingest_*)" if NATIVE_INGEST and not a.pinned_store else "python StreamingFold",
         "decode_views_s": round(t_decode, 4), "h2d_pinned_gbs": round(h2d_gbs, 1),
         "ingest_rows": routes,
+        "devices": a.devices or "current GPU",
     }
     if not a.no_cpu:
         if store is not None:
