@@ -98,7 +98,7 @@ enum class SlotState { kFree, kFilling, kQueued, kIssued };
 struct Slot {
     float* host = nullptr;      // [R][ldx] page-locked
     float* dev = nullptr;       // [R][ldx]
-    float* fac_host = nullptr;  // [2][R] page-locked: a, then s
+    float* fac_host = nullptr;  // [2][R] page-locked: a, then s (the head of the slot's one allocation)
     float* fac_dev = nullptr;   // [2][R]
     hipEvent_t h2d_done = nullptr, fold_done = nullptr;
     SlotState state = SlotState::kFree;
@@ -117,6 +117,7 @@ struct QueueItem {
 
 struct fa_ingest {
     int64_t P = 0, ldx = 0, R = 0;
+    int64_t fac_pad = 0;  // floats of factors (2R) rounded up to 64: the rows stay 256-B aligned
     int K = 0, device = 0;
     std::vector<Slot> slots;
     hipStream_t copy = nullptr;
@@ -169,10 +170,11 @@ int issue(fa_ingest* p, const QueueItem& it) {
         p->cv.wait(lk, [&] { return S.outstanding.load() == 0 || p->err != FA_OK; });
         if (p->err != FA_OK) return p->err;
     }
-    hipError_t e = hipMemcpyAsync(S.dev, S.host, (size_t)(S.rows * p->ldx) * sizeof(float), hipMemcpyHostToDevice,
-                                  p->copy);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(S.fac_dev, S.fac_host, (size_t)(2 * p->R) * sizeof(float), hipMemcpyHostToDevice, p->copy);
+    // one DMA per chunk: the factors sit right before the rows in the slot's
+    // allocation (a separate small copy ran as a blit kernel between two SDMA
+    // transfers and left ~25 us of idle DMA engine per chunk)
+    hipError_t e = hipMemcpyAsync(S.fac_dev, S.fac_host, (size_t)(p->fac_pad + S.rows * p->ldx) * sizeof(float),
+                                  hipMemcpyHostToDevice, p->copy);
     if (e == hipSuccess) e = hipEventRecord(S.h2d_done, p->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(p->compute, S.h2d_done, 0);
     if (e != hipSuccess) return hip_err(p, "ingest H2D", e);
@@ -239,9 +241,7 @@ void free_slots(fa_ingest* p) {
         if (S.fold_done) (void)hipEventSynchronize(S.fold_done);
         if (S.h2d_done) (void)hipEventDestroy(S.h2d_done);
         if (S.fold_done) (void)hipEventDestroy(S.fold_done);
-        if (S.host) (void)hipHostFree(S.host);
-        if (S.fac_host) (void)hipHostFree(S.fac_host);
-        if (S.dev) (void)hipFree(S.dev);
+        if (S.fac_host) (void)hipHostFree(S.fac_host);  // the slot's one allocation (factors, then rows)
         if (S.fac_dev) (void)hipFree(S.fac_dev);
     }
     if (p->copy) (void)hipStreamDestroy(p->copy);
@@ -271,15 +271,18 @@ int fa_ingest_create(fa_ingest** out, int64_t P, int64_t chunk_bytes, int slots,
     p->ldx = (P + 63) / 64 * 64;  // 256-B row pitch: the vector folds
     p->R = std::max<int64_t>(1, chunk_bytes / (p->ldx * (int64_t)sizeof(float)));
     p->K = slots;
+    p->fac_pad = (2 * p->R + 63) / 64 * 64;
     p->device = device;
     p->slots = std::vector<Slot>(slots);
     hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
     for (Slot& S : p->slots) {
-        const size_t rowbytes = (size_t)(p->R * p->ldx) * sizeof(float), facbytes = (size_t)(2 * p->R) * sizeof(float);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&S.host, rowbytes, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&S.fac_host, facbytes, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc((void**)&S.dev, rowbytes);
-        if (e == hipSuccess) e = hipMalloc((void**)&S.fac_dev, facbytes);
+        const size_t rowbytes = (size_t)(p->R * p->ldx) * sizeof(float), facbytes = (size_t)p->fac_pad * sizeof(float);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&S.fac_host, facbytes + rowbytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void**)&S.fac_dev, facbytes + rowbytes);
+        if (e == hipSuccess) {
+            S.host = S.fac_host + p->fac_pad;  // rows start 256-B aligned after the factors
+            S.dev = S.fac_dev + p->fac_pad;
+        }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.h2d_done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.fold_done, hipEventDisableTiming);
         if (e == hipSuccess) memset(S.fac_host, 0, facbytes);
@@ -349,7 +352,9 @@ int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, i
     S.has_s = has_s != 0;
     S.fac_host[r] = a;
     S.fac_host[p->R + r] = has_s ? s : 1.0f;
-    // copy tasks of >= 1 MiB, split across pieces and inside large pieces
+    // copy tasks of 1 MiB, split across pieces and inside large pieces; 256 KiB
+    // while the round's first chunks ramp up (the first DMA waits for them)
+    const int64_t task_bytes = p->chunks <= 2 ? kTaskBytes / 4 : kTaskBytes;
     uint8_t* dst = reinterpret_cast<uint8_t*>(S.host + r * p->ldx);
     int64_t off = 0;
     struct Part { const uint8_t* src; uint8_t* dst; int64_t n; };
@@ -370,12 +375,12 @@ int fa_ingest_add(fa_ingest* p, const void* const* srcs, const int64_t* sizes, i
     for (int64_t i = 0; i < n; ++i) {
         const uint8_t* src = (const uint8_t*)srcs[i];
         for (int64_t done = 0; done < sizes[i];) {
-            const int64_t take = std::min(sizes[i] - done, kTaskBytes - batch_bytes);
+            const int64_t take = std::min(sizes[i] - done, task_bytes - batch_bytes);
             batch.push_back({src + done, dst + off, take});
             batch_bytes += take;
             done += take;
             off += take;
-            if (batch_bytes >= kTaskBytes) flush();
+            if (batch_bytes >= task_bytes) flush();
         }
     }
     flush();
