@@ -120,7 +120,8 @@ struct fa_ingest {
     int64_t fac_pad = 0;  // floats of factors (2R) rounded up to 64: the rows stay 256-B aligned
     int K = 0, device = 0;
     std::vector<Slot> slots;
-    hipStream_t copy = nullptr;
+    hipStream_t copy[2] = {nullptr, nullptr};  // chunks alternate between two copy streams
+    int64_t issued = 0;                         // chunks issued (issuer thread)
     // per round
     float* acc = nullptr;
     hipStream_t compute = nullptr;
@@ -172,10 +173,14 @@ int issue(fa_ingest* p, const QueueItem& it) {
     }
     // one DMA per chunk: the factors sit right before the rows in the slot's
     // allocation (a separate small copy ran as a blit kernel between two SDMA
-    // transfers and left ~25 us of idle DMA engine per chunk)
+    // transfers and left ~25 us of idle DMA engine per chunk).  Consecutive
+    // chunks alternate between two copy streams: on one stream each transfer
+    // started ~17 us after the previous one ended (profiles/r03_e2e_trace/);
+    // the fold of each chunk still waits for exactly its own transfer.
+    hipStream_t cs = p->copy[p->issued++ & 1];
     hipError_t e = hipMemcpyAsync(S.fac_dev, S.fac_host, (size_t)(p->fac_pad + S.rows * p->ldx) * sizeof(float),
-                                  hipMemcpyHostToDevice, p->copy);
-    if (e == hipSuccess) e = hipEventRecord(S.h2d_done, p->copy);
+                                  hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = hipEventRecord(S.h2d_done, cs);
     if (e == hipSuccess) e = hipStreamWaitEvent(p->compute, S.h2d_done, 0);
     if (e != hipSuccess) return hip_err(p, "ingest H2D", e);
     const int rc = fa_fold_f32(S.dev, S.rows, p->P, p->ldx, S.fac_dev, S.has_s ? S.fac_dev + p->R : nullptr,
@@ -244,7 +249,8 @@ void free_slots(fa_ingest* p) {
         if (S.fac_host) (void)hipHostFree(S.fac_host);  // the slot's one allocation (factors, then rows)
         if (S.fac_dev) (void)hipFree(S.fac_dev);
     }
-    if (p->copy) (void)hipStreamDestroy(p->copy);
+    for (hipStream_t cs : p->copy)
+        if (cs) (void)hipStreamDestroy(cs);
 }
 
 int report(fa_ingest* p) {
@@ -274,7 +280,8 @@ int fa_ingest_create(fa_ingest** out, int64_t P, int64_t chunk_bytes, int slots,
     p->fac_pad = (2 * p->R + 63) / 64 * 64;
     p->device = device;
     p->slots = std::vector<Slot>(slots);
-    hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&p->copy[0], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->copy[1], hipStreamNonBlocking);
     for (Slot& S : p->slots) {
         const size_t rowbytes = (size_t)(p->R * p->ldx) * sizeof(float), facbytes = (size_t)p->fac_pad * sizeof(float);
         if (e == hipSuccess) e = hipHostMalloc((void**)&S.fac_host, facbytes + rowbytes, hipHostMallocDefault);

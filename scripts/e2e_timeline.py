@@ -1,59 +1,43 @@
 #!/usr/bin/env python3
-"""Per-round timeline of an end-to-end run (rocprofv3 --kernel-trace
---memory-copy-trace of bench_e2e.py): rounds are split at idle gaps of more
-than 1 ms; per round the span from the first H2D to the result's D2H, the
-H2D busy time and rate, the gaps in the H2D stream, and what follows the last
-H2D (the tail: last fold + D2H).
+"""Per-round DMA timeline of an end-to-end run (rocprofv3 --kernel-trace
+--memory-copy-trace of bench_e2e.py).  Rounds are the runs of host-to-device
+copies separated by more than 250 us of idle copy engine; per round: the
+number of DMAs, their durations (the chunk ramps show up here), the copy
+engine's busy time and its idle gaps inside the round, and the idle time
+between rounds (the previous round's tail + this round's head).
 
     python scripts/e2e_timeline.py DIR
 """
 import csv
 import glob
 import os
-import statistics
 import sys
-
-
-def load(d, pat):
-    f = glob.glob(os.path.join(d, "**", pat), recursive=True)
-    return list(csv.DictReader(open(f[0]))) if f else []
 
 
 def main():
     d = sys.argv[1]
-    copies = load(d, "*memory_copy_trace.csv")
-    kernels = load(d, "*kernel_trace.csv")
-    ev = []
-    for r in copies:
-        kind = r.get("Direction") or r.get("Operation") or ""
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "D2H" if "DEVICE_TO_HOST" in kind else
-                   "H2D" if "HOST_TO_DEVICE" in kind else kind, int(r.get("Bytes", 0) or 0)))
-    for r in kernels:
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K:" + r["Kernel_Name"][:30], 0))
-    ev.sort()
-    rounds, cur = [], [ev[0]]
-    for e in ev[1:]:
-        if e[0] - max(x[1] for x in cur) > 1_000_000:
-            rounds.append(cur)
+    f = glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r["Start_Timestamp"]))
+    h = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "HOST_TO_DEVICE" in r["Direction"]]
+    segs, cur = [], [h[0]]
+    between = []
+    for a, b in zip(h, h[1:]):
+        if b[0] - a[1] > 250_000:
+            segs.append(cur)
+            between.append(b[0] - a[1])
             cur = []
-        cur.append(e)
-    rounds.append(cur)
-    big = [r for r in rounds if sum(x[3] for x in r if x[2] == "H2D") > 100e6]
-    print(f"# {d}\n\n{len(big)} rounds with > 100 MB of H2D\n")
-    print("| round | span ms | H2D bytes | H2D busy ms | H2D GB/s while busy | H2D gaps ms | tail after last H2D ms |")
+        cur.append(b)
+    segs.append(cur)
+    print(f"# {d}\n")
+    print("| round | DMAs | span us | DMA busy us | idle inside us | idle before the round us | DMA durations us |")
     print("|---|---|---|---|---|---|---|")
-    for i, r in enumerate(big):
-        h2d = sorted(x for x in r if x[2] == "H2D")
-        t0, t1 = r[0][0], max(x[1] for x in r)
-        busy, gaps, end = 0, 0, h2d[0][0]
-        for s, e, _, _ in h2d:
-            if s > end:
-                gaps += s - end
-            busy += e - max(s, end) if e > end else 0
-            end = max(end, e)
-        nbytes = sum(x[3] for x in h2d)
-        print(f"| {i} | {(t1 - t0) / 1e6:.2f} | {nbytes / 1e6:.0f} MB | {busy / 1e6:.2f} | "
-              f"{nbytes / busy / 1e3 if busy else 0:.1f} | {gaps / 1e6:.2f} | {(t1 - end) / 1e6:.2f} |")
+    for i, s in enumerate(segs):
+        busy = sum(e - b for b, e in s)
+        inside = sum(max(0, s[j + 1][0] - s[j][1]) for j in range(len(s) - 1))
+        before = between[i - 1] / 1e3 if i > 0 else float("nan")
+        durs = " ".join(str(round((e - b) / 1e3)) for b, e in s)
+        print(f"| {i} | {len(s)} | {(s[-1][1] - s[0][0]) / 1e3:.0f} | {busy / 1e3:.0f} | {inside / 1e3:.0f} | "
+              f"{before:.0f} | {durs} |")
 
 
 if __name__ == "__main__":
