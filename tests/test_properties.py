@@ -136,3 +136,31 @@ def test_gpu_fold_many_clients(N, P, pad4, seed, scored, cut):
                              None if s is None else s[k:].data_ptr(), acc.data_ptr(), div, 1, acc.data_ptr(),
                              stream), "part 2")
     assert _bits(acc.cpu().numpy(), exp)
+
+
+@pytest.mark.gpu
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                  HealthCheck.function_scoped_fixture])
+@given(w=weights_st, P=st.integers(1, 50000), seed=st.integers(0, 2**32 - 1), scored=st.booleans(),
+       chunk_rows=st.integers(1, 12), slots=st.integers(2, 6), announce=st.sampled_from(["none", "exact", "off"]),
+       cuts=st.lists(st.floats(0, 1), max_size=4))
+def test_gpu_native_ingest_matches_oracle(w, P, seed, scored, chunk_rows, slots, announce, cuts):
+    """The native ingest pipe over random rows split into random pieces, random
+    chunk sizes, slot counts and announced row counts: bit-exact against the C
+    oracle with numpy's weight rounding."""
+    from fedlesscan_amd.ingest import NativeStreamingFold
+    dev = torch.device("cuda", 0)
+    N = len(w)
+    X = synth.clients_f32(seed, N, 0, P)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
+    ldx = (P + 63) // 64 * 64
+    exp_rows = {"none": 0, "exact": N, "off": N + 3}[announce]
+    sf = NativeStreamingFold(P, dev, chunk_bytes=chunk_rows * ldx * 4, slots=slots, expected_rows=exp_rows)
+    edges = sorted({0, P, *(int(c * P) for c in cuts)})
+    for i in range(N):
+        sf.add([X[i, a:b] for a, b in zip(edges, edges[1:])], w[i], None if sc is None else sc[i])
+    with np.errstate(all="ignore"):
+        got = sf.finish().cpu().numpy()
+        exp = OL.fedavg_f32(X, np.array([np.float32(x) for x in w], np.float32), np.float32(sum(w)),
+                            s=None if sc is None else np.array(sc, np.float32))
+    assert _bits(got, exp)
