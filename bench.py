@@ -44,7 +44,7 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import SlotLayout, gather_into  # noqa: E402
+from fedlesscan_amd.sharding import ALIGN, SlotLayout, gather_into, tail_shares  # noqa: E402
 from fedlesscan_amd.sharding import fold_stream as sharding_fold_stream  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--rounds", type=int, default=0,
                     help="exchange rounds per step (fold of round k+1 overlaps the all-gather of round k); "
                          "default 1 on one GPU, 4 on several")
+    ap.add_argument("--tail", type=float, default=1.0,
+                    help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
+                         "left exposed after the step's folds); 1 = equal rounds")
     return ap.parse_args()
 
 
@@ -192,25 +195,25 @@ class Workload:
     slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
     With rounds=1 that is one contiguous bucket per rank."""
 
-    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0):
+    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0, tail=1.0):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
-        self.layout = (SlotLayout(self.P_total, world, rounds) if align is None
-                       else SlotLayout(self.P_total, world, rounds, align=align))
+        self.layout = SlotLayout(self.P_total, world, rounds, align=ALIGN if align is None else align,
+                                 shares=tail_shares(rounds, tail))
         self.slots = self.layout.slots(rank)
         self.P = sum(hi - lo for lo, hi in self.slots)  # real columns this rank folds
         self.rank, self.world, self.dev = rank, world, dev
         B = _lib.load_bench()  # input generator (bench / test support library)
         st = torch.cuda.current_stream(dev).cuda_stream
         tdt = torch.float32 if self.dtype == "f32" else torch.bfloat16
-        sub, W = self.layout.sub, self.layout.local_width
+        W = self.layout.local_width
         self.ldx = W + pitch_extra  # row pitch (elements): the slots side by side, plus any extra padding
         self.X = torch.zeros((self.N, self.ldx), dtype=tdt, device=dev)
         gen = B.fa_synth_f32 if self.dtype == "f32" else B.fa_synth_bf16
         esz = self.X.element_size()
         for k, (lo, hi) in enumerate(self.slots):
             if hi > lo:
-                _lib.check(gen(self.X.data_ptr() + k * sub * esz, self.N, hi - lo, self.ldx, self.seed, 0, lo, st),
+                _lib.check(gen(self.X.data_ptr() + self.layout.offset(k) * esz, self.N, hi - lo, self.ldx, self.seed, 0, lo, st),
                            "synth", bench=True)
         self.col0 = self.slots[0][0]
         self.weights = synth.cardinalities(self.seed, self.N, 1, card_hi)
@@ -236,10 +239,10 @@ class Workload:
         L = _lib.load()
         st = torch.cuda.current_stream(self.dev).cuda_stream
         s = None if self.s is None else self.s.data_ptr()
-        sub, W = self.layout.sub, self.layout.local_width
-        x = self.X.data_ptr() + k * sub * self.X.element_size()
-        o = self.out.data_ptr() + k * sub * 4
-        ob = None if self.out_bf16 is None else self.out_bf16.data_ptr() + k * sub * 2
+        off, sub = self.layout.offset(k), self.layout.width(k)
+        x = self.X.data_ptr() + off * self.X.element_size()
+        o = self.out.data_ptr() + off * 4
+        ob = None if self.out_bf16 is None else self.out_bf16.data_ptr() + off * 2
         bench = variant > 0
         if self.dtype == "f32" and variant < 0:  # opt-in split-client fold
             rc = L.fa_fedavg_f32_splitn(x, self.N, sub, self.ldx, self.a.data_ptr(), s, self.div, o, st)
@@ -346,7 +349,8 @@ def main():
     rounds = args.rounds or (4 if dist_on else 1)
     if args.splitn:
         args.variant = -1
-    wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra)
+    wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra,
+                  tail=args.tail if rounds > 1 else 1.0)
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
@@ -390,7 +394,6 @@ def main():
             log(f"variant {v} {vname(v).decode():10s} median {ts[len(ts)//2]:.4f} ms  "
                 f"min {ts[0]:.4f} ms  -> {wl.bytes / (ts[len(ts)//2] * 1e-3) / 1e9:.1f} GB/s")
 
-    sub = lay.sub
     # the exchanged model: fp32 result for fp32 updates, the RNE bf16 result
     # for bf16 updates (2 B/param over xGMI: half the bytes of the fp32 result)
     send = wl.out if wl.dtype == "f32" else wl.out_bf16
@@ -406,7 +409,7 @@ def main():
                 ev[0][k][1].record(stream)
             if dist_on:  # reassemble the global model: RCCL all-gather over xGMI, overlapping round k+1
                 lo, hi = lay.round_range(k)
-                w = gather_into(full[lo:hi], send[k * sub:(k + 1) * sub], None, async_op=True)
+                w = gather_into(full[lo:hi], send[lay.offset(k):lay.offset(k + 1)], None, async_op=True)
                 if w is not None:
                     works.append(w)
         for w in works:
@@ -446,7 +449,7 @@ def main():
         iv = torch.int32 if wl.dtype == "f32" else torch.int16
         for k, (lo, hi) in enumerate(wl.slots):
             if hi > lo:
-                ok &= torch.equal(full[lo:hi].view(iv), send[k * sub:k * sub + hi - lo].view(iv))
+                ok &= torch.equal(full[lo:hi].view(iv), send[lay.offset(k):lay.offset(k) + hi - lo].view(iv))
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
@@ -526,6 +529,7 @@ def main():
                     f" + {'RCCL' if backend == 'nccl' else backend} all_gather in {rounds} rounds overlapped with "
                     "the fold" if dist_on else ""),
                 "rounds": rounds,
+                "round_widths": lay.widths,
                 "fold_stream": "high priority" if dist_on else "default",
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),

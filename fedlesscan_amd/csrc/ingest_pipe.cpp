@@ -253,6 +253,16 @@ void free_slots(fa_ingest* p) {
         if (cs) (void)hipStreamDestroy(cs);
 }
 
+// Wait until no copy task of any slot is running (they read the caller's rows
+// and write the slots).  Under p->mu.
+void wait_packs(fa_ingest* p, std::unique_lock<std::mutex>& lk) {
+    p->cv.wait(lk, [&] {
+        for (const Slot& S : p->slots)
+            if (S.outstanding.load() != 0) return false;
+        return true;
+    });
+}
+
 int report(fa_ingest* p) {
     std::lock_guard<std::mutex> lk(p->mu);
     if (p->err == FA_OK) return FA_OK;
@@ -311,9 +321,23 @@ int fa_ingest_rows_per_chunk(const fa_ingest* p) { return p ? (int)p->R : 0; }
 
 int fa_ingest_begin(fa_ingest* p, float* acc, void* stream, int64_t expected_rows) {
     if (!p || !acc || expected_rows < 0) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: bad arguments");
-    {
-        std::lock_guard<std::mutex> lk(p->mu);
-        if (p->in_flight) return fa_internal_fail(FA_ERR_ARG, "fa_ingest_begin: previous round not finished");
+    {  // a round abandoned half-way (an error in add, or no finish) may still
+       // have chunks queued and copies running, and a slot half filled: they
+       // drain first (the issuer stops issuing once the round has failed), and
+       // the half-filled slot's rows do not join this round
+        std::unique_lock<std::mutex> lk(p->mu);
+        if (p->in_flight && p->err == FA_OK) {
+            p->err = FA_ERR_ARG;  // the queued chunks of the abandoned round are drained, not issued
+            p->errmsg = "round abandoned";
+            p->cv.notify_all();
+        }
+        p->cv.wait(lk, [&] { return p->in_flight == 0; });
+        wait_packs(p, lk);
+        for (Slot& S : p->slots)
+            if (S.state == SlotState::kFilling) {
+                S.state = SlotState::kFree;
+                S.rows = 0;
+            }
         p->err = FA_OK;
         p->errmsg.clear();
     }
@@ -412,7 +436,10 @@ int fa_ingest_finish(fa_ingest* p, float divisor) {
     }
     {
         std::unique_lock<std::mutex> lk(p->mu);
-        p->cv.wait(lk, [&] { return p->in_flight == 0; });  // every pack done, every DMA and fold enqueued
+        p->cv.wait(lk, [&] { return p->in_flight == 0; });  // every DMA and fold enqueued
+        // every pack done: after an error the drained items were never issued,
+        // and their copies may still be reading the caller's rows
+        wait_packs(p, lk);
     }
     return report(p);
 }
@@ -427,11 +454,7 @@ int fa_ingest_destroy(fa_ingest* p) {
     if (p->issuer.joinable()) p->issuer.join();
     {  // copy tasks still running read from the caller's rows and write the slots
         std::unique_lock<std::mutex> lk(p->mu);
-        p->cv.wait(lk, [&] {
-            for (const Slot& S : p->slots)
-                if (S.outstanding.load() != 0) return false;
-            return true;
-        });
+        wait_packs(p, lk);
     }
     int prev = 0;
     (void)hipGetDevice(&prev);

@@ -13,6 +13,7 @@ count, so 1/2/4/8 GPUs use the same code.
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -38,37 +39,79 @@ def chunk_size(P: int, world: int, align: int = ALIGN) -> int:
     return b[0][1] - b[0][0]
 
 
+def tail_shares(rounds: int, tail: float) -> List[float]:
+    """Round shares with the last round `tail` times the others (tail=1: equal).
+    Only the last round's exchange is left exposed after the step's folds, so a
+    short last round shortens it; the earlier rounds' gathers hide behind the
+    folds that follow them."""
+    if not 0 < tail <= 1:
+        raise ValueError("tail must be in (0, 1]")
+    return [1.0] * (rounds - 1) + [float(tail)]
+
+
 class SlotLayout:
     """Round-robin parameter slots for an exchange that overlaps the fold.
 
-    The global vector is cut into rounds*world equal `sub`-element slots
-    (64-element aligned, the last ones partly or wholly past P).  Slot
-    j = k*world + r belongs to rank r, so round k's slots of all ranks form the
-    CONTIGUOUS global range [k*world*sub, (k+1)*world*sub): one
-    all_gather_into_tensor per round writes it in place, while the fold of
-    round k+1 runs.  A rank stores its slots side by side, local width
-    rounds*sub.  rounds=1 is exactly bucket_bounds().
+    The global vector is cut into `rounds` rounds of `world` slots each
+    (64-element aligned, the last ones partly or wholly past P).  In round k
+    every rank's slot is width(k) elements; slot r of round k belongs to rank
+    r, so round k's slots of all ranks form the CONTIGUOUS global range
+    round_range(k): one all_gather_into_tensor per round writes it in place,
+    while the fold of round k+1 runs.  A rank stores its slots side by side:
+    round k at local columns [offset(k), offset(k) + width(k)), local width
+    sum(width).  By default every round has the same width `sub` (offset(k) =
+    k*sub); `shares` sizes the rounds unequally (tail_shares: a short last
+    round, whose exchange is the one the step leaves exposed).  rounds=1 is
+    exactly bucket_bounds().
     """
 
-    def __init__(self, P: int, world: int, rounds: int = 1, align: int = ALIGN):
+    def __init__(self, P: int, world: int, rounds: int = 1, align: int = ALIGN,
+                 shares: Optional[Sequence[float]] = None):
         if world < 1 or rounds < 1:
             raise ValueError("world and rounds must be >= 1")
         self.P, self.world, self.rounds = P, world, rounds
         units = -(-P // align)
-        self.sub = align * -(-units // (world * rounds)) if P else 0
-        self.local_width = rounds * self.sub
-        self.padded_total = rounds * world * self.sub
+        if shares is None or len(set(shares)) <= 1:
+            if shares is not None and len(shares) != rounds:
+                raise ValueError(f"{len(shares)} shares for {rounds} rounds")
+            w = align * -(-units // (world * rounds)) if P else 0
+            self.widths = [w] * rounds
+        else:
+            if len(shares) != rounds or min(shares) <= 0:
+                raise ValueError(f"need {rounds} positive shares, got {list(shares)}")
+            tot = float(sum(shares))
+            # each round's slot rounds UP to whole align units, so the rounds cover [0, P)
+            self.widths = [align * math.ceil(units * s / (world * tot)) if P else 0 for s in shares]
+            while P and world * sum(self.widths) < align * units:  # float rounding slack
+                self.widths[0] += align
+        self.sub = self.widths[0]  # the uniform layout's slot width (offset(k) = k*sub there)
+        self._offs = [0]
+        for w in self.widths:
+            self._offs.append(self._offs[-1] + w)
+        self.local_width = self._offs[-1]
+        self.padded_total = world * self.local_width
+
+    @property
+    def uniform(self) -> bool:
+        return len(set(self.widths)) <= 1
+
+    def width(self, k: int) -> int:
+        return self.widths[k]
+
+    def offset(self, k: int) -> int:
+        """Local column of round k's slot in a rank's side-by-side storage."""
+        return self._offs[k]
 
     def slot(self, rank: int, k: int) -> Tuple[int, int]:
         """Global [lo, hi) of rank's k-th slot (clipped to P; may be empty)."""
-        j = k * self.world + rank
-        return min(self.P, j * self.sub), min(self.P, (j + 1) * self.sub)
+        lo = self.world * self._offs[k] + rank * self.widths[k]
+        return min(self.P, lo), min(self.P, lo + self.widths[k])
 
     def slots(self, rank: int) -> List[Tuple[int, int]]:
         return [self.slot(rank, k) for k in range(self.rounds)]
 
     def round_range(self, k: int) -> Tuple[int, int]:
-        return k * self.world * self.sub, (k + 1) * self.world * self.sub
+        return self.world * self._offs[k], self.world * self._offs[k + 1]
 
 
 _fold_streams: dict = {}
@@ -193,7 +236,6 @@ class ShardedAggregator:
         return full
 
     def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
-        sub = layout.sub
         bf16 = X_local.dtype == torch.bfloat16
         odt = torch.bfloat16 if bf16 else torch.float32
         full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
@@ -203,15 +245,15 @@ class ShardedAggregator:
         local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=X_local.device) if bf16 else None
         works = []
         for k in range(layout.rounds):
-            piece = local[k * sub:(k + 1) * sub]
-            if sub:
+            a, b = layout.offset(k), layout.offset(k) + layout.width(k)
+            piece = local[a:b]
+            if b > a:
                 if bf16:
-                    _, pb = self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece, total=total,
-                                      want_bf16=True)
-                    local_b[k * sub:(k + 1) * sub].copy_(pb)
+                    _, pb = self.fold(X_local[:, a:b], weights, scores, out=piece, total=total, want_bf16=True)
+                    local_b[a:b].copy_(pb)
                 else:
-                    self.fold(X_local[:, k * sub:(k + 1) * sub], weights, scores, out=piece, total=total)
-            send = local_b[k * sub:(k + 1) * sub] if bf16 else piece
+                    self.fold(X_local[:, a:b], weights, scores, out=piece, total=total)
+            send = local_b[a:b] if bf16 else piece
             lo, hi = layout.round_range(k)
             if self.world == 1:
                 full[lo:hi].copy_(send)

@@ -190,9 +190,13 @@ int fa_copy_peer(void* dst, int dst_device, const void* src, int src_device, int
  *                      pieces must stay valid until fa_ingest_finish returns.
  *   fa_ingest_finish:  fold the last chunk and divide by `divisor`; returns when
  *                      every copy is done and every DMA and fold is enqueued
- *                      (the caller waits on `stream` for the result)
+ *                      (the caller waits on `stream` for the result); after an
+ *                      error it returns once no copy reads the pieces any more
  *   fa_ingest_destroy: wait for outstanding copies, free everything.
- * The pipe is reusable round after round (begin ... finish). */
+ * The pipe is reusable round after round (begin ... finish).  A begin after a
+ * round that was abandoned (an add failed, or finish never came) drains that
+ * round first (its queued chunks are not folded) and drops its partly filled
+ * chunk, so none of its rows join the new round. */
 typedef struct fa_ingest fa_ingest;
 int fa_ingest_create(fa_ingest** pipe, int64_t P, int64_t chunk_bytes, int slots, int device);
 int fa_ingest_rows_per_chunk(const fa_ingest* pipe);

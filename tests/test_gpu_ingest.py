@@ -278,3 +278,42 @@ def test_native_pipe_chunk_ramps(dev, expected, chunk_rows):
     got = sf.finish().cpu().numpy()
     exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
     assert G.same_bits(got, exp)
+
+
+def test_native_pipe_abandoned_round_then_reuse_raw_abi(dev):
+    """Through the C-ABI: a round abandoned with a chunk half filled (no finish),
+    then fa_ingest_begin on the SAME pipe: the abandoned rows are dropped, the
+    new round is bit-exact (the Python class never reuses a failed pipe; the
+    C-ABI contract allows it)."""
+    import ctypes
+
+    import torch
+
+    from fedlesscan_amd import _lib
+    L = _lib.load()
+    N, P = 9, 5003
+    X = synth.clients_f32(64, N, 0, P)
+    w = synth.cardinalities(64, N)
+    ldx = (P + 63) // 64 * 64
+    h = ctypes.c_void_p()
+    _lib.call("fa_ingest_create", ctypes.byref(h), P, 4 * ldx * 4, 3, dev.index)
+    try:
+        acc = torch.empty(P, dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        junk = np.full(P, 1e6, np.float32)
+        ptrs = (ctypes.c_void_p * 1)(junk.ctypes.data)
+        size = (ctypes.c_int64 * 1)(junk.nbytes)
+        _lib.check(L.fa_ingest_begin(h, acc.data_ptr(), st, 0), "begin")
+        for _ in range(2):  # chunk 0 takes 1 row (sent), chunk 1 ramps to 2 rows: half filled
+            _lib.check(L.fa_ingest_add(h, ptrs, size, 1, 5.0, 1.0, 0), "add junk")
+        _lib.check(L.fa_ingest_begin(h, acc.data_ptr(), st, N), "begin after an abandoned round")
+        for i in range(N):
+            row = np.ascontiguousarray(X[i])
+            _lib.check(L.fa_ingest_add(h, (ctypes.c_void_p * 1)(row.ctypes.data), (ctypes.c_int64 * 1)(row.nbytes),
+                                       1, float(np.float32(w[i])), 1.0, 0), "add")
+        _lib.check(L.fa_ingest_finish(h, float(np.float32(sum(w)))), "finish")
+        got = acc.cpu().numpy()
+    finally:
+        L.fa_ingest_destroy(h)
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    assert G.same_bits(got, exp)

@@ -20,7 +20,9 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 N, SEED = 41, 21
-CASES = [("f32", 10007, 4), ("f32", 262144 + 5, 4), ("bf16", 8 * 1000 + 3, 4), ("bf16", 65536, 3)]
+# (dtype, P, rounds, tail): tail < 1 is the short-last-round layout (tail_shares)
+CASES = [("f32", 10007, 4, 1.0), ("f32", 262144 + 5, 4, 1.0), ("bf16", 8 * 1000 + 3, 4, 1.0), ("bf16", 65536, 3, 1.0),
+         ("f32", 262144 + 5, 4, 0.25), ("bf16", 100003, 4, 0.1)]
 
 
 def _free_port():
@@ -38,7 +40,7 @@ def _scores(seed, n):
 def _rccl_worker(port, q):
     import torch as T
     import torch.distributed as dist
-    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, tail_shares
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     T.cuda.set_device(0)
     dev = T.device("cuda", 0)
@@ -48,18 +50,18 @@ def _rccl_worker(port, q):
         agg = ShardedAggregator()
         w = synth.cardinalities(SEED, N)
         sc = _scores(SEED, N)
-        for dt, P, rounds in CASES:
-            lay = SlotLayout(P, 1, rounds)
+        for dt, P, rounds, tail in CASES:
+            lay = SlotLayout(P, 1, rounds, shares=tail_shares(rounds, tail))
             bf16 = dt == "bf16"
             X = T.zeros((N, lay.local_width), dtype=T.int16 if bf16 else T.float32, device=dev)
             for k, (lo, hi) in enumerate(lay.slots(0)):
                 if hi > lo:
                     part = (synth.clients_bf16(SEED, N, lo, hi - lo).view(np.int16) if bf16
                             else synth.clients_f32(SEED, N, lo, hi - lo))
-                    X[:, k * lay.sub:k * lay.sub + hi - lo] = T.from_numpy(part).to(dev)
+                    X[:, lay.offset(k):lay.offset(k) + hi - lo] = T.from_numpy(part).to(dev)
             for scored in (False, True):
                 full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
-                out[(dt, P, scored)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
+                out[(dt, P, tail, scored)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
         m = G.manifest()["f32_small"]
         layers = agg.aggregate_layers(G.parameters("f32_small"), m["weights"])
         out["layers"] = [np.array(a) for a in layers]
@@ -81,16 +83,17 @@ def test_rccl_world1_slots_and_layers_bit_exact():
     assert got["backend"] == "nccl"
     w = synth.cardinalities(SEED, N)
     sc = _scores(SEED, N)
-    for dt, P, _ in CASES:
+    for dt, P, _, tail in CASES:
         for scored in (False, True):
             s = sc if scored else None
             if dt == "bf16":
                 _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(SEED, N, 0, P), w, s)
-                assert np.array_equal(np.frombuffer(got[(dt, P, scored)], dtype=np.uint16), exp), (dt, P, scored)
+                assert np.array_equal(np.frombuffer(got[(dt, P, tail, scored)], dtype=np.uint16), exp), \
+                    (dt, P, tail, scored)
             else:
                 exp = O.fedavg_stacked(synth.clients_f32(SEED, N, 0, P), w, s)
-                assert np.array_equal(np.frombuffer(got[(dt, P, scored)], dtype=np.uint32),
-                                      exp.view(np.uint32)), (dt, P, scored)
+                assert np.array_equal(np.frombuffer(got[(dt, P, tail, scored)], dtype=np.uint32),
+                                      exp.view(np.uint32)), (dt, P, tail, scored)
     exp_layers = G.expected("f32_small", "fedavg")
     assert len(got["layers"]) == len(exp_layers)
     assert all(a.shape == b.shape and G.same_bits(a, b) for a, b in zip(got["layers"], exp_layers))

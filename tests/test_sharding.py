@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from fedlesscan_amd import synth
-from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, bucket_bounds, chunk_size
+from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, bucket_bounds, chunk_size, tail_shares
 
 
 def test_bucket_bounds_cover_and_align():
@@ -32,8 +32,18 @@ def test_bucket_bounds_cover_and_align():
 def test_slot_layout_partitions_the_vector():
     for P in (1, 64, 1000, 10007, 10_000_000):
         for world in (1, 2, 3, 8):
-            for rounds in (1, 2, 4):
-                lay = SlotLayout(P, world, rounds)
+            for rounds, tail in ((1, 1), (2, 1), (4, 1), (2, 0.5), (4, 0.25), (4, 0.01), (8, 0.125)):
+                lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, tail))
+                assert lay.local_width == sum(lay.widths) and lay.padded_total == world * lay.local_width
+                assert all(w % 64 == 0 for w in lay.widths)
+                assert [lay.offset(k) for k in range(rounds)] == [sum(lay.widths[:k]) for k in range(rounds)]
+                if tail == 1:
+                    assert lay.uniform and lay.widths == [lay.sub] * rounds
+                elif P >= 64 * world * rounds * 100:  # big enough for the ratio to show through the alignment
+                    assert lay.widths[-1] < lay.widths[0]
+                    assert abs(lay.widths[-1] / lay.widths[0] - tail) < 0.02
+                # no round is wholly padding beyond what one aligned unit per slot needs
+                assert world * (lay.local_width - len(lay.widths) * 64) < P + 64 * world * rounds
                 cover = []
                 for r in range(world):
                     for k, (lo, hi) in enumerate(lay.slots(r)):
@@ -117,16 +127,17 @@ def test_sharded_fold_gloo_matches_oracle(world, P, scored):
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
 
 
-def _slot_worker(rank, world, port, N, P, rounds, seed, q):
+def _slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         agg = ShardedAggregator(fold=_oracle_fold)
-        lay = SlotLayout(P, world, rounds)
+        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, tail))
         X = torch.zeros((N, lay.local_width))
         for k, (lo, hi) in enumerate(lay.slots(rank)):
             if hi > lo:
-                X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(synth.clients_f32(seed, N, lo, hi - lo))
+                o = lay.offset(k)
+                X[:, o:o + hi - lo] = torch.from_numpy(synth.clients_f32(seed, N, lo, hi - lo))
         w = synth.cardinalities(seed, N)
         full = agg.aggregate_slots(X, w, None, lay)
         q.put((rank, full.numpy().tobytes()))
@@ -134,14 +145,17 @@ def _slot_worker(rank, world, port, N, P, rounds, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,rounds", [(2, 10007, 3), (3, 5000, 2), (2, 64, 4)])
-def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds):
+@pytest.mark.parametrize("world,P,rounds,tail", [(2, 10007, 3, 1.0), (3, 5000, 2, 1.0), (2, 64, 4, 1.0),
+                                                 (2, 10007, 4, 0.25), (3, 20000, 3, 0.1)])
+def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds, tail):
+    """Equal rounds and a short last round (tail_shares) reassemble the same model."""
     from oracle import fedavg_oracle as O
     N, seed = 7, 23
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, N, P, rounds, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, N, P, rounds, seed, q, tail))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
@@ -154,18 +168,18 @@ def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds):
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
 
 
-def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q):
+def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
     """BASELINE config 4's layout in miniature: bf16 client rows in round-robin
     slots, fp32 fold per slot, RNE-bf16 slot outputs all-gathered (2 B/param)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         agg = ShardedAggregator(fold=_oracle_fold)
-        lay = SlotLayout(P, world, rounds)
+        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, tail))
         X = torch.zeros((N, lay.local_width), dtype=torch.int16)
         for k, (lo, hi) in enumerate(lay.slots(rank)):
             if hi > lo:
-                X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(
+                X[:, lay.offset(k):lay.offset(k) + hi - lo] = torch.from_numpy(
                     synth.clients_bf16(seed, N, lo, hi - lo).view(np.int16))
         w = synth.cardinalities(seed, N)
         sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
@@ -176,14 +190,14 @@ def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,rounds", [(2, 4099, 4), (3, 1000, 2)])
-def test_bf16_slot_gather_gloo_matches_oracle(world, P, rounds):
+@pytest.mark.parametrize("world,P,rounds,tail", [(2, 4099, 4, 1.0), (3, 1000, 2, 1.0), (2, 9000, 4, 0.25)])
+def test_bf16_slot_gather_gloo_matches_oracle(world, P, rounds, tail):
     from oracle import fedavg_oracle as O
     N, seed = 6, 29
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bf16_slot_worker, args=(r, world, port, N, P, rounds, seed, q))
+    procs = [ctx.Process(target=_bf16_slot_worker, args=(r, world, port, N, P, rounds, seed, q, tail))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -4,8 +4,9 @@
 // left fold with separate roundings).  Many rounds on several pipes from
 // several threads at once, random chunk sizes, slot counts, piece splits and
 // scored / plain rows; every round is compared bit for bit with a direct CPU
-// fold of the same rows.  Also: errors mid-round (a short row, mixed scores)
-// followed by destroy, and finish with no rows.
+// fold of the same rows.  Also: errors mid-round (a short row, mixed scores),
+// a round abandoned with a chunk half filled and the pipe reused (bit-exact),
+// destroy with copies possibly in flight, and finish with no rows.
 //   tools/ingest_pipe_stress.sh   (builds with -fsanitize=thread, then address,undefined)
 #include <stdint.h>
 #include <stdio.h>
@@ -113,6 +114,25 @@ static void worker(int tid, int rounds) {
         check(fa_ingest_add(pipe, &src0, &full, 1, 1.f, 1.f, 0) == FA_OK, "add ok");
         check(fa_ingest_add(pipe, &src0, &shortb, 1, 1.f, 1.f, 0) == FA_ERR_SHAPE, "short row rejected");
         check(fa_ingest_add(pipe, &src0, &full, 1, 1.f, 0.5f, 1) == FA_ERR_SHAPE, "mixed scores rejected");
+        // abandon that round with a chunk half filled (the second chunk ramps to 2 rows), then
+        // reuse the pipe: the abandoned rows must not join the next round
+        check(fa_ingest_add(pipe, &src0, &full, 1, 7.f, 1.f, 0) == FA_OK, "add ok 2");
+        check(fa_ingest_begin(pipe, acc.data(), nullptr, 0) == FA_OK, "begin after an abandoned round");
+        for (int64_t i = 0; i < N; ++i) {
+            const void* src = X.data() + i * P;
+            check(fa_ingest_add(pipe, &src, &full, 1, a[i], s[i], 0) == FA_OK, "add after abandon");
+        }
+        {
+            float total = 0.f;
+            for (int64_t i = 0; i < N; ++i) total = total + a[i];
+            check(fa_ingest_finish(pipe, total) == FA_OK, "finish after abandon");
+            std::vector<float> exp(P);
+            fa_fold_f32(X.data(), N, P, P, a.data(), nullptr, nullptr, total, 1, exp.data(), nullptr);
+            check(memcmp(exp.data(), acc.data(), P * 4) == 0, "bit-exact after an abandoned round");
+        }
+        // abandoned again, now with copies possibly in flight: destroy
+        check(fa_ingest_begin(pipe, acc.data(), nullptr, 0) == FA_OK, "begin 4");
+        for (int k = 0; k < 3; ++k) check(fa_ingest_add(pipe, &src0, &full, 1, 1.f, 1.f, 0) == FA_OK, "add 3");
         fa_ingest_destroy(pipe);
         fa_ingest* empty = nullptr;
         check(fa_ingest_create(&empty, P, chunk, slots, 0) == FA_OK, "create 2");
