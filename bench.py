@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--tail", type=float, default=1.0,
                     help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
                          "left exposed after the step's folds); 1 = equal rounds")
+    ap.add_argument("--tail-steps", type=int, default=1,
+                    help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
+                         "rounds: shares 1, 1, 0.5, 0.25)")
     return ap.parse_args()
 
 
@@ -195,11 +198,11 @@ class Workload:
     slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
     With rounds=1 that is one contiguous bucket per rank."""
 
-    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0, tail=1.0):
+    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0, tail=1.0, tail_steps=1):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
         self.layout = SlotLayout(self.P_total, world, rounds, align=ALIGN if align is None else align,
-                                 shares=tail_shares(rounds, tail))
+                                 shares=tail_shares(rounds, tail, tail_steps))
         self.slots = self.layout.slots(rank)
         self.P = sum(hi - lo for lo, hi in self.slots)  # real columns this rank folds
         self.rank, self.world, self.dev = rank, world, dev
@@ -350,7 +353,7 @@ def main():
     if args.splitn:
         args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra,
-                  tail=args.tail if rounds > 1 else 1.0)
+                  tail=args.tail if rounds > 1 else 1.0, tail_steps=args.tail_steps)
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,

@@ -39,14 +39,24 @@ def chunk_size(P: int, world: int, align: int = ALIGN) -> int:
     return b[0][1] - b[0][0]
 
 
-def tail_shares(rounds: int, tail: float) -> List[float]:
-    """Round shares with the last round `tail` times the others (tail=1: equal).
-    Only the last round's exchange is left exposed after the step's folds, so a
-    short last round shortens it; the earlier rounds' gathers hide behind the
-    folds that follow them."""
+def tail_shares(rounds: int, tail: float, steps: int = 1) -> List[float]:
+    """Round shares whose last `steps` rounds shrink geometrically down to
+    `tail` times the full rounds (tail=1: equal rounds; rounds=4, tail=0.25,
+    steps=2: [1, 1, 0.5, 0.25]).
+
+    Round k's all-gather runs while round k+1 folds, so only the last round's
+    exchange is left exposed after the step's folds: a short last round
+    shortens it.  But each gather must also fit behind the NEXT fold, or it is
+    exposed instead: with gather/fold time ratio rho per parameter (C4 bf16 on
+    8 GPUs ~0.6, C3 fp32 ~0.2), round k+1 should keep at least
+    rho of round k's width, hence the geometric steps rather than one cut."""
     if not 0 < tail <= 1:
         raise ValueError("tail must be in (0, 1]")
-    return [1.0] * (rounds - 1) + [float(tail)]
+    steps = max(1, min(int(steps), rounds - 1)) if rounds > 1 else 0
+    if steps == 0:
+        return [1.0] * rounds
+    r = float(tail) ** (1.0 / steps)
+    return [1.0] * (rounds - steps) + [r ** (j + 1) for j in range(steps)]
 
 
 class SlotLayout:

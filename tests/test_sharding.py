@@ -64,6 +64,21 @@ def test_slot_layout_partitions_the_vector():
                     assert [lay.slot(r, 0) for r in range(world)] == bucket_bounds(P, world)
 
 
+def test_tail_shares():
+    assert tail_shares(4, 1.0) == [1.0] * 4
+    assert tail_shares(4, 0.25) == [1.0, 1.0, 1.0, 0.25]
+    assert tail_shares(4, 0.25, 2) == [1.0, 1.0, 0.5, 0.25]
+    assert tail_shares(1, 0.25, 2) == [1.0]
+    sh = tail_shares(4, 0.125, 9)  # steps capped at rounds - 1
+    assert sh[0] == 1.0 and abs(sh[-1] - 0.125) < 1e-12 and sh == sorted(sh, reverse=True)
+    with pytest.raises(ValueError):
+        tail_shares(4, 0.0)
+    lay = SlotLayout(100_000_000, 8, 4, shares=tail_shares(4, 0.25, 2))
+    w = lay.widths
+    assert w[0] == w[1] and abs(w[2] / w[0] - 0.5) < 1e-3 and abs(w[3] / w[0] - 0.25) < 1e-3
+    assert lay.round_range(3)[1] == lay.padded_total >= 100_000_000
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
