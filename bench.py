@@ -421,6 +421,19 @@ def main():
             ev[1].record(stream)
 
     torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
+    # the library's tuner times each candidate kernel form on the first calls of
+    # a new shape (fa_set_autotune): run the folds alone (no collectives, so the
+    # ranks need not agree on a count) until every slot shape has its form, as
+    # the first aggregation rounds of a deployment would
+    L = _lib.load()
+    tune_calls = 0
+    if args.variant == 0 and L.fa_set_autotune(-1) == 1:
+        for tune_calls in range(1, 201):
+            for k in range(rounds):
+                wl.launch(0, k)
+            torch.cuda.synchronize()
+            if L.fa_autotune_pending() == 0:
+                break
     for _ in range(args.warmup):
         step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -495,6 +508,12 @@ def main():
     # the committed PMC pass measured exactly this launch: the unmodified config, one fold per step
     traffic, traffic_src = (read_traffic(args.config) if not (args.clients or args.params) and rounds == 1
                             else (None, None))
+    if traffic is not None and wl.dtype == "f32" and args.variant == 0:
+        # the committed pass measured the policy's form; another measured choice is another kernel
+        form = L.fa_fold_form(1, wl.N, lay.width(0), wl.ldx, 1 if wl.scored else 0, stream.cuda_stream).decode()
+        pol = B.fa_f32_pick_name(wl.N, lay.width(0), 0).decode()
+        if form != pol:
+            traffic, traffic_src = None, f"{traffic_src}: measured form {pol}, this run took {form}"
     devices = rank_devices(dev)
     cpu = None
     # the CPU baseline runs on rank 0 at every world size, after the timed
@@ -537,8 +556,15 @@ def main():
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
                 # the kernel form the product's fp32 auto fold takes for one launch of this rank
-                "fold_form": (B.fa_f32_pick_name(wl.N, lay.sub, 0).decode()
-                              if wl.dtype == "f32" and args.variant == 0 and not args.unpadded else None),
+                # the kernel form each distinct slot width ran (the tuner's measured choice), and the
+                # shape policy's form for the first slot (what runs with FEDAVG_AUTOTUNE=0)
+                "fold_form": ({str(w): L.fa_fold_form(1 if wl.dtype == "f32" else 2, wl.N, w, wl.ldx,
+                                                      1 if wl.scored else 0, stream.cuda_stream).decode()
+                               for w in dict.fromkeys(lay.widths)} if args.variant == 0 else None),
+                "fold_policy": (B.fa_f32_pick_name(wl.N, lay.sub, 0).decode()
+                                if wl.dtype == "f32" and args.variant == 0 and not args.unpadded else None),
+                "autotune": {"on": bool(L.fa_set_autotune(-1)), "tuning_calls": tune_calls,
+                             "pending": L.fa_autotune_pending()},
             },
             "roofline": {
                 "bound": "hbm",

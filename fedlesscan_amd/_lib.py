@@ -65,6 +65,9 @@ _PROTOS = {
     "fa_host_free": (_int, [_vp]),
     "fa_copy_h2d": (_int, [_vp, _vp, _i64, _vp]),
     "fa_copy_peer": (_int, [_vp, _int, _vp, _int, _i64, _vp]),
+    "fa_set_autotune": (_int, [_int]),
+    "fa_autotune_pending": (_int, []),
+    "fa_fold_form": (ctypes.c_char_p, [_int, _i64, _i64, _i64, _int, _vp]),
     "fa_ingest_create": (_int, [_vp, _i64, _i64, _int, _int]),
     "fa_ingest_rows_per_chunk": (_int, [_vp]),
     "fa_ingest_begin": (_int, [_vp, _vp, _vp, _i64]),

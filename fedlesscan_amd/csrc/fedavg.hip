@@ -255,6 +255,23 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const f
     return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
 }
 
+int fa_set_autotune(int mode) { return g_tuner.set_mode(mode); }
+int fa_autotune_pending(void) { return g_tuner.pending(); }
+
+const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored, void* stream) {
+    if ((kind != FA_FOLD_F32 && kind != FA_FOLD_BF16) || N < 1 || P < 1) return "";
+    StreamDevice on_stream_device(stream);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return "";
+    }
+    const int tuned = g_tuner.set_mode(-1) ? g_tuner.chosen(dev, kind, N, P, ldx, scored != 0) : -2;
+    if (tuned == -1) return "";
+    if (kind == FA_FOLD_F32) return f32_pick_name(tuned >= 0 ? (F32Pick)tuned : pick_f32(N, P));
+    return bf16_form_name(tuned >= 0 ? (Bf16Form)tuned : pick_bf16(N, P));
+}
+
 int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const double* a, const double* s,
                   double divisor, double* out, void* stream) {
     int rc = check_common(N, P, ldx, X, a, out);

@@ -34,7 +34,14 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
 
 #include "fedavg_hip.h"
 
@@ -1408,7 +1415,11 @@ int cu_count() {
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
 enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
-                     kTileC4Plain, kGsBalC2, kGsBalC4 };
+                     kTileC4Plain, kGsBalC2, kGsBalC4,
+                     // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32 };
+constexpr int kNumF32Picks = (int)F32Pick::kLdsQfW4T32 + 1;
+inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
         case F32Pick::kLdsW2T16: return "lds_w2_t16";
@@ -1423,6 +1434,11 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kTileC4Plain: return "tile_16k_ps";
         case F32Pick::kGsBalC2: return "gs_bal_8k";
         case F32Pick::kGsBalC4: return "gs_bands_16k";
+        case F32Pick::kGsBands6: return "gs_bands6_16k";
+        case F32Pick::kGs1C4: return "gs1_16k";
+        case F32Pick::kTileU8C2: return "tile_8k";
+        case F32Pick::kEvenU4C4: return "even_u4c4";
+        case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
     }
     return "";
 }
@@ -1700,6 +1716,323 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
 }
 
 
+// ---------------------------------------------------------------------------
+// Measured form choice (the tuner).  The policy picks above are fitted to
+// sweeps over measured shapes; between those shapes every form swings with
+// how the tiles fall on the CUs (1024 x 909K params: the policy's form 0.70 ms,
+// the even split 0.53 ms; 256 x 3.57M bf16: 0.337 against 0.295 ms;
+// profiles/r03_slot_sweep/).  Every form computes the same bits, so for a plain
+// one-shot fold the tuner times the shape's candidate forms on the caller's
+// own calls: the first calls of a new (device, dtype, N, P, pitch, scored)
+// shape each run one candidate between two events on the caller's stream (no
+// synchronisation: the events are read with hipEventQuery on later calls),
+// kTuneSamples per candidate, and once all are in, every later call of that
+// shape runs the fastest -- the policy's own pick unless another form beats
+// it by more than 3 % (box-to-box spread is ~2-5 %).
+// FEDAVG_AUTOTUNE=0 (or fa_set_autotune(0)) keeps the policy pick.
+// ---------------------------------------------------------------------------
+constexpr int kTuneF32 = 1, kTuneBf16 = 2;
+constexpr int kTuneSamples = 2;
+constexpr float kTuneMargin = 0.97f;
+
+struct TuneChoice {
+    int form;
+    int64_t ticket = -1;  // >= 0: a timed sample; end() records its closing event
+};
+
+class Tuner {
+  public:
+    static int env_mode() {
+        const char* e = getenv("FEDAVG_AUTOTUNE");
+        return (e && e[0] == '0') ? 0 : 1;
+    }
+    int set_mode(int m) {
+        const int prev = mode_.load();
+        if (m >= 0) mode_.store(m ? 1 : 0);
+        return prev;
+    }
+    // The form for this call; `cands(v)` fills the candidate forms (v[0] = the
+    // policy pick) the first time the shape is seen.  Runs on the stream's
+    // device (the callers hold a StreamDevice).
+    template <class Cands>
+    TuneChoice begin(int kind, int64_t N, int64_t P, int64_t ldx, bool scored, int policy, hipStream_t st,
+                     Cands cands) {
+        if (!mode_.load()) return {policy};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return {policy};
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
+        if (it == map_.end()) {
+            Entry e;
+            cands(e.cand);
+            if (e.cand.size() <= 1) e.chosen = policy;
+            e.best.assign(e.cand.size(), 3.4e38f);
+            e.got.assign(e.cand.size(), 0);
+            e.inflight.assign(e.cand.size(), 0);
+            it = map_.emplace(Key{dev, kind, N, P, ldx, scored ? 1 : 0}, std::move(e)).first;
+        }
+        Entry& e = it->second;
+        if (e.chosen >= 0) return {e.chosen};
+        harvest(e);
+        if (decide(e)) return {e.chosen};
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+            (void)hipGetLastError();
+            return {e.cand[0]};
+        }
+        if (cs != hipStreamCaptureStatusNone) return {e.cand[0]};  // no events inside a graph capture
+        // the next candidate still short of samples (in flight ones count)
+        const int n = (int)e.cand.size();
+        int ci = -1;
+        for (int j = 0; j < n; ++j) {
+            const int c = (e.rr + j) % n;
+            if (e.got[c] + e.inflight[c] < kTuneSamples) {
+                ci = c;
+                break;
+            }
+        }
+        if (ci < 0) return {e.cand[0]};  // every sample is in flight: untimed policy launch
+        e.rr = (ci + 1) % n;
+        Sample smp;
+        if (!take_event(e, &smp.e0) || !take_event(e, &smp.e1)) return {e.cand[0]};
+        if (hipEventRecord(smp.e0, st) != hipSuccess) {
+            (void)hipGetLastError();
+            e.free.push_back(smp.e0);
+            e.free.push_back(smp.e1);
+            return {e.cand[0]};
+        }
+        smp.c = ci;
+        smp.ticket = next_ticket_++;
+        e.inflight[ci]++;
+        e.samples.push_back(smp);
+        return {e.cand[ci], smp.ticket};
+    }
+    // Close a timed sample: its second event goes on the stream after the launch.
+    void end(const TuneChoice& tc, int kind, int64_t N, int64_t P, int64_t ldx, bool scored, hipStream_t st) {
+        if (tc.ticket < 0) return;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
+        if (it == map_.end()) return;
+        for (Sample& smp : it->second.samples)
+            if (smp.ticket == tc.ticket) {
+                if (hipEventRecord(smp.e1, st) == hipSuccess) smp.armed = true;
+                else (void)hipGetLastError();  // never armed: dropped when the shape decides
+                break;
+            }
+    }
+    int pending() {
+        std::lock_guard<std::mutex> lk(mu_);
+        int n = 0;
+        for (auto& kv : map_) {
+            if (kv.second.chosen >= 0) continue;
+            harvest(kv.second);  // the shape may have all it needs without a further call
+            if (!decide(kv.second)) ++n;
+        }
+        return n;
+    }
+    // chosen form (>= 0), -1 while the shape is being measured, -2 unknown shape
+    int chosen(int dev, int kind, int64_t N, int64_t P, int64_t ldx, bool scored) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
+        if (it == map_.end()) return -2;
+        if (it->second.chosen < 0) {
+            harvest(it->second);
+            decide(it->second);
+        }
+        return it->second.chosen;
+    }
+
+  private:
+    typedef std::tuple<int, int, int64_t, int64_t, int64_t, int> Key;
+    struct Sample {
+        int c = 0;
+        int64_t ticket = 0;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        bool armed = false;
+    };
+    struct Entry {
+        std::vector<int> cand;
+        std::vector<float> best;
+        std::vector<int> got, inflight;
+        std::vector<Sample> samples;
+        std::vector<hipEvent_t> free;
+        int rr = 0, chosen = -1;
+    };
+    bool take_event(Entry& e, hipEvent_t* ev) {
+        if (!e.free.empty()) {
+            *ev = e.free.back();
+            e.free.pop_back();
+            return true;
+        }
+        if (hipEventCreate(ev) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return true;
+    }
+    void harvest(Entry& e) {
+        for (size_t i = 0; i < e.samples.size();) {
+            Sample& smp = e.samples[i];
+            if (!smp.armed) {
+                ++i;
+                continue;
+            }
+            const hipError_t q = hipEventQuery(smp.e1);
+            if (q == hipErrorNotReady) {
+                ++i;
+                continue;
+            }
+            float ms = 0.f;
+            if (q == hipSuccess && hipEventElapsedTime(&ms, smp.e0, smp.e1) == hipSuccess && ms > 0.f) {
+                if (ms < e.best[smp.c]) e.best[smp.c] = ms;
+                e.got[smp.c]++;
+            } else {
+                (void)hipGetLastError();
+            }
+            e.inflight[smp.c]--;
+            e.free.push_back(smp.e0);
+            e.free.push_back(smp.e1);
+            e.samples.erase(e.samples.begin() + (long)i);
+        }
+    }
+    bool decide(Entry& e) {
+        if (e.chosen >= 0) return true;
+        for (size_t c = 0; c < e.cand.size(); ++c)
+            if (e.got[c] < kTuneSamples) return false;
+        size_t b = 0;
+        for (size_t c = 1; c < e.cand.size(); ++c)
+            if (e.best[c] < e.best[b]) b = c;
+        e.chosen = (e.best[b] < kTuneMargin * e.best[0]) ? e.cand[b] : e.cand[0];
+        bool busy = false;  // samples never armed (a failed record) keep their events
+        for (const Sample& smp : e.samples) busy |= smp.armed;
+        if (!busy) {
+            for (hipEvent_t ev : e.free) (void)hipEventDestroy(ev);
+            e.free.clear();
+        }
+        return true;
+    }
+    std::mutex mu_;
+    std::map<Key, Entry> map_;
+    std::atomic<int> mode_{env_mode()};
+    int64_t next_ticket_ = 0;
+};
+Tuner g_tuner;
+
+// fp32 candidates: the policy pick first, then the forms that won somewhere
+// near this shape in the sweeps (profiles/r02_small_n/, r03_even/, r03_slot_sweep/).
+inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v) {
+    auto add = [&](F32Pick p) {
+        for (int x : v)
+            if (x == (int)p) return;
+        v.push_back((int)p);
+    };
+    v.push_back(policy);
+    const int64_t nq = P >> 2, cus = cu_count();
+    const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
+    if (nq < (1 << 16)) {  // narrow models: the LDS-staged forms, the 4 KiB tile
+        for (F32Pick p : {F32Pick::kLdsW2T16, F32Pick::kLdsW2T16D2, F32Pick::kLdsW2T32, F32Pick::kLdsW4T24,
+                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1})
+            add(p);
+    } else if (tiles4 < 2 * cus) {  // under two 16 KiB tiles per CU: where the forms swing most
+        for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBalC2, F32Pick::kTileC4Plain, F32Pick::kTileC4,
+                          F32Pick::kTileU8C2, F32Pick::kTileC1, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32,
+                          F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6})
+            add(p);
+        if (N < 128) add(F32Pick::kColumn);
+    } else {  // large models: the grid-stride forms, the 16 KiB tile, the even split
+        for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBands6, F32Pick::kGsBalC2, F32Pick::kGs1C4,
+                          F32Pick::kTileC4Plain, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32})
+            add(p);
+    }
+}
+
+// Launch one fp32 form (the 16-B aligned vector path), every (scored,
+// accumulate, finalize) combination for the policy's forms; the tuning-only
+// forms instantiate the plain one-shot fold alone.
+inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N,
+                           int64_t P, int64_t ldx, const float* a, const float* s, const float* acc_in,
+                           float divisor, float* out) {
+    if (f32_tuning_only(pick) && (acc || !fin))
+        return fail(FA_ERR_ARG, "fold form %s runs one-shot folds only", f32_pick_name(pick));
+    int rc = FA_OK;
+    switch (pick) {  // every (scored, accumulate, finalize) combination
+        case F32Pick::kLdsW2T16:
+            // the narrowest models (one block per CU): two-wave blocks, four
+            // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
+            // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
+            rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW2T16D2:
+            rc = launch_lds_flags<2, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW2T32:
+            rc = launch_lds_flags<2, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW4T24:
+            rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW4T40:
+            rc = launch_lds_flags<4, 32, 40, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsW8:
+            rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kColumn:
+#define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
+            if (sc) {
+                if (acc) { if (fin) FA_SC(true, true, true); else FA_SC(true, true, false); }
+                else     { if (fin) FA_SC(true, false, true); else FA_SC(true, false, false); }
+            } else {
+                if (acc) { if (fin) FA_SC(false, true, true); else FA_SC(false, true, false); }
+                else     { if (fin) FA_SC(false, false, true); else FA_SC(false, false, false); }
+            }
+#undef FA_SC
+            break;
+        case F32Pick::kTileC1:  // plain stores (non-temporal ones cost 3-10 % here)
+            rc = launch_tile_flags<4, 1, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileC4:
+            rc = launch_tile_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileC4Plain:
+            rc = launch_tile_flags<8, 4, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kGsBalC2:
+            launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kGsBalC4:  // one band below 3 x CUs tiles; 3-pass bands were 0.3-1 % faster than
+                                 // 4-pass ones at 512-1024 clients (profiles/r02_bands/)
+            launch_gs_bands<8, 4, true, true>(st, 3, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        // tuning-only forms (the sweeps' winners between the policy's measured shapes)
+        case F32Pick::kGsBands6:
+            launch_gs_bands<8, 4, true>(st, 6, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kGs1C4:
+            launch_gs_flags<8, 4, true>(st, 1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kTileU8C2:
+            rc = launch_tile_flags<8, 2, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kEvenU4C4:
+            launch_even_flags<4, 4>(st, cu_count(), sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kLdsQfW4T32:  // LDS-staged, 4 waves, 16-row chunks of 32-quad tiles, quad fold
+            rc = launch_lds_flags<4, 16, 32, 2, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                                      divisor, out);
+            break;
+    }
+    return rc;
+}
+
 // The product fp32 fold: checks, then the scalar fallback for unaligned input
 // or the shape-picked vector fold (pick_f32).  acc_in continues a fold
 // (fa_fold_f32); with acc_in and N == 0 it only finalises.
@@ -1745,59 +2078,115 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
 #undef FA_SC
         return check_launch("k_fold_f32_scalar");
     }
-    int rc = FA_OK;
-    switch (pick_f32(N, P)) {  // every (scored, accumulate, finalize) combination
-        case F32Pick::kLdsW2T16:
-            // the narrowest models (one block per CU): two-wave blocks, four
-            // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
-            // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
-            rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW2T16D2:
-            rc = launch_lds_flags<2, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW2T32:
-            rc = launch_lds_flags<2, 16, 32, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW4T24:
-            rc = launch_lds_flags<4, 32, 24, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW4T40:
-            rc = launch_lds_flags<4, 32, 40, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kLdsW8:
-            rc = launch_lds_flags<8, 64, 32, 1, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kColumn:
-#define FA_SC(SC, ACC, FIN) launch_scalar<SC, ACC, FIN>(st, X, N, P, ldx, a, s, acc_in, divisor, out)
-            if (sc) {
-                if (acc) { if (fin) FA_SC(true, true, true); else FA_SC(true, true, false); }
-                else     { if (fin) FA_SC(true, false, true); else FA_SC(true, false, false); }
-            } else {
-                if (acc) { if (fin) FA_SC(false, true, true); else FA_SC(false, true, false); }
-                else     { if (fin) FA_SC(false, false, true); else FA_SC(false, false, false); }
-            }
-#undef FA_SC
-            break;
-        case F32Pick::kTileC1:  // plain stores (non-temporal ones cost 3-10 % here)
-            rc = launch_tile_flags<4, 1, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kTileC4:
-            rc = launch_tile_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kTileC4Plain:
-            rc = launch_tile_flags<8, 4, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kGsBalC2:
-            launch_gs_flags<8, 2, true, kBlock, true>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        default:  // one band below 3 x CUs tiles; 3-pass bands were 0.3-1 % faster than
-                  // 4-pass ones at 512-1024 clients (profiles/r02_bands/)
-            launch_gs_bands<8, 4, true, true>(st, 3, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
+    const F32Pick policy = pick_f32(N, P);
+    // a plain one-shot fold (no accumulator in, with the divide) of a shape
+    // seen before takes the form the tuner measured fastest on this device
+    if (!acc && fin && N > 0) {
+        const TuneChoice tc = g_tuner.begin(kTuneF32, N, P, ldx, sc, (int)policy, st,
+                                            [&](std::vector<int>& c) { f32_candidates(N, P, (int)policy, c); });
+        int rc = launch_f32_pick((F32Pick)tc.form, st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+        g_tuner.end(tc, kTuneF32, N, P, ldx, sc, st);
+        if (rc) return rc;
+        return check_launch("fold_f32");
     }
+    int rc = launch_f32_pick(policy, st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
     if (rc) return rc;
     return check_launch("fold_f32");
+}
+
+// bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
+enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
+inline const char* bf16_form_name(Bf16Form f) {
+    switch (f) {
+        case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
+        case Bf16Form::kV8U4C4: return "bf16_tile_u4c4";
+        case Bf16Form::kV8U8C2: return "bf16_tile_u8c2";
+        case Bf16Form::kV8U8C1: return "bf16_tile_u8c1";
+        case Bf16Form::kBandsU8C4: return "bf16_bands4_u8c4";
+        case Bf16Form::kBandsU8C2: return "bf16_bands4_u8c2";
+        case Bf16Form::kBandsU2C8: return "bf16_bands2_u2c8";
+        case Bf16Form::kBandsU4C4: return "bf16_bands4_u4c4";
+        case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
+        case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
+        case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
+    }
+    return "";
+}
+
+// The policy's bf16 form by shape.
+inline Bf16Form pick_bf16(int64_t N, int64_t P) {
+    // 2.9M-5.6M params, 128+ clients (the 3.125M-param round slot of an 8-GPU C4 bucket):
+    // four octets per lane (8 rows x 4 x 16 B in flight per lane), column bands of 4
+    // passes: 0.238 against 0.260 ms at 256 x 3.125M (profiles/r03_c4_budget/), 5-11 %
+    // faster at 3.1M-5M and 128-256 clients, but 2-8 % slower at 2.5M-3M and 6.25M-8M
+    // (profiles/r02_slots/bf16_octets_scan/), hence the narrow range
+    if (N >= 128 && (P >> 3) >= 368000 && (P >> 3) < 700000) return Bf16Form::kBandsU8C4;
+    // per-GPU C4 buckets (256 x 12.5M) and their multi-GPU round slots
+    // (256 x 3.125M): grid-stride, 8 rows x 2 octets, balanced passes in
+    // column bands of 4 passes: +7 % over the row-streaming pick (DESIGN.md
+    // 5), +1-1.4 % over one block per CU (profiles/r02_slots/)
+    if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) return Bf16Form::kBandsU8C2;
+    // whole large models (C4's 100M on one GPU): balanced grid-stride
+    // launches over 32 KiB tiles (fewer tile switches per block), in
+    // column bands of 2 passes: +4 % over one launch
+    if ((P >> 3) >= ((int64_t)1 << 22)) return Bf16Form::kBandsU2C8;
+    // smaller models: one block per tile, octets per lane from the client count
+    switch (pick_octets(N, P)) {
+        case 8: return Bf16Form::kV8U2C8;
+        case 4: return Bf16Form::kV8U4C4;
+        case 2: return Bf16Form::kV8U8C2;
+        default: return Bf16Form::kV8U8C1;
+    }
+}
+
+inline void bf16_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v) {
+    auto add = [&](Bf16Form f) {
+        for (int x : v)
+            if (x == (int)f) return;
+        v.push_back((int)f);
+    };
+    v.push_back(policy);
+    if ((P >> 3) >= ((int64_t)1 << 17))
+        for (Bf16Form f : {Bf16Form::kBandsU8C2, Bf16Form::kBandsU8C4, Bf16Form::kBandsU4C4, Bf16Form::kGsBalU8C2,
+                           Bf16Form::kGs1U8C4, Bf16Form::kBandsU2C8, Bf16Form::kBandsU16C2, Bf16Form::kV8U8C1})
+            add(f);
+    else
+        for (Bf16Form f : {Bf16Form::kV8U8C1, Bf16Form::kV8U8C2, Bf16Form::kV8U4C4, Bf16Form::kV8U2C8,
+                           Bf16Form::kGs1U8C4, Bf16Form::kGsBalU8C2, Bf16Form::kBandsU8C4})
+            add(f);
+}
+
+inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                             const float* a, const float* s, float divisor, float* out_f32, uint16_t* out_bf16) {
+#define FA_BF(U, C)                                                                                         \
+    {                                                                                                       \
+        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);            \
+        const dim3 grid((unsigned)((units + per_block - 1) / per_block));                                   \
+        if (s)                                                                                              \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a, s, \
+                               divisor, out_f32, out_bf16);                                                 \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a,  \
+                               s, divisor, out_f32, out_bf16);                                              \
+    }
+    switch (f) {
+        case Bf16Form::kV8U2C8: FA_BF(2, 8); break;
+        case Bf16Form::kV8U4C4: FA_BF(4, 4); break;
+        case Bf16Form::kV8U8C2: FA_BF(8, 2); break;
+        case Bf16Form::kV8U8C1: FA_BF(8, 1); break;
+        case Bf16Form::kBandsU8C4: launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kBandsU8C2: launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kBandsU2C8: launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kBandsU4C4: launch_bf16_bands<4, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kBandsU16C2:
+            launch_bf16_bands<16, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kGsBalU8C2: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kGs1U8C4: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+    }
+#undef FA_BF
 }
 
 // The product bf16 fold (exact upcast, fp32 fold in order, optional RNE bf16 copy).
@@ -1818,45 +2207,11 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
                                divisor, out_f32, out_bf16);
         return check_launch("k_fedavg_bf16_scalar");
     }
-    if (N >= 128 && (P >> 3) >= 368000 && (P >> 3) < 700000) {
-        // 2.9M-5.6M params, 128+ clients (the 3.125M-param round slot of an 8-GPU C4 bucket):
-        // four octets per lane (8 rows x 4 x 16 B in flight per lane), column bands of 4
-        // passes: 0.238 against 0.260 ms at 256 x 3.125M (profiles/r03_c4_budget/), 5-11 %
-        // faster at 3.1M-5M and 128-256 clients, but 2-8 % slower at 2.5M-3M and 6.25M-8M
-        // (profiles/r02_slots/bf16_octets_scan/), hence the narrow range
-        launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-    } else if (N >= 128 && (P >> 3) >= ((int64_t)1 << 17) && (P >> 3) < ((int64_t)1 << 22)) {
-        // per-GPU C4 buckets (256 x 12.5M) and their multi-GPU round slots
-        // (256 x 3.125M): grid-stride, 8 rows x 2 octets, balanced passes in
-        // column bands of 4 passes: +7 % over the row-streaming pick (DESIGN.md
-        // 5), +1-1.4 % over one block per CU (profiles/r02_slots/)
-        launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-    } else if ((P >> 3) >= ((int64_t)1 << 22)) {
-        // whole large models (C4's 100M on one GPU): balanced grid-stride
-        // launches over 32 KiB tiles (fewer tile switches per block), in
-        // column bands of 2 passes: +4 % over one launch
-        launch_bf16_bands<2, 8>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-    } else {
-        // smaller models: one block per tile, octets per lane from the client count
-#define FA_BF(U, C)                                                                                         \
-    {                                                                                                       \
-        const int64_t per_block = (int64_t)kBlock * (C), units = (P >> 3) + ((P & 7) ? 1 : 0);            \
-        const dim3 grid((unsigned)((units + per_block - 1) / per_block));                                   \
-        if (s)                                                                                              \
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, true>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a, s, \
-                               divisor, out_f32, out_bf16);                                                 \
-        else                                                                                                \
-            hipLaunchKernelGGL((k_fedavg_bf16_v8<U, C, false>), grid, dim3(kBlock), 0, st, X, N, P, ldx, a,  \
-                               s, divisor, out_f32, out_bf16);                                              \
-    }
-        switch (pick_octets(N, P)) {
-            case 8: FA_BF(2, 8); break;
-            case 4: FA_BF(4, 4); break;
-            case 2: FA_BF(8, 2); break;
-            default: FA_BF(8, 1); break;
-        }
-#undef FA_BF
-    }
+    const Bf16Form policy = pick_bf16(N, P);
+    const TuneChoice tc = g_tuner.begin(kTuneBf16, N, P, ldx, s != nullptr, (int)policy, st,
+                                        [&](std::vector<int>& c) { bf16_candidates(N, P, (int)policy, c); });
+    launch_bf16_form((Bf16Form)tc.form, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+    g_tuner.end(tc, kTuneBf16, N, P, ldx, s != nullptr, st);
     return check_launch("fedavg_bf16");
 }
 

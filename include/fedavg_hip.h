@@ -20,7 +20,9 @@
  *    stall-aware variant, NULL for FedAvg; divisor = fl(sum_i n_i) with the
  *    sum taken exactly (Python int).  These are [device] arrays of N.
  *  - stream is a hipStream_t (NULL = legacy default stream).  All work is
- *    enqueued on it; no call synchronises.  Calls are stateless and reentrant.
+ *    enqueued on it; no call synchronises.  Calls are reentrant; the only
+ *    state they keep is the measured kernel form per shape (fa_set_autotune),
+ *    which changes which kernel runs, never the result.
  *  - Result, bit for bit:  acc = t_0; acc = acc + t_i (i = 1..N-1, in order);
  *    out = acc / divisor, where t_i = (x_i * a_i) [* s_i] with separate
  *    roundings (no FMA) and an IEEE divide.
@@ -126,6 +128,27 @@ int fa_fedavg_f32_ptrs_hostf(const float* const* xi, int64_t N, int64_t P,
 int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                          const float* a, const float* s, float divisor,
                          float* out_f32, uint16_t* out_bf16, void* stream);
+
+/* Measured form choice.  Every kernel form of the fp32 and bf16 folds
+ * computes the same bits; which is fastest depends on how a shape's tiles fall
+ * on the CUs.  For plain one-shot folds (fa_fedavg_f32 / _bf16 and their
+ * _hostf forms) the library times each candidate form on the first calls of a
+ * new (device, dtype, N, P, ldx, scored) shape -- one candidate per call,
+ * between two events on the caller's stream, read back without synchronising
+ * on later calls -- and from then on runs the fastest (the shape policy's own
+ * form unless another is > 3 % faster).  Outputs are bit-identical whatever
+ * form runs.  Library-wide switch, on unless FEDAVG_AUTOTUNE=0 at load.
+ *   fa_set_autotune:     1 on, 0 off (the policy form only), -1 query;
+ *                        returns the previous setting
+ *   fa_autotune_pending: shapes seen whose measurement is not complete
+ *   fa_fold_form:        the form a shape runs on the stream's device:
+ *                        the measured choice, "" while it is being measured,
+ *                        the policy's form for an unseen shape or with the
+ *                        tuner off.  kind: FA_FOLD_F32 or FA_FOLD_BF16. */
+enum fa_fold_kind { FA_FOLD_F32 = 1, FA_FOLD_BF16 = 2 };
+int fa_set_autotune(int mode);
+int fa_autotune_pending(void);
+const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored, void* stream);
 
 /* float64 updates (the reference unit-test fixture is float64,
  * test/test_aggregation.py:23-38). */
