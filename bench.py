@@ -64,6 +64,18 @@ CONFIGS = {
 }
 
 
+# Slot layout of the overlapped exchange at N > 1, per input dtype: (tail, steps)
+# for sharding.tail_shares.  Each round's all-gather must hide behind the next
+# round's fold, and the last one is exposed.  Per parameter, the gather moves
+# (world-1) x the output bytes over xGMI while the fold reads N x the input
+# bytes from HBM: at 8 GPUs, ~7 TB/s of fold and an assumed ~0.35 TB/s per
+# rank of all-gather, rho = gather/fold time ~0.14 for C3 (1024 clients,
+# fp32 out) and ~0.55 for C4 (256 clients, bf16 in and out).  fp32: a steep
+# tail (shares 1, 1, 0.35, 0.125); bf16: a gentle one (1, 0.7, 0.49, 0.34), so
+# every round still covers the previous round's gather.
+DEFAULT_TAIL = {"f32": (0.125, 2), "bf16": (0.343, 3)}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -95,10 +107,11 @@ def parse():
     ap.add_argument("--rounds", type=int, default=0,
                     help="exchange rounds per step (fold of round k+1 overlaps the all-gather of round k); "
                          "default 1 on one GPU, 4 on several")
-    ap.add_argument("--tail", type=float, default=1.0,
+    ap.add_argument("--tail", type=float, default=None,
                     help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
-                         "left exposed after the step's folds); 1 = equal rounds")
-    ap.add_argument("--tail-steps", type=int, default=1,
+                         "left exposed after the step's folds); 1 = equal rounds.  Default with several rounds: "
+                         "the layout for the dtype (DEFAULT_TAIL)")
+    ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
                          "rounds: shares 1, 1, 0.5, 0.25)")
     return ap.parse_args()
@@ -353,7 +366,8 @@ def main():
     if args.splitn:
         args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra,
-                  tail=args.tail if rounds > 1 else 1.0, tail_steps=args.tail_steps)
+                  tail=(args.tail if args.tail is not None else DEFAULT_TAIL[cfg[2]][0]) if rounds > 1 else 1.0,
+                  tail_steps=args.tail_steps if args.tail_steps is not None else DEFAULT_TAIL[cfg[2]][1])
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
@@ -367,6 +381,20 @@ def main():
         # the all-gather's copy, when both sat on one queue)
         stream = sharding_fold_stream(dev)
         stream.wait_stream(torch.cuda.current_stream(dev))
+
+    # the library's tuner times each candidate kernel form on the first calls of
+    # a new shape (fa_set_autotune): run the folds alone (no collectives, so the
+    # ranks need not agree on a count) until every slot shape has its form, as
+    # the first aggregation rounds of a deployment would
+    L = _lib.load()
+    tune_calls = 0
+    if args.variant == 0 and L.fa_set_autotune(-1) == 1:
+        for tune_calls in range(1, 201):
+            for k in range(rounds):
+                wl.launch(0, k)
+            torch.cuda.synchronize()
+            if L.fa_autotune_pending() == 0:
+                break
 
     if args.sweep and rank == 0:
         nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()
@@ -421,19 +449,6 @@ def main():
             ev[1].record(stream)
 
     torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
-    # the library's tuner times each candidate kernel form on the first calls of
-    # a new shape (fa_set_autotune): run the folds alone (no collectives, so the
-    # ranks need not agree on a count) until every slot shape has its form, as
-    # the first aggregation rounds of a deployment would
-    L = _lib.load()
-    tune_calls = 0
-    if args.variant == 0 and L.fa_set_autotune(-1) == 1:
-        for tune_calls in range(1, 201):
-            for k in range(rounds):
-                wl.launch(0, k)
-            torch.cuda.synchronize()
-            if L.fa_autotune_pending() == 0:
-                break
     for _ in range(args.warmup):
         step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -18,10 +18,11 @@ run() {  # name, args...
   echo "$name: $(python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('widths', d['config']['round_widths'], 'fold_ms', d['fold_ms'], 'exposed', d['gather_exposed_ms'], 'ms_per_step', d['ms_per_step'], 'gather_check', d['gather_check'])")"
 }
 for pass in 1 2; do
-  for t in 1 0.5 0.25 0.125; do
-    run "c4_t${t}_p$pass" --config c4 --params 12500000 --rounds 4 --tail $t --steps 30 --warmup 5
-  done
-  for t in 1 0.25 0.125; do
-    run "c3_t${t}_p$pass" --config c3 --rounds 4 --tail $t --steps 10 --warmup 3
-  done
+  # equal rounds against the bench's default layout for the dtype (DEFAULT_TAIL) and the single-cut tails
+  run "c4_equal_p$pass" --config c4 --params 12500000 --rounds 4 --tail 1 --steps 30 --warmup 5
+  run "c4_default_p$pass" --config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5
+  run "c4_t0.125_p$pass" --config c4 --params 12500000 --rounds 4 --tail 0.125 --tail-steps 1 --steps 30 --warmup 5
+  run "c3_equal_p$pass" --config c3 --rounds 4 --tail 1 --steps 10 --warmup 3
+  run "c3_default_p$pass" --config c3 --rounds 4 --steps 10 --warmup 3
+  run "c3_t0.125_p$pass" --config c3 --rounds 4 --tail 0.125 --tail-steps 1 --steps 10 --warmup 3
 done
