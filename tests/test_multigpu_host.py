@@ -126,3 +126,26 @@ def test_bench_launches_torch_distributed_run_as_child(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE")
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     assert bench.launch_ranks(bench.parse()) is None
+
+
+def test_bench_default_slot_layouts():
+    """bench.DEFAULT_TAIL: for every world size of the scaling run, the default
+    per-dtype slot layouts of C3 (weak: 10M params per rank) and C4 (strong:
+    100M in total) cover the model, stay 64-aligned, and shrink toward the
+    last round (whose all-gather is the one left exposed)."""
+    sys.path.insert(0, REPO)
+    import bench
+    from fedlesscan_amd.sharding import SlotLayout, tail_shares
+    for world in (1, 2, 4, 8):
+        for cfg in ("c3", "c4"):
+            N, P, dt = bench.CONFIGS[cfg][:3]
+            P_total = P * world if bench.CONFIGS[cfg][6] == "weak" else P
+            tail, steps = bench.DEFAULT_TAIL[dt]
+            lay = SlotLayout(P_total, world, 4, shares=tail_shares(4, tail, steps))
+            assert lay.padded_total >= P_total and lay.padded_total - P_total < 64 * world * 4 + 64 * world
+            assert all(w % 64 == 0 for w in lay.widths)
+            assert lay.widths == sorted(lay.widths, reverse=True) and lay.widths[-1] < lay.widths[0]
+            assert abs(lay.widths[-1] / lay.widths[0] - tail) < 0.01
+            covered = sorted(sl for r in range(world) for sl in lay.slots(r) if sl[1] > sl[0])
+            assert covered[0][0] == 0 and covered[-1][1] == P_total
+            assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
