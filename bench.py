@@ -44,7 +44,7 @@ sys.path.insert(0, REPO)
 
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import ALIGN, SlotLayout, gather_into, tail_shares  # noqa: E402
+from fedlesscan_amd.sharding import ALIGN, DEFAULT_TAIL, SlotLayout, gather_into, tail_shares  # noqa: E402
 from fedlesscan_amd.sharding import fold_stream as sharding_fold_stream  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -62,18 +62,6 @@ CONFIGS = {
     "c5": (512, 25_000_000, "f32", True, 5, 2000, "weak",
            "512 clients x 25M fp32 FedLesScan stall-aware, tolerance 2, R=10 (BASELINE config 5)"),
 }
-
-
-# Slot layout of the overlapped exchange at N > 1, per input dtype: (tail, steps)
-# for sharding.tail_shares.  Each round's all-gather must hide behind the next
-# round's fold, and the last one is exposed.  Per parameter, the gather moves
-# (world-1) x the output bytes over xGMI while the fold reads N x the input
-# bytes from HBM: at 8 GPUs, ~7 TB/s of fold and an assumed ~0.35 TB/s per
-# rank of all-gather, rho = gather/fold time ~0.14 for C3 (1024 clients,
-# fp32 out) and ~0.55 for C4 (256 clients, bf16 in and out).  fp32: a steep
-# tail (shares 1, 1, 0.35, 0.125); bf16: a gentle one (1, 0.7, 0.49, 0.34), so
-# every round still covers the previous round's gather.
-DEFAULT_TAIL = {"f32": (0.125, 2), "bf16": (0.343, 3)}
 
 
 def log(*a):

@@ -48,7 +48,7 @@ def tail_shares(rounds: int, tail: float, steps: int = 1) -> List[float]:
     exchange is left exposed after the step's folds: a short last round
     shortens it.  But each gather must also fit behind the NEXT fold, or it is
     exposed instead: with gather/fold time ratio rho per parameter (C4 bf16 on
-    8 GPUs ~0.6, C3 fp32 ~0.2), round k+1 should keep at least
+    8 GPUs ~0.55, C3 fp32 ~0.14, DEFAULT_TAIL), round k+1 should keep at least
     rho of round k's width, hence the geometric steps rather than one cut."""
     if not 0 < tail <= 1:
         raise ValueError("tail must be in (0, 1]")
@@ -57,6 +57,25 @@ def tail_shares(rounds: int, tail: float, steps: int = 1) -> List[float]:
         return [1.0] * rounds
     r = float(tail) ** (1.0 / steps)
     return [1.0] * (rounds - steps) + [r ** (j + 1) for j in range(steps)]
+
+
+# Default overlap layout per input dtype: (tail, steps) for tail_shares.  Each
+# round's all-gather must hide behind the next round's fold, and the last one is
+# exposed.  Per parameter, the gather moves (world-1) x the output bytes over
+# xGMI while the fold reads N x the input bytes from HBM: at 8 GPUs, ~7 TB/s of
+# fold and an assumed ~0.35 TB/s per rank of all-gather give a gather/fold
+# time ratio rho ~0.14 for C3 (1024 clients, fp32 out) and ~0.55 for C4 (256
+# clients, bf16 in and out).  fp32: a steep tail (shares 1, 1, 0.35, 0.125);
+# bf16: a gentle one (1, 0.7, 0.49, 0.34), so that every round still covers
+# the previous round's gather.
+DEFAULT_TAIL = {"f32": (0.125, 2), "bf16": (0.343, 3)}
+
+
+def overlap_layout(P: int, world: int, dtype: str = "f32", rounds: int = 4, align: int = ALIGN) -> "SlotLayout":
+    """The SlotLayout ShardedAggregator.aggregate_slots should get for a
+    `dtype` ("f32" / "bf16") model of P params over `world` ranks."""
+    tail, steps = DEFAULT_TAIL[dtype]
+    return SlotLayout(P, world, rounds, align=align, shares=tail_shares(rounds, tail, steps) if rounds > 1 else None)
 
 
 class SlotLayout:

@@ -12,7 +12,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from fedlesscan_amd import synth
-from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, bucket_bounds, chunk_size, tail_shares
+from fedlesscan_amd.sharding import (ShardedAggregator, SlotLayout, bucket_bounds, chunk_size, overlap_layout,
+                                     tail_shares)
 
 
 def test_bucket_bounds_cover_and_align():
@@ -77,6 +78,10 @@ def test_tail_shares():
     w = lay.widths
     assert w[0] == w[1] and abs(w[2] / w[0] - 0.5) < 1e-3 and abs(w[3] / w[0] - 0.25) < 1e-3
     assert lay.round_range(3)[1] == lay.padded_total >= 100_000_000
+    assert overlap_layout(100_000_000, 8, "bf16").widths == SlotLayout(100_000_000, 8, 4,
+                                                                       shares=tail_shares(4, 0.343, 3)).widths
+    assert overlap_layout(80_000_000, 8).widths == SlotLayout(80_000_000, 8, 4, shares=tail_shares(4, 0.125, 2)).widths
+    assert overlap_layout(1000, 2, rounds=1).widths == SlotLayout(1000, 2, 1).widths
 
 
 def _free_port():
