@@ -65,10 +65,12 @@ def tail_shares(rounds: int, tail: float, steps: int = 1) -> List[float]:
 # xGMI while the fold reads N x the input bytes from HBM: at 8 GPUs, ~7 TB/s of
 # fold and an assumed ~0.35 TB/s per rank of all-gather give a gather/fold
 # time ratio rho ~0.14 for C3 (1024 clients, fp32 out) and ~0.55 for C4 (256
-# clients, bf16 in and out).  fp32: a steep tail (shares 1, 1, 0.35, 0.125);
-# bf16: a gentle one (1, 0.7, 0.49, 0.34), so that every round still covers
-# the previous round's gather.
-DEFAULT_TAIL = {"f32": (0.125, 2), "bf16": (0.343, 3)}
+# clients, bf16 in and out).  fp32: one cut, shares 1, 1, 1, 0.125 (round 3's
+# gather still hides behind round 4's fold at rho 0.14; the steeper 1, 1,
+# 0.35, 0.125 measured 0.11 ms more fold per C3 rank step on one GPU);
+# bf16: a gentle geometric tail, 1, 0.7, 0.49, 0.34, so that every round
+# still covers the previous round's gather.
+DEFAULT_TAIL = {"f32": (0.125, 1), "bf16": (0.343, 3)}
 
 
 def overlap_layout(P: int, world: int, dtype: str = "f32", rounds: int = 4, align: int = ALIGN) -> "SlotLayout":

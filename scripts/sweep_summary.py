@@ -22,7 +22,8 @@ def load(d):
         for line in open(f):
             mm = re.match(r"variant (\d+) (\S+)\s+median ([\d.]+) ms", line)
             if mm:
-                row[mm.group(2)] = float(mm.group(3))
+                # the product's auto fold is "auto" (fp32) or "bf16auto" (bf16)
+                row["auto" if mm.group(2) == "bf16auto" else mm.group(2)] = float(mm.group(3))
         if row:
             T[(int(m.group(1)), int(m.group(2)))] = row
     return T

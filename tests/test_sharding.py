@@ -80,7 +80,7 @@ def test_tail_shares():
     assert lay.round_range(3)[1] == lay.padded_total >= 100_000_000
     assert overlap_layout(100_000_000, 8, "bf16").widths == SlotLayout(100_000_000, 8, 4,
                                                                        shares=tail_shares(4, 0.343, 3)).widths
-    assert overlap_layout(80_000_000, 8).widths == SlotLayout(80_000_000, 8, 4, shares=tail_shares(4, 0.125, 2)).widths
+    assert overlap_layout(80_000_000, 8).widths == SlotLayout(80_000_000, 8, 4, shares=tail_shares(4, 0.125)).widths
     assert overlap_layout(1000, 2, rounds=1).widths == SlotLayout(1000, 2, 1).widths
 
 
