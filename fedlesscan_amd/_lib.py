@@ -86,6 +86,12 @@ _BENCH_PROTOS = {
     "fa_num_variants": (_int, []),
     "fa_variant_name": (ctypes.c_char_p, [_int]),
     "fa_f32_pick_name": (ctypes.c_char_p, [_i64, _i64, _i64]),
+    "fa_num_f32_forms": (_int, []),
+    "fa_f32_form_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_f32_form": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
+    "fa_num_bf16_forms": (_int, []),
+    "fa_bf16_form_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_bf16_form": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
     "fa_fedavg_bf16_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),
     "fa_num_bf16_variants": (_int, []),
     "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),

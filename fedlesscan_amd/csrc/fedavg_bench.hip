@@ -442,6 +442,37 @@ const char* fa_f32_pick_name(int64_t N, int64_t P, int64_t cus) {
     if (N < 1 || P < 1) return "";
     return f32_pick_name(pick_f32(N, P, cus));
 }
+int fa_num_f32_forms(void) { return kNumF32Picks; }
+const char* fa_f32_form_name(int form) { return (form >= 0 && form < kNumF32Picks) ? f32_pick_name((F32Pick)form) : ""; }
+int fa_fedavg_f32_form(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                       float divisor, float* out, void* stream, int form) {
+    if (form < 0 || form >= kNumF32Picks) return fail(FA_ERR_ARG, "unknown fp32 form %d", form);
+    int rc = check_common(N, P, ldx, X, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(X) || (ldx % 4) || !aligned16(out)) return fail(FA_ERR_ARG, "the vector forms need 16-B rows");
+    StreamDevice on_stream_device(stream);
+    rc = launch_f32_pick((F32Pick)form, (hipStream_t)stream, s != nullptr, false, true, X, N, P, ldx, a, s, nullptr,
+                         divisor, out);
+    if (rc) return rc;
+    return check_launch("fa_fedavg_f32_form");
+}
+int fa_num_bf16_forms(void) { return kNumBf16Forms; }
+const char* fa_bf16_form_name(int form) {
+    return (form >= 0 && form < kNumBf16Forms) ? bf16_form_name((Bf16Form)form) : "";
+}
+int fa_fedavg_bf16_form(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                        float divisor, float* out_f32, uint16_t* out_bf16, void* stream, int form) {
+    if (form < 0 || form >= kNumBf16Forms) return fail(FA_ERR_ARG, "unknown bf16 form %d", form);
+    int rc = check_common(N, P, ldx, X, a, out_f32);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(X) || (ldx % 8) || !aligned16(out_f32) || (out_bf16 && !aligned16(out_bf16)))
+        return fail(FA_ERR_ARG, "the vector forms need 16-B rows");
+    StreamDevice on_stream_device(stream);
+    launch_bf16_form((Bf16Form)form, (hipStream_t)stream, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+    return check_launch("fa_fedavg_bf16_form");
+}
 const char* fa_variant_name(int variant) {
     return (variant >= 0 && variant < kNumVariants) ? kVariants[variant] : "";
 }

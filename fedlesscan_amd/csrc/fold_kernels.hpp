@@ -1442,6 +1442,27 @@ inline const char* f32_pick_name(F32Pick p) {
     }
     return "";
 }
+// bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
+enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
+inline const char* bf16_form_name(Bf16Form f) {
+    switch (f) {
+        case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
+        case Bf16Form::kV8U4C4: return "bf16_tile_u4c4";
+        case Bf16Form::kV8U8C2: return "bf16_tile_u8c2";
+        case Bf16Form::kV8U8C1: return "bf16_tile_u8c1";
+        case Bf16Form::kBandsU8C4: return "bf16_bands4_u8c4";
+        case Bf16Form::kBandsU8C2: return "bf16_bands4_u8c2";
+        case Bf16Form::kBandsU2C8: return "bf16_bands2_u2c8";
+        case Bf16Form::kBandsU4C4: return "bf16_bands4_u4c4";
+        case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
+        case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
+        case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
+    }
+    return "";
+}
+
 // Column tile of the LDS fold for 32K-256K params: the launch is ~2-8 blocks
 // per CU, so how evenly the blocks fill the CUs decides the time (a scan over
 // P at 1024 clients: 768 blocks of 32 quads ran at 7.17 TB/s, 526 blocks at
@@ -1721,24 +1742,25 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
 // sweeps over measured shapes; between those shapes every form swings with
 // how the tiles fall on the CUs (1024 x 909K params: the policy's form 0.70 ms,
 // the even split 0.53 ms; 256 x 3.57M bf16: 0.337 against 0.295 ms;
-// profiles/r03_slot_sweep/).  Every form computes the same bits, so for a plain
-// one-shot fold the tuner times the shape's candidate forms on the caller's
-// own calls: the first calls of a new (device, dtype, N, P, pitch, scored)
-// shape each run one candidate between two events on the caller's stream (no
-// synchronisation: the events are read with hipEventQuery on later calls),
-// kTuneSamples per candidate, and once all are in, every later call of that
-// shape runs the fastest -- the policy's own pick unless another form beats
-// it by more than 3 % (box-to-box spread is ~2-5 %).
-// FEDAVG_AUTOTUNE=0 (or fa_set_autotune(0)) keeps the policy pick.
+// profiles/r03_slot_sweep/).  Every form computes the same bits, and a plain
+// one-shot fold overwrites its whole output, so the FIRST call of a new
+// (device, dtype, N, P, pitch, scored) shape runs every candidate form on the
+// caller's own data, on the caller's stream: one untimed launch (code-object
+// load, cold TLBs), then `batch` back-to-back launches between two events
+// (batch sized to ~0.3 ms, so launch gaps do not decide between forms of a
+// 20 us kernel: timing single launches between events misranked them,
+// profiles/r03_tuner/probe.log).  Whichever form ran last, the output is the
+// fold.  Nothing synchronises: later calls read the events with
+// hipEventQuery and run the policy's pick until they are complete; from then
+// on the shape runs the fastest form -- the policy's own pick unless another
+// beats it by more than 3 % (box-to-box spread is ~2-5 %).
+// FEDAVG_AUTOTUNE=0 (or fa_set_autotune(0)) keeps the policy pick;
+// FEDAVG_AUTOTUNE_LOG=1 prints every decision with each candidate's time.
 // ---------------------------------------------------------------------------
 constexpr int kTuneF32 = 1, kTuneBf16 = 2;
-constexpr int kTuneSamples = 2;
 constexpr float kTuneMargin = 0.97f;
-
-struct TuneChoice {
-    int form;
-    int64_t ticket = -1;  // >= 0: a timed sample; end() records its closing event
-};
+constexpr double kTuneBatchMs = 0.3;  // timed span per candidate
+constexpr int kTuneMaxBatch = 16;
 
 class Tuner {
   public:
@@ -1751,82 +1773,78 @@ class Tuner {
         if (m >= 0) mode_.store(m ? 1 : 0);
         return prev;
     }
-    // The form for this call; `cands(v)` fills the candidate forms (v[0] = the
-    // policy pick) the first time the shape is seen.  Runs on the stream's
-    // device (the callers hold a StreamDevice).
-    template <class Cands>
-    TuneChoice begin(int kind, int64_t N, int64_t P, int64_t ldx, bool scored, int policy, hipStream_t st,
-                     Cands cands) {
-        if (!mode_.load()) return {policy};
+    // Run this call's fold: launch(form) enqueues one fold of that form and
+    // returns an FA status.  `cands(v)` fills the candidate forms (v[0] = the
+    // policy pick) the first time the shape is seen; `bytes` sizes the batch.
+    // Runs on the stream's device (the callers hold a StreamDevice).
+    template <class Cands, class Launch>
+    int run(int kind, int64_t N, int64_t P, int64_t ldx, bool scored, int policy, double bytes, hipStream_t st,
+            Cands cands, Launch launch) {
+        if (!mode_.load()) return launch(policy);
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) {
             (void)hipGetLastError();
-            return {policy};
+            return launch(policy);
         }
-        std::lock_guard<std::mutex> lk(mu_);
-        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
-        if (it == map_.end()) {
-            Entry e;
-            cands(e.cand);
-            if (e.cand.size() <= 1) e.chosen = policy;
-            e.best.assign(e.cand.size(), 3.4e38f);
-            e.got.assign(e.cand.size(), 0);
-            e.inflight.assign(e.cand.size(), 0);
-            it = map_.emplace(Key{dev, kind, N, P, ldx, scored ? 1 : 0}, std::move(e)).first;
-        }
-        Entry& e = it->second;
-        if (e.chosen >= 0) return {e.chosen};
-        harvest(e);
-        if (decide(e)) return {e.chosen};
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
-            (void)hipGetLastError();
-            return {e.cand[0]};
-        }
-        if (cs != hipStreamCaptureStatusNone) return {e.cand[0]};  // no events inside a graph capture
-        // the next candidate still short of samples (in flight ones count)
-        const int n = (int)e.cand.size();
-        int ci = -1;
-        for (int j = 0; j < n; ++j) {
-            const int c = (e.rr + j) % n;
-            if (e.got[c] + e.inflight[c] < kTuneSamples) {
-                ci = c;
-                break;
+        const Key key{dev, kind, N, P, ldx, scored ? 1 : 0};
+        Entry* e = nullptr;
+        bool explore = false;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = map_.find(key);
+            if (it == map_.end()) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(st, &cs) != hipSuccess) (void)hipGetLastError();
+                if (cs != hipStreamCaptureStatusNone) return launch(policy);  // no events inside a graph capture
+                Entry fresh;
+                cands(fresh.cand);
+                fresh.kind = kind;
+                fresh.N = N;
+                fresh.P = P;
+                fresh.ldx = ldx;
+                fresh.scored = scored;
+                if (fresh.cand.size() <= 1) fresh.chosen = policy;
+                it = map_.emplace(key, std::move(fresh)).first;
+                explore = it->second.chosen < 0;
+            }
+            e = &it->second;  // std::map nodes are stable
+            if (!explore) {
+                if (e->chosen < 0) {
+                    harvest(*e);
+                    if (e->chosen < 0) return launch(e->cand[0]);  // measurement still in flight
+                }
+                return launch(e->chosen);
             }
         }
-        if (ci < 0) return {e.cand[0]};  // every sample is in flight: untimed policy launch
-        e.rr = (ci + 1) % n;
-        Sample smp;
-        if (!take_event(e, &smp.e0) || !take_event(e, &smp.e1)) return {e.cand[0]};
-        if (hipEventRecord(smp.e0, st) != hipSuccess) {
-            (void)hipGetLastError();
-            e.free.push_back(smp.e0);
-            e.free.push_back(smp.e1);
-            return {e.cand[0]};
-        }
-        smp.c = ci;
-        smp.ticket = next_ticket_++;
-        e.inflight[ci]++;
-        e.samples.push_back(smp);
-        return {e.cand[ci], smp.ticket};
-    }
-    // Close a timed sample: its second event goes on the stream after the launch.
-    void end(const TuneChoice& tc, int kind, int64_t N, int64_t P, int64_t ldx, bool scored, hipStream_t st) {
-        if (tc.ticket < 0) return;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        std::lock_guard<std::mutex> lk(mu_);
-        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
-        if (it == map_.end()) return;
-        for (Sample& smp : it->second.samples)
-            if (smp.ticket == tc.ticket) {
-                if (hipEventRecord(smp.e1, st) == hipSuccess) smp.armed = true;
-                else (void)hipGetLastError();  // never armed: dropped when the shape decides
-                break;
+        // First call of the shape: time every candidate (this thread owns the
+        // entry's events until `armed` is set; other threads run the policy).
+        const double est_ms = bytes / 5.0e9;  // ~5 TB/s
+        int batch = (int)(kTuneBatchMs / (est_ms > 1e-6 ? est_ms : 1e-6)) + 1;
+        if (batch > kTuneMaxBatch) batch = kTuneMaxBatch;
+        const int n = (int)e->cand.size();
+        std::vector<hipEvent_t> ev(2 * (size_t)n, nullptr);
+        bool timed = true;
+        for (auto& x : ev)
+            if (hipEventCreate(&x) != hipSuccess) {
+                (void)hipGetLastError();
+                x = nullptr;
+                timed = false;
             }
+        int rc = FA_OK;
+        for (int c = 0; c < n && rc == FA_OK; ++c) {
+            rc = launch(e->cand[c]);  // untimed: code-object load, cold TLBs
+            if (timed && hipEventRecord(ev[2 * c], st) != hipSuccess) timed = false;
+            for (int b = 0; b < batch && rc == FA_OK; ++b) rc = launch(e->cand[c]);
+            if (timed && hipEventRecord(ev[2 * c + 1], st) != hipSuccess) timed = false;
+        }
+        if (!timed) (void)hipGetLastError();
+        std::lock_guard<std::mutex> lk(mu_);
+        e->batch = batch;
+        e->events = ev;
+        if (rc != FA_OK || !timed) e->chosen = e->cand[0];  // a failed or untimed measurement keeps the policy
+        e->armed = true;
+        if (e->chosen >= 0) release(*e);
+        return rc;
     }
     int pending() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -1834,7 +1852,7 @@ class Tuner {
         for (auto& kv : map_) {
             if (kv.second.chosen >= 0) continue;
             harvest(kv.second);  // the shape may have all it needs without a further call
-            if (!decide(kv.second)) ++n;
+            if (kv.second.chosen < 0) ++n;
         }
         return n;
     }
@@ -1843,86 +1861,68 @@ class Tuner {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
         if (it == map_.end()) return -2;
-        if (it->second.chosen < 0) {
-            harvest(it->second);
-            decide(it->second);
-        }
+        if (it->second.chosen < 0) harvest(it->second);
         return it->second.chosen;
     }
 
   private:
     typedef std::tuple<int, int, int64_t, int64_t, int64_t, int> Key;
-    struct Sample {
-        int c = 0;
-        int64_t ticket = 0;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        bool armed = false;
-    };
     struct Entry {
         std::vector<int> cand;
-        std::vector<float> best;
-        std::vector<int> got, inflight;
-        std::vector<Sample> samples;
-        std::vector<hipEvent_t> free;
-        int rr = 0, chosen = -1;
+        std::vector<hipEvent_t> events;  // [2c] start, [2c+1] end of candidate c's batch
+        int batch = 1, chosen = -1;
+        bool armed = false;  // the exploring call has recorded every event
+        int kind = 0;
+        int64_t N = 0, P = 0, ldx = 0;
+        bool scored = false;
     };
-    bool take_event(Entry& e, hipEvent_t* ev) {
-        if (!e.free.empty()) {
-            *ev = e.free.back();
-            e.free.pop_back();
-            return true;
-        }
-        if (hipEventCreate(ev) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        return true;
+    static const char* form_name(int kind, int form) {
+        return kind == kTuneF32 ? f32_pick_name((F32Pick)form) : bf16_form_name((Bf16Form)form);
     }
+    void release(Entry& e) {
+        for (hipEvent_t x : e.events)
+            if (x) (void)hipEventDestroy(x);
+        e.events.clear();
+    }
+    // Decide once the last candidate's end event has completed (the events
+    // complete in stream order).  Under mu_.
     void harvest(Entry& e) {
-        for (size_t i = 0; i < e.samples.size();) {
-            Sample& smp = e.samples[i];
-            if (!smp.armed) {
-                ++i;
-                continue;
-            }
-            const hipError_t q = hipEventQuery(smp.e1);
-            if (q == hipErrorNotReady) {
-                ++i;
-                continue;
-            }
-            float ms = 0.f;
-            if (q == hipSuccess && hipEventElapsedTime(&ms, smp.e0, smp.e1) == hipSuccess && ms > 0.f) {
-                if (ms < e.best[smp.c]) e.best[smp.c] = ms;
-                e.got[smp.c]++;
-            } else {
-                (void)hipGetLastError();
-            }
-            e.inflight[smp.c]--;
-            e.free.push_back(smp.e0);
-            e.free.push_back(smp.e1);
-            e.samples.erase(e.samples.begin() + (long)i);
+        if (e.chosen >= 0 || !e.armed) return;
+        const int n = (int)e.cand.size();
+        const hipError_t q = hipEventQuery(e.events[2 * n - 1]);
+        if (q == hipErrorNotReady) return;
+        std::vector<float> ms(n, 3.4e38f);
+        bool ok = q == hipSuccess;
+        for (int c = 0; ok && c < n; ++c) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, e.events[2 * c], e.events[2 * c + 1]) != hipSuccess || !(t > 0.f)) ok = false;
+            else ms[c] = t / (float)e.batch;
         }
-    }
-    bool decide(Entry& e) {
-        if (e.chosen >= 0) return true;
-        for (size_t c = 0; c < e.cand.size(); ++c)
-            if (e.got[c] < kTuneSamples) return false;
-        size_t b = 0;
-        for (size_t c = 1; c < e.cand.size(); ++c)
-            if (e.best[c] < e.best[b]) b = c;
-        e.chosen = (e.best[b] < kTuneMargin * e.best[0]) ? e.cand[b] : e.cand[0];
-        bool busy = false;  // samples never armed (a failed record) keep their events
-        for (const Sample& smp : e.samples) busy |= smp.armed;
-        if (!busy) {
-            for (hipEvent_t ev : e.free) (void)hipEventDestroy(ev);
-            e.free.clear();
+        if (!ok) {
+            (void)hipGetLastError();
+            e.chosen = e.cand[0];
+            release(e);
+            return;
         }
-        return true;
+        int b = 0;
+        for (int c = 1; c < n; ++c)
+            if (ms[c] < ms[b]) b = c;
+        e.chosen = (ms[b] < kTuneMargin * ms[0]) ? e.cand[b] : e.cand[0];
+        if (log_) {
+            char line[1024];
+            int k = snprintf(line, sizeof(line), "fedavg tuner: %s N=%lld P=%lld ldx=%lld%s batch=%d -> %s |",
+                             e.kind == kTuneF32 ? "f32" : "bf16", (long long)e.N, (long long)e.P, (long long)e.ldx,
+                             e.scored ? " scored" : "", e.batch, form_name(e.kind, e.chosen));
+            for (int c = 0; c < n && k > 0 && k < (int)sizeof(line); ++c)
+                k += snprintf(line + k, sizeof(line) - k, " %s %.4f", form_name(e.kind, e.cand[c]), ms[c]);
+            fprintf(stderr, "%s ms\n", line);
+        }
+        release(e);
     }
     std::mutex mu_;
     std::map<Key, Entry> map_;
     std::atomic<int> mode_{env_mode()};
-    int64_t next_ticket_ = 0;
+    const bool log_ = getenv("FEDAVG_AUTOTUNE_LOG") && getenv("FEDAVG_AUTOTUNE_LOG")[0] == '1';
 };
 Tuner g_tuner;
 
@@ -2082,37 +2082,18 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
     // a plain one-shot fold (no accumulator in, with the divide) of a shape
     // seen before takes the form the tuner measured fastest on this device
     if (!acc && fin && N > 0) {
-        const TuneChoice tc = g_tuner.begin(kTuneF32, N, P, ldx, sc, (int)policy, st,
-                                            [&](std::vector<int>& c) { f32_candidates(N, P, (int)policy, c); });
-        int rc = launch_f32_pick((F32Pick)tc.form, st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-        g_tuner.end(tc, kTuneF32, N, P, ldx, sc, st);
+        const int rc = g_tuner.run(kTuneF32, N, P, ldx, sc, (int)policy, (double)N * (double)P * 4.0, st,
+                                   [&](std::vector<int>& c) { f32_candidates(N, P, (int)policy, c); },
+                                   [&](int form) {
+                                       return launch_f32_pick((F32Pick)form, st, sc, acc, fin, X, N, P, ldx, a, s,
+                                                              acc_in, divisor, out);
+                                   });
         if (rc) return rc;
         return check_launch("fold_f32");
     }
     int rc = launch_f32_pick(policy, st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
     if (rc) return rc;
     return check_launch("fold_f32");
-}
-
-// bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
-enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
-                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
-constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
-inline const char* bf16_form_name(Bf16Form f) {
-    switch (f) {
-        case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
-        case Bf16Form::kV8U4C4: return "bf16_tile_u4c4";
-        case Bf16Form::kV8U8C2: return "bf16_tile_u8c2";
-        case Bf16Form::kV8U8C1: return "bf16_tile_u8c1";
-        case Bf16Form::kBandsU8C4: return "bf16_bands4_u8c4";
-        case Bf16Form::kBandsU8C2: return "bf16_bands4_u8c2";
-        case Bf16Form::kBandsU2C8: return "bf16_bands2_u2c8";
-        case Bf16Form::kBandsU4C4: return "bf16_bands4_u4c4";
-        case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
-        case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
-        case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
-    }
-    return "";
 }
 
 // The policy's bf16 form by shape.
@@ -2208,10 +2189,12 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
         return check_launch("k_fedavg_bf16_scalar");
     }
     const Bf16Form policy = pick_bf16(N, P);
-    const TuneChoice tc = g_tuner.begin(kTuneBf16, N, P, ldx, s != nullptr, (int)policy, st,
-                                        [&](std::vector<int>& c) { bf16_candidates(N, P, (int)policy, c); });
-    launch_bf16_form((Bf16Form)tc.form, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-    g_tuner.end(tc, kTuneBf16, N, P, ldx, s != nullptr, st);
+    g_tuner.run(kTuneBf16, N, P, ldx, s != nullptr, (int)policy, (double)N * (double)P * 2.0, st,
+                [&](std::vector<int>& c) { bf16_candidates(N, P, (int)policy, c); },
+                [&](int form) {
+                    launch_bf16_form((Bf16Form)form, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+                    return FA_OK;
+                });
     return check_launch("fedavg_bf16");
 }
 

@@ -44,6 +44,17 @@ const char* fa_variant_name(int variant);
  * N clients x P params (16-B aligned rows) on a GPU with `cus` compute units
  * (<= 0: the current device's), e.g. "tile_4k", "gs_bands_16k"; "" if N or P < 1. */
 const char* fa_f32_pick_name(int64_t N, int64_t P, int64_t cus);
+/* One kernel form of the product's fp32 / bf16 fold, by index (the forms the
+ * shape policy and the tuner choose between: fa_num_*_forms, fa_*_form_name);
+ * a plain one-shot fold.  Lets the tests check every form the tuner may pick. */
+int fa_num_f32_forms(void);
+const char* fa_f32_form_name(int form);
+int fa_fedavg_f32_form(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                       float divisor, float* out, void* stream, int form);
+int fa_num_bf16_forms(void);
+const char* fa_bf16_form_name(int form);
+int fa_fedavg_bf16_form(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                        float divisor, float* out_f32, uint16_t* out_bf16, void* stream, int form);
 /* Same for the bf16 fold (variant 0 = fa_fedavg_bf16). */
 int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                            const float* a, const float* s, float divisor,

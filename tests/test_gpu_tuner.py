@@ -1,13 +1,15 @@
 """The measured form choice (fa_set_autotune, csrc/fold_kernels.hpp Tuner).
 
-The first calls of a new shape each run one candidate kernel form between two
-events; once every candidate has its samples the shape runs the fastest.  All
-forms compute the same bits, so every call of a shape -- whichever candidate
-it ran -- must be bit-identical to the oracle (the fold of
-fed_avg_aggregator.py:24-42 / stall_aware_aggregation.py:42-67).  The shapes
-below are called until their measurement is complete, so every candidate form
-runs on each of them: narrow (LDS forms), a few tiles per CU (every form),
-large (grid-stride forms), P % 4 / P % 8 tails, a padded row pitch, one client.
+The first call of a new shape runs every candidate kernel form on the
+caller's data (an untimed launch, then a timed batch each); later calls run
+the fastest once the events are in.  All forms compute the same bits, so:
+every form the tuner can choose is checked bit for bit against the oracle
+(the fold of fed_avg_aggregator.py:24-42 / stall_aware_aggregation.py:42-67)
+through the bench library's per-form entry, on shapes covering narrow (LDS
+forms), a few tiles per CU (every form), large (grid-stride forms), P % 4 /
+P % 8 tails, a padded row pitch and one client; and the tuned product calls
+themselves -- the exploring call and the calls after the decision -- are
+bit-exact too.
 """
 import numpy as np
 import pytest
@@ -19,7 +21,7 @@ from oracle import oracle_lib as OL  # checker
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-F32_SHAPES = [  # (N, P, ldx pad, scored)
+F32_SHAPES = [  # (N, P, extra row pitch, scored)
     (1, 1003, 0, False),
     (3, 4099, 0, True),
     (17, 70001, 0, False),
@@ -27,7 +29,7 @@ F32_SHAPES = [  # (N, P, ldx pad, scored)
     (64, 909123, 0, False),
     (300, 1048579, 0, True),
     (1024, 65536, 0, False),
-    (10, 5000, 120, False),
+    (10, 5000, 128, False),
     (7, 2_000_001, 0, False),
 ]
 BF16_SHAPES = [(5, 3001, False), (129, 1_048_583, True), (200, 1_100_003, False)]
@@ -48,7 +50,7 @@ def L():
     lib.fa_set_autotune(prev)
 
 
-def _run_until_tuned(L, fold, form, max_calls=80):
+def _run_until_tuned(L, fold, form, max_calls=8):
     """Call fold() until fa_fold_form names a form; returns the outputs of every call."""
     outs = []
     for _ in range(max_calls):
@@ -60,39 +62,47 @@ def _run_until_tuned(L, fold, form, max_calls=80):
 
 
 @pytest.mark.parametrize("N,P,pad,scored", F32_SHAPES)
-def test_f32_every_candidate_bit_exact(dev, L, N, P, pad, scored):
+def test_f32_every_form_and_the_tuned_calls_bit_exact(dev, L, N, P, pad, scored):
+    from fedlesscan_amd import _lib
+    B = _lib.load_bench()
     seed = 71 + N
     X = synth.clients_f32(seed, N, 0, P)
     w = synth.cardinalities(seed, N)
     sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
-    ldx = P + pad
+    ldx = (P + 63) // 64 * 64 + pad  # 16-B rows (the vector path, the one the tuner measures); P % 4 tails stay
     Xd = torch.zeros((N, ldx), dtype=torch.float32, device=dev)
     Xd[:, :P] = torch.from_numpy(X).to(dev)
     a = torch.tensor(np.array(w, np.float32), device=dev)
     s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
+    sp = None if s is None else s.data_ptr()
     div = float(np.float32(sum(w)))
     st = torch.cuda.current_stream(dev).cuda_stream
-    from fedlesscan_amd import _lib
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    for f in range(B.fa_num_f32_forms()):  # every form the policy or the tuner can run
+        o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
+        _lib.check(B.fa_fedavg_f32_form(Xd.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(), st, f),
+                   "form", bench=True)
+        assert G.same_bits(o.cpu().numpy(), exp), (B.fa_f32_form_name(f), N, P)
 
     def fold():
         o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-        _lib.check(L.fa_fedavg_f32(Xd.data_ptr(), N, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(),
-                                   div, o.data_ptr(), st), "fa_fedavg_f32")
+        _lib.check(L.fa_fedavg_f32(Xd.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(), st), "fold")
         return o
 
     form = lambda: L.fa_fold_form(1, N, P, ldx, 1 if scored else 0, st).decode()  # noqa: E731
+    assert form() == B.fa_f32_pick_name(N, P, 0).decode()  # unseen: the policy's form
     outs = _run_until_tuned(L, fold, form)
-    assert form(), f"{N} x {P}: measurement did not complete in {len(outs)} calls"
-    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
-                        s=None if sc is None else np.array(sc, np.float32))
+    assert form(), f"{N} x {P}: no decision after {len(outs)} calls"
+    outs.append(fold())  # the decided form
     for k, o in enumerate(outs):
         assert G.same_bits(o.cpu().numpy(), exp), (N, P, k)
-    # the measured shape keeps its form: a later call is bit-exact too
-    assert G.same_bits(fold().cpu().numpy(), exp)
 
 
 @pytest.mark.parametrize("N,P,scored", BF16_SHAPES)
-def test_bf16_every_candidate_bit_exact(dev, L, N, P, scored):
+def test_bf16_every_form_and_the_tuned_calls_bit_exact(dev, L, N, P, scored):
+    from fedlesscan_amd import _lib
+    B = _lib.load_bench()
     seed = 91 + N
     Xb = synth.clients_bf16(seed, N, 0, P)
     w = synth.cardinalities(seed, N)
@@ -102,22 +112,33 @@ def test_bf16_every_candidate_bit_exact(dev, L, N, P, scored):
     Xd[:, :P] = torch.from_numpy(Xb.view(np.int16)).to(dev)
     a = torch.tensor(np.array(w, np.float32), device=dev)
     s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
+    sp = None if s is None else s.data_ptr()
     div = float(np.float32(sum(w)))
     st = torch.cuda.current_stream(dev).cuda_stream
-    from fedlesscan_amd import _lib
+    ef, eb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)),
+                            s=None if sc is None else np.array(sc, np.float32))
+
+    def fresh():
+        return (torch.full((P,), float("nan"), dtype=torch.float32, device=dev),
+                torch.zeros((P,), dtype=torch.int16, device=dev))
+
+    for f in range(B.fa_num_bf16_forms()):
+        o, ob = fresh()
+        _lib.check(B.fa_fedavg_bf16_form(Xd.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(),
+                                         ob.data_ptr(), st, f), "bf16 form", bench=True)
+        assert G.same_bits(o.cpu().numpy(), ef), (B.fa_bf16_form_name(f), N, P)
+        assert np.array_equal(ob.cpu().numpy().view(np.uint16), eb), (B.fa_bf16_form_name(f), N, P)
 
     def fold():
-        o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-        ob = torch.zeros((P,), dtype=torch.int16, device=dev)
-        _lib.check(L.fa_fedavg_bf16(Xd.data_ptr(), N, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(),
-                                    div, o.data_ptr(), ob.data_ptr(), st), "fa_fedavg_bf16")
+        o, ob = fresh()
+        _lib.check(L.fa_fedavg_bf16(Xd.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(), ob.data_ptr(),
+                                    st), "fa_fedavg_bf16")
         return o, ob
 
     form = lambda: L.fa_fold_form(2, N, P, ldx, 1 if scored else 0, st).decode()  # noqa: E731
     outs = _run_until_tuned(L, fold, form)
-    assert form(), f"bf16 {N} x {P}: measurement did not complete in {len(outs)} calls"
-    ef, eb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)),
-                            s=None if sc is None else np.array(sc, np.float32))
+    assert form(), f"bf16 {N} x {P}: no decision after {len(outs)} calls"
+    outs.append(fold())
     for k, (o, ob) in enumerate(outs):
         assert G.same_bits(o.cpu().numpy(), ef), (N, P, k)
         assert np.array_equal(ob.cpu().numpy().view(np.uint16), eb), (N, P, k)
@@ -127,13 +148,13 @@ def test_hostf_and_engine_path_tuned(dev, L):
     """engine.fold_stacked (the drop-in's path, *_hostf entries) goes through the
     tuner too: repeated calls of one shape stay bit-exact while it measures."""
     from fedlesscan_amd import engine
-    N, P = 48, 600_007
+    N, P = 48, 600_004  # rows 16-B aligned: the vector path the tuner measures
     X = synth.clients_f32(5, N, 0, P)
     w = synth.cardinalities(5, N)
     Xd = torch.from_numpy(X).to(dev)
     exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
     st = torch.cuda.current_stream(dev).cuda_stream
-    for _ in range(60):
+    for _ in range(8):
         got = engine.fold_stacked(Xd, w).cpu().numpy()
         assert G.same_bits(got, exp)
         if L.fa_fold_form(1, N, P, P, 0, st):
