@@ -1745,12 +1745,13 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
 // profiles/r03_slot_sweep/).  Every form computes the same bits, and a plain
 // one-shot fold overwrites its whole output, so the FIRST call of a new
 // (device, dtype, N, P, pitch, scored) shape runs every candidate form on the
-// caller's own data, on the caller's stream: one untimed launch (code-object
-// load, cold TLBs), then `batch` back-to-back launches between two events
-// (batch sized to ~0.3 ms, so launch gaps do not decide between forms of a
-// 20 us kernel: timing single launches between events misranked them,
-// profiles/r03_tuner/probe.log).  Whichever form ran last, the output is the
-// fold.  Nothing synchronises: later calls read the events with
+// caller's own data, on the caller's stream: one untimed launch of each
+// (code-object load, cold TLBs, clocks up from idle), then two timed passes
+// in opposite orders, `batch` back-to-back launches of a form between two
+// events (batch sized to ~0.3 ms, so launch gaps do not decide between forms
+// of a 20 us kernel: timing single launches between events misranked them,
+// profiles/r03_tuner/probe_single_launch.log); a form's time is the faster
+// pass.  Whichever form ran last, the output is the fold.  Nothing synchronises: later calls read the events with
 // hipEventQuery and run the policy's pick until they are complete; from then
 // on the shape runs the fastest form -- the policy's own pick unless another
 // beats it by more than 3 % (box-to-box spread is ~2-5 %).
@@ -1760,7 +1761,7 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
 constexpr int kTuneF32 = 1, kTuneBf16 = 2;
 constexpr float kTuneMargin = 0.97f;
 constexpr double kTuneBatchMs = 0.3;  // timed span per candidate
-constexpr int kTuneMaxBatch = 16;
+constexpr int kTuneMaxBatch = 32;
 
 class Tuner {
   public:
@@ -1822,7 +1823,7 @@ class Tuner {
         int batch = (int)(kTuneBatchMs / (est_ms > 1e-6 ? est_ms : 1e-6)) + 1;
         if (batch > kTuneMaxBatch) batch = kTuneMaxBatch;
         const int n = (int)e->cand.size();
-        std::vector<hipEvent_t> ev(2 * (size_t)n, nullptr);
+        std::vector<hipEvent_t> ev(4 * (size_t)n, nullptr);  // [pass][candidate][start, end]
         bool timed = true;
         for (auto& x : ev)
             if (hipEventCreate(&x) != hipSuccess) {
@@ -1831,12 +1832,18 @@ class Tuner {
                 timed = false;
             }
         int rc = FA_OK;
-        for (int c = 0; c < n && rc == FA_OK; ++c) {
-            rc = launch(e->cand[c]);  // untimed: code-object load, cold TLBs
-            if (timed && hipEventRecord(ev[2 * c], st) != hipSuccess) timed = false;
-            for (int b = 0; b < batch && rc == FA_OK; ++b) rc = launch(e->cand[c]);
-            if (timed && hipEventRecord(ev[2 * c + 1], st) != hipSuccess) timed = false;
-        }
+        // untimed: one launch of every form (code-object loads, cold TLBs; the
+        // clocks come up from idle), then two timed passes in opposite orders,
+        // so a drift over the measurement favours no candidate
+        for (int c = 0; c < n && rc == FA_OK; ++c) rc = launch(e->cand[c]);
+        for (int pass = 0; pass < 2; ++pass)
+            for (int j = 0; j < n && rc == FA_OK; ++j) {
+                const int c = pass == 0 ? j : n - 1 - j;
+                hipEvent_t* pe = &ev[2 * ((size_t)pass * n + c)];
+                if (timed && hipEventRecord(pe[0], st) != hipSuccess) timed = false;
+                for (int b = 0; b < batch && rc == FA_OK; ++b) rc = launch(e->cand[c]);
+                if (timed && hipEventRecord(pe[1], st) != hipSuccess) timed = false;
+            }
         if (!timed) (void)hipGetLastError();
         std::lock_guard<std::mutex> lk(mu_);
         e->batch = batch;
@@ -1869,7 +1876,7 @@ class Tuner {
     typedef std::tuple<int, int, int64_t, int64_t, int64_t, int> Key;
     struct Entry {
         std::vector<int> cand;
-        std::vector<hipEvent_t> events;  // [2c] start, [2c+1] end of candidate c's batch
+        std::vector<hipEvent_t> events;  // [2(pass*n + c)] start, [... + 1] end of candidate c's batch
         int batch = 1, chosen = -1;
         bool armed = false;  // the exploring call has recorded every event
         int kind = 0;
@@ -1889,15 +1896,18 @@ class Tuner {
     void harvest(Entry& e) {
         if (e.chosen >= 0 || !e.armed) return;
         const int n = (int)e.cand.size();
-        const hipError_t q = hipEventQuery(e.events[2 * n - 1]);
+        // the second pass runs backwards: candidate 0's end event is the last one recorded
+        const hipError_t q = hipEventQuery(e.events[2 * (size_t)n + 1]);
         if (q == hipErrorNotReady) return;
-        std::vector<float> ms(n, 3.4e38f);
+        std::vector<float> ms(n, 3.4e38f);  // per launch, the faster of the two passes
         bool ok = q == hipSuccess;
-        for (int c = 0; ok && c < n; ++c) {
-            float t = 0.f;
-            if (hipEventElapsedTime(&t, e.events[2 * c], e.events[2 * c + 1]) != hipSuccess || !(t > 0.f)) ok = false;
-            else ms[c] = t / (float)e.batch;
-        }
+        for (int pass = 0; ok && pass < 2; ++pass)
+            for (int c = 0; ok && c < n; ++c) {
+                const size_t i = 2 * ((size_t)pass * n + c);
+                float t = 0.f;
+                if (hipEventElapsedTime(&t, e.events[i], e.events[i + 1]) != hipSuccess || !(t > 0.f)) ok = false;
+                else if (t / (float)e.batch < ms[c]) ms[c] = t / (float)e.batch;
+            }
         if (!ok) {
             (void)hipGetLastError();
             e.chosen = e.cand[0];
@@ -1946,7 +1956,7 @@ inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v
                           F32Pick::kTileU8C2, F32Pick::kTileC1, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32,
                           F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6})
             add(p);
-        if (N < 128) add(F32Pick::kColumn);
+        add(F32Pick::kColumn);
     } else {  // large models: the grid-stride forms, the 16 KiB tile, the even split
         for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBands6, F32Pick::kGsBalC2, F32Pick::kGs1C4,
                           F32Pick::kTileC4Plain, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32})

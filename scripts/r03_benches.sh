@@ -4,6 +4,7 @@
 # default slot layouts.  Outputs: gpurun_out/benches/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export FEDAVG_AUTOTUNE_LOG=1  # the tuner's decisions (every candidate's time) go to the stderr logs
 OUT=${OUT:-gpurun_out/benches}
 mkdir -p "$OUT"
 run() {  # name, seconds, args...

@@ -5,6 +5,7 @@
 # SHAPES_BF16 / SHAPES_F32 override.  Outputs: gpurun_out/bf16_slots/, gpurun_out/f32_slots/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export FEDAVG_AUTOTUNE_LOG=1  # the tuner's decisions (every candidate's time) go to the stderr logs
 B=${B:-gpurun_out/bf16_slots}; F=${F:-gpurun_out/f32_slots}
 mkdir -p "$B" "$F"
 SHAPES_BF16=${SHAPES_BF16:-"256:961600 256:1136384 256:1250000 256:1500000 256:1785728 256:2000000 256:2272768 256:2500000 256:2750000 256:3125056 256:3571456 256:3846208 256:4545472"}

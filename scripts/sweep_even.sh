@@ -6,6 +6,7 @@
 # per round, medians.  Outputs: gpurun_out/even/<N>x<P>.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export FEDAVG_AUTOTUNE_LOG=1  # the tuner's decisions (every candidate's time) go to the stderr logs
 OUT=${OUT:-gpurun_out/even}
 mkdir -p "$OUT"
 NS=${NS:-"10 32 64 80 100 200 1024"}
