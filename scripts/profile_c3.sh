@@ -14,12 +14,14 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
+# the trace and counter passes with the tuner off: its first call runs every
+# candidate form once (C3: the gs kernel over other band and grid sizes among
+# them), which would mix into the per-kernel averages and the per-dispatch
+# counter medians; C3's measured form is the policy's gs_bands_16k anyway
+# (bench.json config.fold_form), so the profiled kernel is the one the line times
+export FEDAVG_AUTOTUNE=0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o c3 --output-format csv -- \
     python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
-# the counter passes with the tuner off: its first call runs every candidate form, some of
-# them the same kernel template over other band sizes, which would mix into the per-dispatch
-# medians; C3's measured form is the policy's gs_bands_16k anyway (bench.json fold_form)
-export FEDAVG_AUTOTUNE=0
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c3 -- \
     python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/fetch.err"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c3 -- \
