@@ -89,6 +89,9 @@ _BENCH_PROTOS = {
     "fa_num_f32_forms": (_int, []),
     "fa_f32_form_name": (ctypes.c_char_p, [_int]),
     "fa_fedavg_f32_form": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
+    "fa_num_ptrs_forms": (_int, []),
+    "fa_ptrs_form_name": (ctypes.c_char_p, [_int]),
+    "fa_fedavg_f32_ptrs_form": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
     "fa_num_bf16_forms": (_int, []),
     "fa_bf16_form_name": (ctypes.c_char_p, [_int]),
     "fa_fedavg_bf16_form": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _int]),

@@ -168,53 +168,11 @@ int fa_fedavg_f32_ptrs_aligned(const float* const* xi, int64_t N, int64_t P, con
     if (!aligned16(out)) return fail(FA_ERR_ARG, "fa_fedavg_f32_ptrs_aligned needs a 16-B aligned out");
     hipStream_t st = (hipStream_t)stream;
     StreamDevice on_stream_device(stream);
-    const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
-#define FA_R(U, C, GRIDCAP)                                                                                    \
-    {                                                                                                          \
-        const int64_t tiles = (units + (int64_t)kBlock * (C) - 1) / ((int64_t)kBlock * (C));                   \
-        const int64_t g = (GRIDCAP) > 0 && tiles > (GRIDCAP) ? (GRIDCAP) : tiles;                              \
-        if (s)                                                                                                 \
-            hipLaunchKernelGGL((k_fold_f32_rows_gs<U, C, true>), dim3((unsigned)g), dim3(kBlock), 0, st, xi, N, \
-                               P, a, s, divisor, out, tiles);                                                  \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_fold_f32_rows_gs<U, C, false>), dim3((unsigned)g), dim3(kBlock), 0, st, xi,  \
-                               N, P, a, s, divisor, out, tiles);                                               \
-    }
-    // narrow models (the stacked fold's LDS-staged picks) and everything up
-    // to ~3M params: the LDS-staged fold reading row bases from the table;
-    // large models: ~one block per CU walking 16 KiB tiles (as the stacked
-    // default)
-    const F32Pick pk = pick_f32(N, P);
-    rc = FA_OK;
-    if (pk == F32Pick::kLdsW2T16)  // as the stacked pick, with the pointer ring (LOPT 4)
-        rc = launch_lds_flags<2, 32, 16, 4, false, true, true, 4>(st, s != nullptr, false, true, (const float*)xi, N,
-                                                                  P, P, a, s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW2T16D2)  // two-wave 16-quad tiles, as the stacked pick (1.2-1.6x over the
-                                          // 4-wave 32-quad table fold at 32K-65K, profiles/r02_lds/ptrs_two_wave/)
-        rc = launch_lds_flags<2, 32, 16, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW2T32)  // two-wave 32-quad tiles, as the stacked pick
-        rc = launch_lds_flags<2, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW4T24)
-        rc = launch_lds_flags<4, 32, 24, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW4T40)
-        rc = launch_lds_flags<4, 32, 40, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else if (pk == F32Pick::kLdsW8)
-        rc = launch_lds_flags<8, 64, 32, 1, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else if ((P >> 2) < ((int64_t)3 << 18))
-        // up to ~3M params, past the stacked fold's LDS range: the 32-quad LDS
-        // fold beat the tile kernel below on table rows (100 x 582K: 42.3
-        // against 76.6 us; 1024 x 2.5M: 1.62 against 1.70 ms), but not at 4M
-        // with 1024 clients (2.60 against 2.49 ms) (profiles/r02_lds/dw_ptrs.log,
-        // ptrs_large.log, ptrs_mid.log)
-        rc = launch_lds_flags<4, 16, 32, 2, false, true>(st, s != nullptr, false, true, (const float*)xi, N, P, P, a,
-                                                         s, nullptr, divisor, out);
-    else FA_R(8, 4, (int64_t)cu_count())
-#undef FA_R
+    const PtrsForm policy = pick_ptrs(N, P);
+    const bool sc = s != nullptr;
+    rc = g_tuner.run(kTunePtrs, N, P, P, sc, (int)policy, (double)N * (double)P * 4.0, st,
+                     [&](std::vector<int>& c) { ptrs_candidates(N, P, (int)policy, c); },
+                     [&](int form) { return launch_ptrs_form((PtrsForm)form, st, xi, N, P, a, s, divisor, out); });
     if (rc) return rc;
     return check_launch("fa_fedavg_f32_ptrs_aligned");
 }
@@ -259,7 +217,7 @@ int fa_set_autotune(int mode) { return g_tuner.set_mode(mode); }
 int fa_autotune_pending(void) { return g_tuner.pending(); }
 
 const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored, void* stream) {
-    if ((kind != FA_FOLD_F32 && kind != FA_FOLD_BF16) || N < 1 || P < 1) return "";
+    if ((kind != FA_FOLD_F32 && kind != FA_FOLD_BF16 && kind != FA_FOLD_F32_ROWS) || N < 1 || P < 1) return "";
     StreamDevice on_stream_device(stream);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) {
@@ -269,6 +227,7 @@ const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored
     const int tuned = g_tuner.set_mode(-1) ? g_tuner.chosen(dev, kind, N, P, ldx, scored != 0) : -2;
     if (tuned == -1) return "";
     if (kind == FA_FOLD_F32) return f32_pick_name(tuned >= 0 ? (F32Pick)tuned : pick_f32(N, P));
+    if (kind == FA_FOLD_F32_ROWS) return ptrs_form_name(tuned >= 0 ? (PtrsForm)tuned : pick_ptrs(N, P));
     return bf16_form_name(tuned >= 0 ? (Bf16Form)tuned : pick_bf16(N, P));
 }
 

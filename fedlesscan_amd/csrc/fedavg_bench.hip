@@ -457,6 +457,22 @@ int fa_fedavg_f32_form(const float* X, int64_t N, int64_t P, int64_t ldx, const 
     if (rc) return rc;
     return check_launch("fa_fedavg_f32_form");
 }
+int fa_num_ptrs_forms(void) { return kNumPtrsForms; }
+const char* fa_ptrs_form_name(int form) {
+    return (form >= 0 && form < kNumPtrsForms) ? ptrs_form_name((PtrsForm)form) : "";
+}
+int fa_fedavg_f32_ptrs_form(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                            float divisor, float* out, void* stream, int form) {
+    if (form < 0 || form >= kNumPtrsForms) return fail(FA_ERR_ARG, "unknown pointer-table form %d", form);
+    int rc = check_common(N, P, P, xi, a, out);
+    if (rc) return rc;
+    if (P == 0) { g_err[0] = 0; return FA_OK; }
+    if (!aligned16(out)) return fail(FA_ERR_ARG, "needs a 16-B aligned out");
+    StreamDevice on_stream_device(stream);
+    rc = launch_ptrs_form((PtrsForm)form, (hipStream_t)stream, xi, N, P, a, s, divisor, out);
+    if (rc) return rc;
+    return check_launch("fa_fedavg_f32_ptrs_form");
+}
 int fa_num_bf16_forms(void) { return kNumBf16Forms; }
 const char* fa_bf16_form_name(int form) {
     return (form >= 0 && form < kNumBf16Forms) ? bf16_form_name((Bf16Form)form) : "";

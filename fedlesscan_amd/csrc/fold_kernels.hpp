@@ -1738,9 +1738,108 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
 }
 
 
+// ---- the pointer-table fold's forms (fa_fedavg_f32_ptrs_aligned) ----------
+// Row bases come from a device table; the LDS-staged forms mirror the stacked
+// fold's narrow picks, the grid-stride form its large-model default.
+enum class PtrsForm { kLdsW2T16Ring, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kLdsW4T32, kRowsGs };
+constexpr int kNumPtrsForms = (int)PtrsForm::kRowsGs + 1;
+inline const char* ptrs_form_name(PtrsForm f) {
+    switch (f) {
+        case PtrsForm::kLdsW2T16Ring: return "ptrs_lds_w2_t16_ring";
+        case PtrsForm::kLdsW2T16D2: return "ptrs_lds_w2_t16_d2";
+        case PtrsForm::kLdsW2T32: return "ptrs_lds_w2_t32";
+        case PtrsForm::kLdsW4T24: return "ptrs_lds_w4_t24";
+        case PtrsForm::kLdsW4T40: return "ptrs_lds_w4_t40";
+        case PtrsForm::kLdsW8: return "ptrs_lds_w8_t32";
+        case PtrsForm::kLdsW4T32: return "ptrs_lds_w4_t32";
+        case PtrsForm::kRowsGs: return "ptrs_rows_gs_16k";
+    }
+    return "";
+}
+
+// The policy: the stacked fold's LDS picks for narrow models, the 32-quad
+// LDS fold up to ~3M params (it beat the tile kernel on table rows: 100 x
+// 582K 42.3 against 76.6 us, 1024 x 2.5M 1.62 against 1.70 ms, but not at 4M
+// with 1024 clients, 2.60 against 2.49 ms; profiles/r02_lds/dw_ptrs.log,
+// ptrs_large.log, ptrs_mid.log), then ~one block per CU over 16 KiB tiles.
+inline PtrsForm pick_ptrs(int64_t N, int64_t P) {
+    switch (pick_f32(N, P)) {
+        case F32Pick::kLdsW2T16: return PtrsForm::kLdsW2T16Ring;  // with the pointer ring (LOPT 4)
+        case F32Pick::kLdsW2T16D2: return PtrsForm::kLdsW2T16D2;  // 1.2-1.6x over the 4-wave 32-quad table fold
+                                                                  // at 32K-65K (profiles/r02_lds/ptrs_two_wave/)
+        case F32Pick::kLdsW2T32: return PtrsForm::kLdsW2T32;
+        case F32Pick::kLdsW4T24: return PtrsForm::kLdsW4T24;
+        case F32Pick::kLdsW4T40: return PtrsForm::kLdsW4T40;
+        case F32Pick::kLdsW8: return PtrsForm::kLdsW8;
+        default: break;
+    }
+    return (P >> 2) < ((int64_t)3 << 18) ? PtrsForm::kLdsW4T32 : PtrsForm::kRowsGs;
+}
+
+inline void ptrs_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v) {
+    (void)N;
+    v.push_back(policy);
+    auto add = [&](PtrsForm f) {
+        for (int x : v)
+            if (x == (int)f) return;
+        v.push_back((int)f);
+    };
+    if ((P >> 2) < (1 << 16))
+        for (PtrsForm f : {PtrsForm::kLdsW2T16Ring, PtrsForm::kLdsW2T16D2, PtrsForm::kLdsW2T32, PtrsForm::kLdsW4T24,
+                           PtrsForm::kLdsW4T40, PtrsForm::kLdsW8, PtrsForm::kLdsW4T32})
+            add(f);
+    else
+        for (PtrsForm f : {PtrsForm::kLdsW4T32, PtrsForm::kLdsW8, PtrsForm::kLdsW4T40, PtrsForm::kRowsGs})
+            add(f);
+}
+
+inline int launch_ptrs_form(PtrsForm f, hipStream_t st, const float* const* xi, int64_t N, int64_t P, const float* a,
+                            const float* s, float divisor, float* out) {
+    const bool sc = s != nullptr;
+    const float* X = (const float*)xi;
+    switch (f) {
+        case PtrsForm::kLdsW2T16Ring:
+            return launch_lds_flags<2, 32, 16, 4, false, true, true, 4>(st, sc, false, true, X, N, P, P, a, s, nullptr,
+                                                                        divisor, out);
+        case PtrsForm::kLdsW2T16D2:
+            return launch_lds_flags<2, 32, 16, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kLdsW2T32:
+            return launch_lds_flags<2, 16, 32, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kLdsW4T24:
+            return launch_lds_flags<4, 32, 24, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kLdsW4T40:
+            return launch_lds_flags<4, 32, 40, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kLdsW8:
+            return launch_lds_flags<8, 64, 32, 1, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kLdsW4T32:
+            return launch_lds_flags<4, 16, 32, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
+                                                               out);
+        case PtrsForm::kRowsGs: {
+            const int64_t units = (P >> 2) + ((P & 3) ? 1 : 0);
+            const int64_t tiles = (units + (int64_t)kBlock * 4 - 1) / ((int64_t)kBlock * 4);
+            const int64_t cap = cu_count();
+            const int64_t g = tiles > cap ? cap : tiles;
+            if (sc)
+                hipLaunchKernelGGL((k_fold_f32_rows_gs<8, 4, true>), dim3((unsigned)g), dim3(kBlock), 0, st, xi, N,
+                                   P, a, s, divisor, out, tiles);
+            else
+                hipLaunchKernelGGL((k_fold_f32_rows_gs<8, 4, false>), dim3((unsigned)g), dim3(kBlock), 0, st, xi, N,
+                                   P, a, s, divisor, out, tiles);
+            return FA_OK;
+        }
+    }
+    return fail(FA_ERR_ARG, "unknown pointer-table form");
+}
+
 // The tuner (tuner.hpp): a measured form per shape.
-constexpr int kTuneF32 = 1, kTuneBf16 = 2;
+constexpr int kTuneF32 = 1, kTuneBf16 = 2, kTunePtrs = 3;
 inline const char* tune_form_name(int kind, int form) {
+    if (kind == kTunePtrs) return ptrs_form_name((PtrsForm)form);
     return kind == kTuneF32 ? f32_pick_name((F32Pick)form) : bf16_form_name((Bf16Form)form);
 }
 fa_tune::Tuner g_tuner(tune_form_name);

@@ -206,7 +206,7 @@ class Tuner {
         if (log_) {
             char line[1024];
             int k = snprintf(line, sizeof(line), "fedavg tuner: %s N=%lld P=%lld ldx=%lld%s batch=%d -> %s |",
-                             e.kind == 1 ? "f32" : "bf16", (long long)e.N, (long long)e.P, (long long)e.ldx,
+                             e.kind == 1 ? "f32" : e.kind == 2 ? "bf16" : "f32 rows", (long long)e.N, (long long)e.P, (long long)e.ldx,
                              e.scored ? " scored" : "", e.batch, form_name(e.kind, e.chosen));
             for (int c = 0; c < n && k > 0 && k < (int)sizeof(line); ++c)
                 k += snprintf(line + k, sizeof(line) - k, " %s %.4f", form_name(e.kind, e.cand[c]), ms[c]);

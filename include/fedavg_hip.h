@@ -129,23 +129,29 @@ int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                          const float* a, const float* s, float divisor,
                          float* out_f32, uint16_t* out_bf16, void* stream);
 
-/* Measured form choice.  Every kernel form of the fp32 and bf16 folds
- * computes the same bits; which is fastest depends on how a shape's tiles fall
- * on the CUs.  For plain one-shot folds (fa_fedavg_f32 / _bf16 and their
- * _hostf forms) the library times each candidate form on the first calls of a
- * new (device, dtype, N, P, ldx, scored) shape -- one candidate per call,
- * between two events on the caller's stream, read back without synchronising
- * on later calls -- and from then on runs the fastest (the shape policy's own
- * form unless another is > 3 % faster).  Outputs are bit-identical whatever
- * form runs.  Library-wide switch, on unless FEDAVG_AUTOTUNE=0 at load.
+/* Measured form choice.  Every kernel form of the fp32, bf16 and row-table
+ * folds computes the same bits; which is fastest depends on how a shape's
+ * tiles fall on the CUs.  For plain one-shot folds (fa_fedavg_f32, _bf16,
+ * _f32_ptrs_aligned and their _hostf forms) the FIRST call of a new (device,
+ * kind, N, P, ldx, scored) shape runs every candidate form on the caller's
+ * data and stream (an untimed launch each, then two timed passes of batched
+ * launches between events), and once those events have completed -- read
+ * back without synchronising on later calls -- the shape runs the fastest
+ * (the shape policy's own form unless another is > 3 % faster).  Outputs are
+ * bit-identical whatever form runs.  Library-wide switch, on unless
+ * FEDAVG_AUTOTUNE=0 at load; FEDAVG_AUTOTUNE_LOG=1 prints each decision.
  *   fa_set_autotune:     1 on, 0 off (the policy form only), -1 query;
  *                        returns the previous setting
  *   fa_autotune_pending: shapes seen whose measurement is not complete
  *   fa_fold_form:        the form a shape runs on the stream's device:
  *                        the measured choice, "" while it is being measured,
  *                        the policy's form for an unseen shape or with the
- *                        tuner off.  kind: FA_FOLD_F32 or FA_FOLD_BF16. */
-enum fa_fold_kind { FA_FOLD_F32 = 1, FA_FOLD_BF16 = 2 };
+ *                        tuner off. */
+enum fa_fold_kind {
+    FA_FOLD_F32 = 1,      /* fa_fedavg_f32 (_hostf)                     */
+    FA_FOLD_BF16 = 2,     /* fa_fedavg_bf16 (_hostf)                    */
+    FA_FOLD_F32_ROWS = 3, /* fa_fedavg_f32_ptrs_aligned (_hostf), ldx = P */
+};
 int fa_set_autotune(int mode);
 int fa_autotune_pending(void);
 const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored, void* stream);

@@ -51,6 +51,10 @@ int fa_num_f32_forms(void);
 const char* fa_f32_form_name(int form);
 int fa_fedavg_f32_form(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
                        float divisor, float* out, void* stream, int form);
+int fa_num_ptrs_forms(void);
+const char* fa_ptrs_form_name(int form);
+int fa_fedavg_f32_ptrs_form(const float* const* xi, int64_t N, int64_t P, const float* a, const float* s,
+                            float divisor, float* out, void* stream, int form);
 int fa_num_bf16_forms(void);
 const char* fa_bf16_form_name(int form);
 int fa_fedavg_bf16_form(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,

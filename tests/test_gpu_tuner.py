@@ -180,3 +180,42 @@ def test_tuner_off_runs_the_policy_form(dev, L):
     finally:
         L.fa_set_autotune(prev)
     assert L.fa_fold_form(9, N, P, P, 0, st) == b""  # unknown kind
+
+
+@pytest.mark.parametrize("N,P,scored", [(1, 5, False), (33, 4099, True), (100, 67267, False), (257, 20011, True),
+                                        (64, 300_001, False), (40, 1_200_003, True)])
+def test_row_table_every_form_and_the_tuned_calls_bit_exact(dev, L, N, P, scored):
+    """fa_fedavg_f32_ptrs_aligned (separately allocated 16-B aligned rows, the
+    engine's fold_rows path): every form it can choose, and its tuned calls."""
+    from fedlesscan_amd import _lib
+    B = _lib.load_bench()
+    X = synth.clients_f32(211 + N, N, 0, P)
+    w = synth.cardinalities(211 + N, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(211, N, 10, 2)] if scored else None
+    rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]  # caching allocator: 256-B aligned rows
+    tab = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
+    sp = None if s is None else s.data_ptr()
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)),
+                        s=None if sc is None else np.array(sc, np.float32))
+    for f in range(B.fa_num_ptrs_forms()):
+        o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
+        _lib.check(B.fa_fedavg_f32_ptrs_form(tab.data_ptr(), N, P, a.data_ptr(), sp, div, o.data_ptr(), st, f),
+                   "ptrs form", bench=True)
+        assert G.same_bits(o.cpu().numpy(), exp), (B.fa_ptrs_form_name(f), N, P)
+
+    def fold():
+        o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
+        _lib.check(L.fa_fedavg_f32_ptrs_aligned(tab.data_ptr(), N, P, a.data_ptr(), sp, div, o.data_ptr(), st),
+                   "fa_fedavg_f32_ptrs_aligned")
+        return o
+
+    form = lambda: L.fa_fold_form(3, N, P, P, 1 if scored else 0, st).decode()  # noqa: E731
+    outs = _run_until_tuned(L, fold, form)
+    assert form(), f"rows {N} x {P}: no decision after {len(outs)} calls"
+    outs.append(fold())
+    for k, o in enumerate(outs):
+        assert G.same_bits(o.cpu().numpy(), exp), (N, P, k)
