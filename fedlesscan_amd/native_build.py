@@ -26,6 +26,7 @@ CSRC = os.path.join(PKG, "csrc")
 SRC = os.path.join(CSRC, "fedavg.hip")
 BENCH_SRC = os.path.join(CSRC, "fedavg_bench.hip")
 KERNELS = os.path.join(CSRC, "fold_kernels.hpp")
+TUNER = os.path.join(CSRC, "tuner.hpp")
 HOST_SRCS = [os.path.join(CSRC, f) for f in ("ingest_host.cpp", "bson_host.cpp", "ingest_pipe.cpp")]
 HDR = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HDR = os.path.join(REPO, "include", "fedavg_hip_bench.h")
@@ -36,8 +37,8 @@ HOSTFAST_SRC = os.path.join(CSRC, "hostfast.c")
 HOSTFAST = os.path.join(OUT_DIR, "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))  # = _lib.HOSTFAST_PATH
 # library -> (sources compiled into it, files it depends on)
 TARGETS = {
-    LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, HDR, *HOST_SRCS, os.path.join(CSRC, "host_copy.hpp")]),
-    BENCH_LIB: ([BENCH_SRC], [BENCH_SRC, KERNELS, HDR, BENCH_HDR]),
+    LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, TUNER, HDR, *HOST_SRCS, os.path.join(CSRC, "host_copy.hpp")]),
+    BENCH_LIB: ([BENCH_SRC], [BENCH_SRC, KERNELS, TUNER, HDR, BENCH_HDR]),
     HOSTFAST: ([HOSTFAST_SRC], [HOSTFAST_SRC]),
 }
 ARCH = os.environ.get("FEDAVG_OFFLOAD_ARCH", "gfx950")
