@@ -51,10 +51,25 @@ class CopyPool {
     void submit(std::function<void()> f) {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            if (workers_.empty()) start();
+            if (workers_.empty()) start(per_device());
             q_.push_back(std::move(f));
         }
         cv_.notify_one();
+    }
+    // A pipe on a new device: the pool grows by one device's share of workers
+    // (each GPU of a node comes with its own share of host cores, and each
+    // GPU's pipe packs its own column bucket: multigpu.py), up to the host's
+    // hardware threads.  FEDAVG_COPY_THREADS fixes the size instead.
+    void add_device(int device) {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (int d : devices_)
+            if (d == device) return;
+        devices_.push_back(device);
+        if (!workers_.empty() && !getenv("FEDAVG_COPY_THREADS")) start(per_device());
+    }
+    int threads() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return (int)workers_.size();
     }
     ~CopyPool() {
         {
@@ -66,11 +81,16 @@ class CopyPool {
     }
 
   private:
-    void start() {  // under mu_
-        int n = 16;  // the GPU box's CPU share of one GPU; FEDAVG_COPY_THREADS overrides
-        if (const char* e = getenv("FEDAVG_COPY_THREADS")) n = std::max(1, atoi(e));
-        n = std::min<int>(n, std::max(1u, std::thread::hardware_concurrency()));
-        for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    static int per_device() { return 16; }  // the GPU box's CPU share of one GPU
+    // Grow the pool by `add` workers (under mu_); the total follows the
+    // devices with pipes, FEDAVG_COPY_THREADS overrides it, the host's
+    // hardware threads cap it.
+    void start(int add) {
+        int target = (int)workers_.size() + add;
+        if (workers_.empty()) target = per_device() * std::max<int>(1, (int)devices_.size());
+        if (const char* e = getenv("FEDAVG_COPY_THREADS")) target = std::max(1, atoi(e));
+        target = std::min<int>(target, std::max(1u, std::thread::hardware_concurrency()));
+        while ((int)workers_.size() < target) workers_.emplace_back([this] { loop(); });
     }
     void loop() {
         std::unique_lock<std::mutex> lk(mu_);
@@ -88,6 +108,7 @@ class CopyPool {
     std::condition_variable cv_;
     std::deque<std::function<void()>> q_;
     std::vector<std::thread> workers_;
+    std::vector<int> devices_;  // devices that have had a pipe
     bool stop_ = false;
 };
 
@@ -313,6 +334,7 @@ int fa_ingest_create(fa_ingest** out, int64_t P, int64_t chunk_bytes, int slots,
     }
     p->issuer = std::thread(issuer_loop, p);
     (void)hipSetDevice(prev);
+    CopyPool::get().add_device(device);
     *out = p;
     return FA_OK;
 }

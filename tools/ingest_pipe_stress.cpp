@@ -78,7 +78,7 @@ static void worker(int tid, int rounds) {
             s[i] = (float)(1 + rng() % 11) / 11.f;
         }
         fa_ingest* pipe = nullptr;
-        check(fa_ingest_create(&pipe, P, chunk, slots, 0) == FA_OK, "create");
+        check(fa_ingest_create(&pipe, P, chunk, slots, tid % 2) == FA_OK, "create");  // two devices: the pool grows
         std::vector<float> acc(P, -1.f);
         for (int rep = 0; rep < 2; ++rep) {  // the pipe is reused
             // the announced row count: unknown, exact, too high, too low (only the chunk sizes change)
