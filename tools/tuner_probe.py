@@ -45,6 +45,12 @@ def main():
         else:
             _lib.check(L.fa_fedavg_f32(X.data_ptr(), N, P, ldx, a.data_ptr(), None, div, out.data_ptr(), st), "f32")
 
+    # the first call of the shape (it runs every candidate form), wall time to completion
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    call()
+    torch.cuda.synchronize()
+    first_ms = (time.perf_counter() - t0) * 1e3
     n = 0
     for n in range(1, 400):
         call()
@@ -64,8 +70,14 @@ def main():
         call()
     e1.record()
     e1.synchronize()
-    print(f"{'b2b' if args.b2b else 'isolated'} {N}x{P}: {n} tuning calls -> {form}, "
-          f"back-to-back {e0.elapsed_time(e1) / 50:.4f} ms", flush=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    call()
+    torch.cuda.synchronize()
+    later_ms = (time.perf_counter() - t0) * 1e3
+    print(f"{'b2b' if args.b2b else 'isolated'} {N}x{P}: first call {first_ms:.2f} ms (measures every form), "
+          f"a later call {later_ms:.3f} ms, then {n} calls -> {form}, back-to-back {e0.elapsed_time(e1) / 50:.4f} ms",
+          flush=True)
 
 
 if __name__ == "__main__":
