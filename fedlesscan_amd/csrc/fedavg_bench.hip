@@ -170,6 +170,8 @@ constexpr const char* kVariants[] = {
     // auto = quads per lane from the range (k_fold_f32_even, round 3)
     "even_auto", "even_g2_auto", "even_u16c2", "even_u32c1", "even_u8c4", "even_u4c4", "even_g2_u8c2",
     "even_g4_auto",
+    // one wave per 64 columns, LDS-DMA chunks, no barriers (k_fold_f32_w1, round 3): w1_r<rows>s<slots>
+    "w1_r32s6", "w1_r64s4", "w1_r16s12", "w1_r32s8",
 };
 constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
 constexpr int kEndAnyAlign = 92;
@@ -417,6 +419,10 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 103: FA_VE(cu_count(), 4, 4); break;
         case 104: FA_VE(2 * cu_count(), 8, 2); break;
         case 105: launch_even_auto(st, 4 * cu_count(), sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out); break;
+        case 106: rc = launch_w1<32, 6>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
+        case 107: rc = launch_w1<64, 4>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
+        case 108: rc = launch_w1<16, 12>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
+        case 109: rc = launch_w1<32, 8>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
 #undef FA_VE
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }

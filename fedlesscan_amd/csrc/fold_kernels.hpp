@@ -794,6 +794,157 @@ int launch_ring_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* 
     return FA_OK;
 }
 
+// ---------------------------------------------------------------------------
+// One-wave LDS-DMA fold for narrow models (k_fold_f32_w1, round 3; a tuner
+// candidate, never the policy's pick).  A block is ONE wave owning 64 columns
+// (16 quads): every chunk of R client rows is copied HBM -> LDS with
+// global_load_lds_dwordx4 (a wave-instruction moves 4 rows x 256 B), S-1
+// chunks in flight, and the same wave folds each landed chunk with one column
+// per lane (all 64 lanes, a 4-byte LDS read, a multiply and an add per row),
+// strictly in row order.  One wave needs no s_barrier: the chunk's vmcnt
+// retires its copies, and a slot is refilled only after the wave has folded
+// it (its reads were consumed by the adds).  The multi-wave LDS forms pay two
+// barriers per chunk and fold with half the lanes idle at 16K params (two
+// waves over 64 columns, CPW = 32).  The last partial chunk (N % R rows) and
+// the P%4 tail columns take register paths, as k_fold_f32_ring.
+// ---------------------------------------------------------------------------
+template <int R, int S, bool SCORED>
+__global__ __launch_bounds__(64) void k_fold_f32_w1(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor, float* out) {
+    constexpr int TQ = 16;                                   // quads per block: 64 columns
+    constexpr int LQ = R * TQ / 64;                          // 16-B copies per lane per chunk
+    constexpr int F = SCORED ? 2 : 1;                        // factor copies per chunk
+    constexpr int TILE_B = R * TQ * 16;                      // R rows x 256 B
+    constexpr int SLOT_B = TILE_B + ((F * R * 4 + 15) / 16) * 16;
+    static_assert(R % 4 == 0 && R <= 64 && S >= 3, "w1 shape");
+    static_assert((S - 2) * (LQ + F) < 64, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) char smem[S * SLOT_B];
+    const int t = threadIdx.x;
+    const int64_t nq = P >> 2;
+    const int64_t nbq = (nq + TQ - 1) / TQ;
+    const int64_t ldq = ldx >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(X);
+
+    if ((int64_t)blockIdx.x >= nbq) {
+        // ---- the P%4 tail columns: row-parallel terms, lane 0 adds in order ----
+        f32x4* tile0 = reinterpret_cast<f32x4*>(smem);
+        const int w4 = (int)(P & 3);
+        const int64_t col0 = nq * 4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int64_t r0 = 0; r0 < N; r0 += 64) {
+            const int64_t row = r0 + t;
+            if (row < N) {
+                f32x4 x = {0.f, 0.f, 0.f, 0.f};
+                for (int k = 0; k < w4; ++k) x[k] = X[row * ldx + col0 + k];
+                tile0[t] = term4<SCORED>(x, a[row], SCORED ? s[row] : 1.0f);
+            }
+            __syncthreads();
+            if (t == 0) {
+                const int rows = (N - r0) < 64 ? (int)(N - r0) : 64;
+                int i = 0;
+                if (r0 == 0) {
+                    acc = tile0[0];
+                    i = 1;
+                }
+                for (; i < rows; ++i) acc = add4(acc, tile0[i]);
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            const f32x4 res = div4(acc, divisor);
+            for (int k = 0; k < w4; ++k) out[col0 + k] = res[k];
+        }
+        return;
+    }
+
+    const int64_t q0 = (int64_t)blockIdx.x * TQ;
+    const int tq = (int)((nq - q0) < TQ ? (nq - q0) : TQ);
+    // the quad this lane copies (the same for every copy: 16 lanes per row), clamped
+    // for the last block's lanes past the end (a valid address whose value is never stored)
+    const int64_t myq = (q0 + (t % TQ)) < nq ? q0 + (t % TQ) : nq - 1;
+    const int rsub = t / TQ;  // this lane's row within each 4-row copy
+    float acc = 0.f;
+    const int64_t nfull = N / R;
+    auto issue = [&](int64_t c) {
+        char* slot = smem + (int)(c % S) * SLOT_B;
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) glds16(X4 + (c * R + 4 * j + rsub) * ldq + myq, slot + j * 1024);
+        if (t < R) {
+            glds4(a + c * R + t, slot + TILE_B);
+            if constexpr (SCORED) glds4(s + c * R + t, slot + TILE_B + R * 4);
+        }
+    };
+    auto fold = [&](const char* slot, int rows, bool first) {
+        const float* tile = reinterpret_cast<const float*>(slot);  // [rows][64] floats
+        const float* fa = reinterpret_cast<const float*>(slot + TILE_B);
+        const float* fs = fa + R;
+        int r = 0;
+        if (first) {
+            acc = term1<SCORED>(tile[t], fa[0], SCORED ? fs[0] : 1.0f);
+            r = 1;
+        }
+        for (; r + 8 <= rows; r += 8) {
+            float x[8], f[8], g[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = tile[(r + k) * 64 + t];
+                f[k] = fa[r + k];
+                g[k] = SCORED ? fs[r + k] : 1.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = acc + term1<SCORED>(x[k], f[k], g[k]);
+        }
+        for (; r < rows; ++r) acc = acc + term1<SCORED>(tile[r * 64 + t], fa[r], SCORED ? fs[r] : 1.0f);
+    };
+    const int64_t pre = nfull < S - 1 ? nfull : S - 1;
+    for (int64_t c = 0; c < pre; ++c) issue(c);
+    for (int64_t c = 0; c < nfull; ++c) {
+        // chunk c landed; chunks c+1 .. c+S-2 stay in flight
+        if (c + S - 2 < nfull) wait_vmcnt<(S - 2) * (LQ + F)>();
+        else wait_vmcnt<0>();
+        // slot (c-1) % S was folded in the previous iteration: its LDS reads
+        // are complete before the copies into it are issued; the "memory"
+        // clobber also keeps the compiler from moving chunk c's LDS reads above
+        // the vmcnt wait
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c + S - 1 < nfull) issue(c + S - 1);
+        fold(smem + (int)(c % S) * SLOT_B, R, c == 0);
+    }
+    wait_vmcnt<0>();
+    if (nfull * R < N) {  // the last, partial chunk: register path through slot 0
+        const int64_t c = nfull;
+        f32x4* tile = reinterpret_cast<f32x4*>(smem);
+        float* fa = reinterpret_cast<float*>(smem + TILE_B);
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+            const int64_t row = c * R + 4 * j + rsub;
+            if (row < N) tile[j * 64 + t] = __builtin_nontemporal_load(X4 + row * ldq + myq);
+        }
+        if (t < R && c * R + t < N) {
+            fa[t] = a[c * R + t];
+            if constexpr (SCORED) fa[R + t] = s[c * R + t];
+        }
+        __syncthreads();
+        fold(smem, (int)(N - c * R), c == 0);
+    }
+    if (t < 4 * tq) __builtin_nontemporal_store(acc / divisor, out + q0 * 4 + t);
+}
+
+template <int R, int S>
+int launch_w1(hipStream_t st, bool sc, const float* X, int64_t N, int64_t P, int64_t ldx, const float* a,
+              const float* s, float d, float* out) {
+    const int64_t blocks = ((P >> 2) + 15) / 16 + ((P & 3) ? 1 : 0);
+    if (blocks > (int64_t)0x7FFFFFFF) return fail(FA_ERR_ARG, "P=%lld too large for a w1 launch", (long long)P);
+    if (sc)
+        hipLaunchKernelGGL((k_fold_f32_w1<R, S, true>), dim3((unsigned)blocks), dim3(64), 0, st, X, N, P, ldx, a, s,
+                           d, out);
+    else
+        hipLaunchKernelGGL((k_fold_f32_w1<R, S, false>), dim3((unsigned)blocks), dim3(64), 0, st, X, N, P, ldx, a, s,
+                           d, out);
+    return FA_OK;
+}
+
 // Split-client fold (opt-in, NOT bit-exact; fa_fedavg_f32_splitn).
 //   For models too narrow to fill the chip even with LDS staging, the
 //   clients of every column are cut into S = 4*NW contiguous slices.  A block
@@ -1418,8 +1569,8 @@ int cu_count() {
 enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
-                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32 };
-constexpr int kNumF32Picks = (int)F32Pick::kLdsQfW4T32 + 1;
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kW1R32S6, kW1R64S4 };
+constexpr int kNumF32Picks = (int)F32Pick::kW1R64S4 + 1;
 inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
@@ -1440,6 +1591,8 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kTileU8C2: return "tile_8k";
         case F32Pick::kEvenU4C4: return "even_u4c4";
         case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
+        case F32Pick::kW1R32S6: return "w1_r32_s6";
+        case F32Pick::kW1R64S4: return "w1_r64_s4";
     }
     return "";
 }
@@ -1857,12 +2010,13 @@ inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (nq < (1 << 16)) {  // narrow models: the LDS-staged forms, the 4 KiB tile
         for (F32Pick p : {F32Pick::kLdsW2T16, F32Pick::kLdsW2T16D2, F32Pick::kLdsW2T32, F32Pick::kLdsW4T24,
-                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1})
+                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1,
+                          F32Pick::kW1R32S6, F32Pick::kW1R64S4})
             add(p);
     } else if (tiles4 < 2 * cus) {  // under two 16 KiB tiles per CU: where the forms swing most
         for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBalC2, F32Pick::kTileC4Plain, F32Pick::kTileC4,
                           F32Pick::kTileU8C2, F32Pick::kTileC1, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32,
-                          F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6})
+                          F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6, F32Pick::kW1R32S6})
             add(p);
         add(F32Pick::kColumn);
     } else {  // large models: the grid-stride forms, the 16 KiB tile, the even split
@@ -1946,6 +2100,12 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
         case F32Pick::kLdsQfW4T32:  // LDS-staged, 4 waves, 16-row chunks of 32-quad tiles, quad fold
             rc = launch_lds_flags<4, 16, 32, 2, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
                                                                       divisor, out);
+            break;
+        case F32Pick::kW1R32S6:  // one wave per 64 columns, LDS-DMA chunks of 32 rows, 5 in flight
+            rc = launch_w1<32, 6>(st, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
+        case F32Pick::kW1R64S4:  // one wave per 64 columns, LDS-DMA chunks of 64 rows, 3 in flight
+            rc = launch_w1<64, 4>(st, sc, X, N, P, ldx, a, s, divisor, out);
             break;
     }
     return rc;
