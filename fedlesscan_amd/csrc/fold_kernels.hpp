@@ -795,8 +795,12 @@ int launch_ring_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* 
 }
 
 // ---------------------------------------------------------------------------
-// One-wave LDS-DMA fold for narrow models (k_fold_f32_w1, round 3; a tuner
-// candidate, never the policy's pick).  A block is ONE wave owning 64 columns
+// One-wave LDS-DMA fold for narrow models (k_fold_f32_w1, round 3; measured
+// and NOT adopted: tuning variants w1_* only).  1024 x 16K: 21.3 us (64-row
+// chunks, 3 in flight) against 18.6 us for the two-wave LDS pick; 1024 x 67K
+// 0.065 against 0.045 ms; 16-row chunks 32.5 us: the per-chunk wait / issue
+// cadence of one wave, not the barriers, bounds it
+// (profiles/r03_w1_rejected/).  A block is ONE wave owning 64 columns
 // (16 quads): every chunk of R client rows is copied HBM -> LDS with
 // global_load_lds_dwordx4 (a wave-instruction moves 4 rows x 256 B), S-1
 // chunks in flight, and the same wave folds each landed chunk with one column
@@ -1569,8 +1573,8 @@ int cu_count() {
 enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
-                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kW1R32S6, kW1R64S4 };
-constexpr int kNumF32Picks = (int)F32Pick::kW1R64S4 + 1;
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32 };
+constexpr int kNumF32Picks = (int)F32Pick::kLdsQfW4T32 + 1;
 inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
@@ -1591,8 +1595,6 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kTileU8C2: return "tile_8k";
         case F32Pick::kEvenU4C4: return "even_u4c4";
         case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
-        case F32Pick::kW1R32S6: return "w1_r32_s6";
-        case F32Pick::kW1R64S4: return "w1_r64_s4";
     }
     return "";
 }
@@ -2010,13 +2012,12 @@ inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (nq < (1 << 16)) {  // narrow models: the LDS-staged forms, the 4 KiB tile
         for (F32Pick p : {F32Pick::kLdsW2T16, F32Pick::kLdsW2T16D2, F32Pick::kLdsW2T32, F32Pick::kLdsW4T24,
-                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1,
-                          F32Pick::kW1R32S6, F32Pick::kW1R64S4})
+                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1})
             add(p);
     } else if (tiles4 < 2 * cus) {  // under two 16 KiB tiles per CU: where the forms swing most
         for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBalC2, F32Pick::kTileC4Plain, F32Pick::kTileC4,
                           F32Pick::kTileU8C2, F32Pick::kTileC1, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32,
-                          F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6, F32Pick::kW1R32S6})
+                          F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6})
             add(p);
         add(F32Pick::kColumn);
     } else {  // large models: the grid-stride forms, the 16 KiB tile, the even split
@@ -2100,12 +2101,6 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
         case F32Pick::kLdsQfW4T32:  // LDS-staged, 4 waves, 16-row chunks of 32-quad tiles, quad fold
             rc = launch_lds_flags<4, 16, 32, 2, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
                                                                       divisor, out);
-            break;
-        case F32Pick::kW1R32S6:  // one wave per 64 columns, LDS-DMA chunks of 32 rows, 5 in flight
-            rc = launch_w1<32, 6>(st, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
-        case F32Pick::kW1R64S4:  // one wave per 64 columns, LDS-DMA chunks of 64 rows, 3 in flight
-            rc = launch_w1<64, 4>(st, sc, X, N, P, ldx, a, s, divisor, out);
             break;
     }
     return rc;
