@@ -77,6 +77,11 @@ typedef __attribute__((address_space(1))) const float gf32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+// [a, a + na) and [b, b + nb) share a byte
+inline bool overlaps(const void* a, size_t na, const void* b, size_t nb) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+    return x < y + nb && y < x + na;
+}
 
 // ---------------------------------------------------------------------------
 // device helpers
@@ -2152,9 +2157,12 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
         return check_launch("k_fold_f32_scalar");
     }
     const F32Pick policy = pick_f32(N, P);
-    // a plain one-shot fold (no accumulator in, with the divide) of a shape
-    // seen before takes the form the tuner measured fastest on this device
-    if (!acc && fin && N > 0) {
+    // a plain one-shot fold (no accumulator in, with the divide) takes the
+    // form the tuner measured fastest on this device.  Not when `out` overlaps
+    // the rows: the measuring call runs several launches, and a later one
+    // would read what an earlier one wrote (one launch alone reads every row
+    // of a column before it writes that column)
+    if (!acc && fin && N > 0 && !overlaps(out, (size_t)P * 4, X, ((size_t)(N - 1) * ldx + P) * 4)) {
         const int rc = g_tuner.run(kTuneF32, N, P, ldx, sc, (int)policy, (double)N * (double)P * 4.0, st,
                                    [&](std::vector<int>& c) { f32_candidates(N, P, (int)policy, c); },
                                    [&](int form) {
@@ -2262,6 +2270,11 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
         return check_launch("k_fedavg_bf16_scalar");
     }
     const Bf16Form policy = pick_bf16(N, P);
+    const size_t xbytes = ((size_t)(N - 1) * ldx + P) * 2;
+    if (overlaps(out_f32, (size_t)P * 4, X, xbytes) || (out_bf16 && overlaps(out_bf16, (size_t)P * 2, X, xbytes))) {
+        launch_bf16_form(policy, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);  // in place: one launch
+        return check_launch("fedavg_bf16");
+    }
     g_tuner.run(kTuneBf16, N, P, ldx, s != nullptr, (int)policy, (double)N * (double)P * 2.0, st,
                 [&](std::vector<int>& c) { bf16_candidates(N, P, (int)policy, c); },
                 [&](int form) {

@@ -146,7 +146,11 @@ int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  *   fa_fold_form:        the form a shape runs on the stream's device:
  *                        the measured choice, "" while it is being measured,
  *                        the policy's form for an unseen shape or with the
- *                        tuner off. */
+ *                        tuner off.
+ * The measuring call runs several launches into the same output, so a fold
+ * whose out overlaps its input rows keeps the policy's single launch; for
+ * fa_fedavg_f32_ptrs_aligned (row pointers live in device memory) out must
+ * not alias a row -- as the reference, which returns new arrays. */
 enum fa_fold_kind {
     FA_FOLD_F32 = 1,      /* fa_fedavg_f32 (_hostf)                     */
     FA_FOLD_BF16 = 2,     /* fa_fedavg_bf16 (_hostf)                    */

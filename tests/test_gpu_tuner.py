@@ -219,3 +219,33 @@ def test_row_table_every_form_and_the_tuned_calls_bit_exact(dev, L, N, P, scored
     outs.append(fold())
     for k, o in enumerate(outs):
         assert G.same_bits(o.cpu().numpy(), exp), (N, P, k)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_output_over_the_rows_is_not_measured(dev, L, dt):
+    """out inside the stacked rows (an in-place fold into row 0): the measuring
+    call's later launches would read what earlier ones wrote, so such a call
+    takes the policy's single launch and is still exact."""
+    from fedlesscan_amd import _lib
+    N, P = 64, 300_032
+    w = synth.cardinalities(301, N)
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    div = float(np.float32(sum(w)))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    if dt == "f32":
+        X = synth.clients_f32(301, N, 0, P)
+        exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+        Xd = torch.from_numpy(X).to(dev)
+        _lib.check(L.fa_fedavg_f32(Xd.data_ptr(), N, P, P, a.data_ptr(), None, div, Xd.data_ptr(), st), "in place")
+        got = Xd[0].cpu().numpy()
+        assert G.same_bits(got, exp)
+        assert L.fa_fold_form(1, N, P, P, 0, st) == _lib.load_bench().fa_f32_pick_name(N, P, 0)  # never measured
+    else:
+        Xb = synth.clients_bf16(301, N, 0, P)
+        ef, eb = OL.fedavg_bf16(Xb, np.array(w, np.float32), np.float32(sum(w)))
+        Xd = torch.from_numpy(Xb.view(np.int16)).to(dev)
+        o = torch.empty(P, dtype=torch.float32, device=dev)
+        _lib.check(L.fa_fedavg_bf16(Xd.data_ptr(), N, P, P, a.data_ptr(), None, div, o.data_ptr(), Xd.data_ptr(), st),
+                   "bf16 copy in place")
+        assert G.same_bits(o.cpu().numpy(), ef)
+        assert np.array_equal(Xd[0].cpu().numpy().view(np.uint16), eb)
