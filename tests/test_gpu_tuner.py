@@ -249,3 +249,33 @@ def test_output_over_the_rows_is_not_measured(dev, L, dt):
                    "bf16 copy in place")
         assert G.same_bits(o.cpu().numpy(), ef)
         assert np.array_equal(Xd[0].cpu().numpy().view(np.uint16), eb)
+
+
+def test_fold_inside_a_graph_capture(dev, L):
+    """A fold captured into a HIP graph (torch.cuda.graph) takes the policy's
+    single launch: no events are recorded inside a capture, and replays of
+    the graph are bit-exact."""
+    from fedlesscan_amd import _lib
+    N, P = 48, 640_000
+    X = synth.clients_f32(401, N, 0, P)
+    w = synth.cardinalities(401, N)
+    Xd = torch.from_numpy(X).to(dev)
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    out = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
+    div = float(np.float32(sum(w)))
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            _lib.check(L.fa_fedavg_f32(Xd.data_ptr(), N, P, P, a.data_ptr(), None, div, out.data_ptr(),
+                                       torch.cuda.current_stream(dev).cuda_stream), "captured fold")
+    torch.cuda.current_stream(dev).wait_stream(s)
+    assert L.fa_fold_form(1, N, P, P, 0, torch.cuda.current_stream(dev).cuda_stream) == \
+        _lib.load_bench().fa_f32_pick_name(N, P, 0)  # nothing measured during the capture
+    for _ in range(3):
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert G.same_bits(out.cpu().numpy(), exp)
