@@ -76,15 +76,23 @@ class Tuner {
             return launch(policy);
         }
         const Key key{dev, kind, N, P, ldx, scored ? 1 : 0};
+        // no event calls inside a graph capture: neither the measurement nor
+        // the queries of an earlier one (hipEventQuery is not capture-safe)
+        auto capturing = [&] {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+                (void)hipGetLastError();
+                return true;  // unknown: treat as capturing
+            }
+            return cs != hipStreamCaptureStatusNone;
+        };
         Entry* e = nullptr;
         bool explore = false;
         {
             std::lock_guard<std::mutex> lk(mu_);
             auto it = map_.find(key);
             if (it == map_.end()) {
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                if (hipStreamIsCapturing(st, &cs) != hipSuccess) (void)hipGetLastError();
-                if (cs != hipStreamCaptureStatusNone) return launch(policy);  // no events inside a graph capture
+                if (capturing()) return launch(policy);
                 Entry fresh;
                 cands(fresh.cand);
                 fresh.kind = kind;
@@ -99,6 +107,7 @@ class Tuner {
             e = &it->second;  // std::map nodes are stable
             if (!explore) {
                 if (e->chosen < 0) {
+                    if (capturing()) return launch(e->cand[0]);
                     harvest(*e);
                     if (e->chosen < 0) return launch(e->cand[0]);  // measurement still in flight
                 }

@@ -118,6 +118,22 @@ int main() {
         CHECK(launches == 1 && t.chosen(0, 1, 3, 31, 31, false) == -2);
         CHECK(t.set_mode(1) == 0);
     }
+    // 5b. a capture that starts while a measurement is in flight: no event queries
+    //     inside it (the policy runs), the decision comes after it
+    {
+        Tuner t(name);
+        SimStream s;
+        tunersim::not_ready_queries() = 1;
+        call(t, &s, 4, 44, {1.0, 0.3}, nullptr);
+        s.capturing = true;
+        int launches = 0;
+        for (int i = 0; i < 5; ++i) call(t, &s, 4, 44, {1.0, 0.3}, &launches);
+        CHECK(launches == 5);
+        s.capturing = false;
+        call(t, &s, 4, 44, {1.0, 0.3}, nullptr);  // first query after the capture: still in flight
+        CHECK(t.chosen(0, 1, 4, 44, 44, false) == 1);
+        tunersim::not_ready_queries() = 2;
+    }
     // 6. many threads, many shapes, each thread on its own stream and device
     {
         Tuner t(name);
