@@ -121,6 +121,13 @@ __global__ __launch_bounds__(kBlock) void k_read_sweep(const f32x4* __restrict__
     if (threadIdx.x == 0) sink[blockIdx.x % sink_len] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Grid-stride copy on a fixed number of blocks (fa_bench_copy_f32).
+__global__ __launch_bounds__(kBlock) void k_bench_copy(f32x4* __restrict__ dst, const f32x4* __restrict__ src,
+                                                       int64_t nq) {
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kBlock)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + q), dst + q);
+}
+
 // Variant 0 is the product's auto fold (fold_f32_auto); the others are the
 // alternatives whose sweeps chose it (profiles/r01_sweep_*.log).
 // Names: u<rows ahead>c<quads per lane>, nt = non-temporal loads, _nts =
@@ -636,6 +643,15 @@ int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64
     hipLaunchKernelGGL(k_synth<uint16_t>, dim3(8192), dim3(kBlock), 0, (hipStream_t)stream, X, nrows, ncols,
                        ldx, seed, row0, col0);
     return check_launch("k_synth<bf16>");
+}
+
+int fa_bench_copy_f32(float* dst, const float* src, int64_t n, int blocks, void* stream) {
+    if (n < 0 || blocks < 1 || (n > 0 && (!dst || !src)) || !aligned16(dst) || !aligned16(src) || (n & 3))
+        return fail(FA_ERR_ARG, "bench copy needs 16-B aligned buffers, n %% 4 == 0, blocks >= 1");
+    if (n == 0) { g_err[0] = 0; return FA_OK; }
+    hipLaunchKernelGGL(k_bench_copy, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<f32x4*>(dst), reinterpret_cast<const f32x4*>(src), n >> 2);
+    return check_launch("k_bench_copy");
 }
 
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream) {

@@ -30,6 +30,10 @@ int fa_synth_bf16(uint16_t* X, int64_t nrows, int64_t ncols, int64_t ldx, uint64
  * per lane) -> one partial per block in sink[block % sink_len] (values are
  * meaningless): the streaming-read ceiling the fold is compared with. */
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream);
+/* A copy kernel on a fixed number of blocks (dst <- src, n floats, 16-B
+ * aligned, n % 4 == 0): stands in for a collective's kernels next to the fold
+ * (tools/exchange_interference.py), which occupy a few CUs each. */
+int fa_bench_copy_f32(float* dst, const float* src, int64_t n, int blocks, void* stream);
 /* fa_fedavg_f32 with an explicit kernel variant; variant 0 = the product's
  * auto fold.  Layouts the vector kernels cannot take (X / out not 16-B
  * aligned, ldx % 4 != 0) run the product's scalar fold whatever the variant.

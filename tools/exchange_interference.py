@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""How much does a collective's traffic beside the fold slow the fold?  A proxy
+for the 8-GPU exchange on a one-GPU box: one rank's step with the default slot
+layout (sharding.overlap_layout) on the high-priority fold stream, and after
+each round's fold, on a normal-priority stream, a copy kernel on a fixed
+number of blocks moving the bytes that rank would receive in that round's
+all-gather ((world - 1) x the round's slot).  An RCCL all-gather over xGMI
+only WRITES those bytes into local HBM and runs its own kernels on a few CUs;
+this copy reads and writes them, so it over-states the HBM side and roughly
+matches the CU side.  Prints the fold time per step with and without it.
+
+    python tools/exchange_interference.py [--config c3|c4] [--world 8] [--blocks 16,32,64]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedlesscan_amd import _lib, synth  # noqa: E402
+from fedlesscan_amd.engine import Factors  # noqa: E402
+from fedlesscan_amd.sharding import fold_stream, overlap_layout  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=["c3", "c4"])
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--blocks", default="16,32,64")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L, B = _lib.load(), _lib.load_bench()
+    if args.config == "c3":
+        N, P_rank, dt, esz, out_esz = 1024, 10_000_000, "f32", 4, 4
+        P_total = P_rank * args.world
+    else:
+        N, P_total, dt, esz, out_esz = 256, 100_000_000, "bf16", 2, 2
+    lay = overlap_layout(P_total, args.world, dt)
+    W = lay.local_width
+    st0 = torch.cuda.current_stream(dev)
+    X = torch.empty((N, W), dtype=torch.float32 if dt == "f32" else torch.bfloat16, device=dev)
+    gen = B.fa_synth_f32 if dt == "f32" else B.fa_synth_bf16
+    _lib.check(gen(X.data_ptr(), N, W, W, 11, 0, 0, st0.cuda_stream), "synth", bench=True)
+    w = synth.cardinalities(11, N)
+    a, _ = Factors(w, None, np.dtype(np.float32)).to(dev)
+    div = float(np.float32(sum(w)))
+    out = torch.empty(W, dtype=torch.float32, device=dev)
+    outb = torch.empty(W, dtype=torch.bfloat16, device=dev) if dt == "bf16" else None
+    recv = max(lay.widths) * (args.world - 1) * out_esz // 4 * 4  # floats moved per round, at most
+    src = torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    fs = fold_stream(dev)
+    xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
+
+    def fold(k):
+        off, width = lay.offset(k), lay.width(k)
+        x = X.data_ptr() + off * esz
+        if dt == "f32":
+            rc = L.fa_fedavg_f32(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, fs.cuda_stream)
+        else:
+            rc = L.fa_fedavg_bf16(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+                                  outb.data_ptr() + off * 2, fs.cuda_stream)
+        _lib.check(rc, "fold")
+
+    def step(blocks, ev):
+        for k in range(lay.rounds):
+            ev[k][0].record(fs)
+            fold(k)
+            ev[k][1].record(fs)
+            if blocks:
+                xs.wait_event(ev[k][1])
+                n = (lay.width(k) * (args.world - 1) * out_esz) // 16 * 4
+                _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
+                           bench=True)
+        fs.wait_stream(xs)
+
+    for _ in range(3):  # the tuner's first calls, warm-up
+        step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(lay.rounds)])
+    torch.cuda.synchronize()
+    print(f"{args.config} rank of {args.world}: widths {lay.widths}")
+    for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
+        folds = []
+        for _ in range(args.steps):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(lay.rounds)]
+            step(blocks, ev)
+            torch.cuda.synchronize()
+            folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
+        folds.sort()
+        print(f"  copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
+              f"(min {folds[0]:.4f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
