@@ -221,6 +221,37 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
         fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
 
+// Grid-stride fold with tiles handed out dynamically (k_fold_f32_dyn, round
+// 3): ~one block per CU, each fetching its next tile from a device counter.
+// When other kernels share some CUs -- an all-gather overlapping the next
+// round's fold -- the blocks there run slower, and a static tile assignment
+// makes every other block of the launch wait for them at its end
+// (tools/exchange_interference.py); with dynamic tiles the slowed blocks just
+// fold fewer of them.  ctr = {next tile, blocks done}: the last block to
+// finish zeroes both for the next launch that uses the slot.
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
+__global__ __launch_bounds__(B) void k_fold_f32_dyn(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s,
+    const float* acc_in, float divisor, float* out, int64_t ntiles, unsigned int* ctr) {
+    __shared__ unsigned int next;
+    for (;;) {
+        if (threadIdx.x == 0) next = atomicAdd(&ctr[0], 1u);
+        __syncthreads();
+        const int64_t bid = next;
+        __syncthreads();  // every thread has the tile before thread 0 fetches the next
+        if (bid >= ntiles) break;
+        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
+            atomicExch(&ctr[0], 0u);
+            atomicExch(&ctr[1], 0u);
+        }
+    }
+}
+
 // One block per tile (few clients: more blocks in flight than the grid-stride
 // form, each with a short row run).
 template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
@@ -1555,6 +1586,47 @@ int cu_count() {
     return cus;
 }
 
+// Counter slots of the dynamic-tile folds (k_fold_f32_dyn), per device:
+// kDynSlots pairs of unsigned ints, zeroed when first allocated; a launch takes
+// the next pair (fewer than kDynSlots such launches may be in flight on one
+// device at once) and leaves it zeroed.  nullptr (the caller then launches the
+// static schedule): no device memory, or a stream under graph capture (no
+// allocation there, and a captured slot would be replayed).
+constexpr unsigned kDynSlots = 4096;
+struct DynCounters {
+    std::mutex mu;
+    unsigned int* base = nullptr;
+    std::atomic<unsigned> next{0};
+};
+DynCounters g_dyn[16];
+inline unsigned int* dyn_slot(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    DynCounters& D = g_dyn[dev];
+    {
+        std::lock_guard<std::mutex> lk(D.mu);
+        if (!D.base) {
+            void* p = nullptr;
+            if (hipMalloc(&p, 2 * sizeof(unsigned int) * kDynSlots) != hipSuccess ||
+                hipMemset(p, 0, 2 * sizeof(unsigned int) * kDynSlots) != hipSuccess) {
+                (void)hipGetLastError();
+                if (p) (void)hipFree(p);
+                return nullptr;
+            }
+            D.base = static_cast<unsigned int*>(p);
+        }
+    }
+    return D.base + 2 * (D.next.fetch_add(1) % kDynSlots);
+}
+
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
@@ -1578,8 +1650,8 @@ int cu_count() {
 enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
-                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32 };
-constexpr int kNumF32Picks = (int)F32Pick::kLdsQfW4T32 + 1;
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kDynC4, kDynC2 };
+constexpr int kNumF32Picks = (int)F32Pick::kDynC2 + 1;
 inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
@@ -1600,6 +1672,8 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kTileU8C2: return "tile_8k";
         case F32Pick::kEvenU4C4: return "even_u4c4";
         case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
+        case F32Pick::kDynC4: return "dyn_16k";
+        case F32Pick::kDynC2: return "dyn_8k";
     }
     return "";
 }
@@ -1756,6 +1830,35 @@ void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, co
         else     { if (fin) FA_G(false, false, true); else FA_G(false, false, false); }
     }
 #undef FA_G
+}
+
+// Dynamic tiles (k_fold_f32_dyn) on ~one block per CU; the static balanced
+// grid-stride launch when no counter slot is available.
+template <int U, int C, bool NTS, bool ALLF = false>
+void launch_dyn_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
+                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
+    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
+    if (!ctr) {
+        launch_gs_flags<U, C, NTS, kBlock, ALLF>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out);
+        return;
+    }
+    int64_t grid = cu_count();
+    if (grid > tiles) grid = tiles;
+#define FA_D(SC, ACC, FIN)                                                                                  \
+    hipLaunchKernelGGL((k_fold_f32_dyn<U, C, true, SC, ACC, FIN, NTS>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
+                       X, N, P, ldx, a, s, acc_in, d, out, tiles, ctr)
+    if constexpr (!ALLF) {
+        if (sc) FA_D(true, false, true); else FA_D(false, false, true);
+    } else if (sc) {
+        if (acc) { if (fin) FA_D(true, true, true); else FA_D(true, true, false); }
+        else     { if (fin) FA_D(true, false, true); else FA_D(true, false, false); }
+    } else {
+        if (acc) { if (fin) FA_D(false, true, true); else FA_D(false, true, false); }
+        else     { if (fin) FA_D(false, false, true); else FA_D(false, false, false); }
+    }
+#undef FA_D
 }
 
 // Column bands: the fold as several back-to-back balanced grid-stride
@@ -2106,6 +2209,12 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
         case F32Pick::kLdsQfW4T32:  // LDS-staged, 4 waves, 16-row chunks of 32-quad tiles, quad fold
             rc = launch_lds_flags<4, 16, 32, 2, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
                                                                       divisor, out);
+            break;
+        case F32Pick::kDynC4:  // dynamic 16 KiB tiles on ~one block per CU
+            launch_dyn_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            break;
+        case F32Pick::kDynC2:  // dynamic 8 KiB tiles (twice the tiles: finer balance)
+            launch_dyn_flags<8, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
     }
     return rc;

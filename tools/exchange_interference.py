@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--blocks", default="16,32,64")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--forms", default="", help="fp32 only: comma-separated fold forms (fa_f32_form_name) to force "
+                                              "instead of the product's tuned choice")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L, B = _lib.load(), _lib.load_bench()
@@ -55,9 +57,17 @@ def main():
     fs = fold_stream(dev)
     xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
 
+    names = {B.fa_f32_form_name(i).decode(): i for i in range(B.fa_num_f32_forms())}
+    form = [None]
+
     def fold(k):
         off, width = lay.offset(k), lay.width(k)
         x = X.data_ptr() + off * esz
+        if dt == "f32" and form[0] is not None:
+            rc = B.fa_fedavg_f32_form(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+                                      fs.cuda_stream, form[0])
+            _lib.check(rc, "form", bench=True)
+            return
         if dt == "f32":
             rc = L.fa_fedavg_f32(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, fs.cuda_stream)
         else:
@@ -82,17 +92,24 @@ def main():
                  for _ in range(lay.rounds)])
     torch.cuda.synchronize()
     print(f"{args.config} rank of {args.world}: widths {lay.widths}")
-    for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
-        folds = []
-        for _ in range(args.steps):
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(lay.rounds)]
-            step(blocks, ev)
-            torch.cuda.synchronize()
-            folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
-        folds.sort()
-        print(f"  copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
-              f"(min {folds[0]:.4f})", flush=True)
+    for fname in [f for f in args.forms.split(",") if f] or [None]:
+        form[0] = None if fname is None else names[fname]
+        for _ in range(2):  # warm the forced form
+            step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                     for _ in range(lay.rounds)])
+        torch.cuda.synchronize()
+        label = fname or "tuned"
+        for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
+            folds = []
+            for _ in range(args.steps):
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(lay.rounds)]
+                step(blocks, ev)
+                torch.cuda.synchronize()
+                folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
+            folds.sort()
+            print(f"  {label:14s} copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
+                  f"(min {folds[0]:.4f})", flush=True)
 
 
 if __name__ == "__main__":
