@@ -217,11 +217,6 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
     const float* __restrict__ a, const float* __restrict__ s,
     const float* acc_in, float divisor, float* out, int64_t ntiles) {  // acc_in may alias out
-    // highest wave priority: where another kernel shares a CU (an all-gather
-    // overlapping the next round's fold), the fold's waves win the issue
-    // arbitration, so its blocks do not become the launch's stragglers
-    // (tools/exchange_interference.py); among the fold's own waves it changes nothing
-    __builtin_amdgcn_s_setprio(3);
     for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
         fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
@@ -240,7 +235,6 @@ __global__ __launch_bounds__(B) void k_fold_f32_dyn(
     const float* __restrict__ a, const float* __restrict__ s,
     const float* acc_in, float divisor, float* out, int64_t ntiles, unsigned int* ctr) {
     __shared__ unsigned int next;
-    __builtin_amdgcn_s_setprio(3);  // as k_fold_f32_gs
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(&ctr[0], 1u);
         __syncthreads();
