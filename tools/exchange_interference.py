@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--blocks", default="16,32,64")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--host-src", action="store_true",
+                    help="read the copied bytes from page-locked host memory (long-latency loads over PCIe, closer "
+                         "to an all-gather's remote reads over xGMI than an HBM-to-HBM copy)")
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the received bytes to copy per round")
     ap.add_argument("--forms", default="", help="fp32 only: comma-separated fold forms (fa_f32_form_name) to force "
                                               "instead of the product's tuned choice")
     args = ap.parse_args()
@@ -52,8 +56,9 @@ def main():
     out = torch.empty(W, dtype=torch.float32, device=dev)
     outb = torch.empty(W, dtype=torch.bfloat16, device=dev) if dt == "bf16" else None
     recv = max(lay.widths) * (args.world - 1) * out_esz // 4 * 4  # floats moved per round, at most
-    src = torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev)
-    dst = torch.empty_like(src)
+    src = (torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, pin_memory=True) if args.host_src else
+           torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev))
+    dst = torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev)
     fs = fold_stream(dev)
     xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
 
@@ -82,7 +87,7 @@ def main():
             ev[k][1].record(fs)
             if blocks:
                 xs.wait_event(ev[k][1])
-                n = (lay.width(k) * (args.world - 1) * out_esz) // 16 * 4
+                n = int(lay.width(k) * (args.world - 1) * out_esz * args.scale) // 16 * 4
                 _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
                            bench=True)
         fs.wait_stream(xs)
@@ -91,7 +96,8 @@ def main():
         step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                  for _ in range(lay.rounds)])
     torch.cuda.synchronize()
-    print(f"{args.config} rank of {args.world}: widths {lay.widths}")
+    print(f"{args.config} rank of {args.world}: widths {lay.widths}, copy source "
+          f"{'host (PCIe)' if args.host_src else 'HBM'}, {args.scale:g} of the received bytes")
     for fname in [f for f in args.forms.split(",") if f] or [None]:
         form[0] = None if fname is None else names[fname]
         for _ in range(2):  # warm the forced form
