@@ -83,6 +83,8 @@ _BENCH_PROTOS = {
     "fa_synth_bf16": (_int, [_vp, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _vp]),
     "fa_read_sweep_f32": (_int, [_vp, _i64, _vp, _i64, _vp]),
     "fa_bench_copy_f32": (_int, [_vp, _vp, _i64, _int, _vp]),
+    "fa_bench_stream_cu_mask": (_int, [_int, _vp, _int, _vp]),
+    "fa_bench_stream_destroy": (_int, [_vp]),
     "fa_fedavg_f32_variant": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
     "fa_num_variants": (_int, []),
     "fa_variant_name": (ctypes.c_char_p, [_int]),

@@ -654,6 +654,26 @@ int fa_bench_copy_f32(float* dst, const float* src, int64_t n, int blocks, void*
     return check_launch("k_bench_copy");
 }
 
+int fa_bench_stream_cu_mask(int device, const uint32_t* mask, int words, void** stream) {
+    if (!mask || words < 1 || !stream) return fail(FA_ERR_ARG, "bad CU mask arguments");
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_ERR_HIP, "cannot select device %d", device);
+    }
+    hipStream_t st = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
+    *stream = st;
+    g_err[0] = 0;
+    return FA_OK;
+}
+int fa_bench_stream_destroy(void* stream) {
+    if (stream && hipStreamDestroy((hipStream_t)stream) != hipSuccess) return fail(FA_ERR_HIP, "hipStreamDestroy");
+    return FA_OK;
+}
+
 int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, void* stream) {
     if (n < 0 || !X || !sink || sink_len <= 0 || !aligned16(X) || (n & 3))
         return fail(FA_ERR_ARG, "read sweep needs 16-B aligned X, n %% 4 == 0, sink_len > 0");

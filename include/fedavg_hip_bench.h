@@ -34,6 +34,11 @@ int fa_read_sweep_f32(const float* X, int64_t n, float* sink, int64_t sink_len, 
  * aligned, n % 4 == 0): stands in for a collective's kernels next to the fold
  * (tools/exchange_interference.py), which occupy a few CUs each. */
 int fa_bench_copy_f32(float* dst, const float* src, int64_t n, int blocks, void* stream);
+/* A stream on `device` limited to the CUs whose bit is set in mask[0..words)
+ * (hipExtStreamCreateWithCUMask), and its release: the exchange proxy's
+ * fold stream that leaves some CUs to the collective. */
+int fa_bench_stream_cu_mask(int device, const uint32_t* mask, int words, void** stream);
+int fa_bench_stream_destroy(void* stream);
 /* fa_fedavg_f32 with an explicit kernel variant; variant 0 = the product's
  * auto fold.  Layouts the vector kernels cannot take (X / out not 16-B
  * aligned, ldx % 4 != 0) run the product's scalar fold whatever the variant.

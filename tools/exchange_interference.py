@@ -34,6 +34,11 @@ def main():
                     help="read the copied bytes from page-locked host memory (long-latency loads over PCIe, closer "
                          "to an all-gather's remote reads over xGMI than an HBM-to-HBM copy)")
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the received bytes to copy per round")
+    ap.add_argument("--fold-free", type=int, default=0,
+                    help="leave this many CUs (every (256/k)-th CU id) out of the fold stream's CU mask")
+    ap.add_argument("--copy-on-free", action="store_true",
+                    help="with --fold-free: the copy stream gets exactly the CUs the fold leaves (the ideal "
+                         "placement); otherwise the copy stream has every CU, as RCCL's")
     ap.add_argument("--forms", default="", help="fp32 only: comma-separated fold forms (fa_f32_form_name) to force "
                                               "instead of the product's tuned choice")
     args = ap.parse_args()
@@ -59,8 +64,28 @@ def main():
     src = (torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, pin_memory=True) if args.host_src else
            torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev))
     dst = torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev)
-    fs = fold_stream(dev)
-    xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
+    import ctypes
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    handles = []
+
+    def masked_stream(bits):
+        words = (cus + 31) // 32
+        arr = (ctypes.c_uint32 * words)(*[0] * words)
+        for c in bits:
+            arr[c // 32] |= 1 << (c % 32)
+        h = ctypes.c_void_p()
+        _lib.check(B.fa_bench_stream_cu_mask(0, arr, words, ctypes.byref(h)), "cu mask", bench=True)
+        handles.append(h)
+        return torch.cuda.ExternalStream(h.value, device=dev)
+
+    if args.fold_free:
+        step_ = max(1, cus // args.fold_free)
+        free = [c for c in range(cus) if c % step_ == step_ - 1][:args.fold_free]
+        fs = masked_stream([c for c in range(cus) if c not in free])
+        xs = masked_stream(free) if args.copy_on_free else torch.cuda.Stream(device=dev)
+    else:
+        fs = fold_stream(dev)
+        xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
 
     names = {B.fa_f32_form_name(i).decode(): i for i in range(B.fa_num_f32_forms())}
     form = [None]
@@ -96,7 +121,8 @@ def main():
         step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                  for _ in range(lay.rounds)])
     torch.cuda.synchronize()
-    print(f"{args.config} rank of {args.world}: widths {lay.widths}, copy source "
+    print(f"{args.config} rank of {args.world}: widths {lay.widths}, fold CUs {cus - args.fold_free}"
+          f"{' (copy on the others)' if args.copy_on_free else ''}, copy source "
           f"{'host (PCIe)' if args.host_src else 'HBM'}, {args.scale:g} of the received bytes")
     for fname in [f for f in args.forms.split(",") if f] or [None]:
         form[0] = None if fname is None else names[fname]
