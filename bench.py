@@ -478,13 +478,19 @@ def main():
         exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
         kern_avg = float(np.mean(kern_ms))
         exposed_avg = float(np.mean(exposed_ms))
+        # each round's fold (median over the steps): beside the previous round's
+        # all-gather from round 1 on, alone in round 0 (RCCL's kernels share the CUs)
+        round_ms = [float(np.median([folds[k][0].elapsed_time(folds[k][1]) for folds, _ in evs]))
+                    for k in range(rounds)]
     else:
         kern_avg = region[0].elapsed_time(region[1]) / args.steps  # per fold call, launch gaps included
         exposed_avg = 0.0
+        round_ms = None
     if dist_on:
-        t = torch.tensor([kern_avg, exposed_avg], dtype=torch.float64, device=dev)
+        t = torch.tensor([kern_avg, exposed_avg, *round_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
+        round_ms = [round(float(x), 4) for x in t[2:].tolist()]
 
     # streaming-read ceiling over the same HBM bytes (contiguous, no fold)
     # byte-level sweep: bf16 input is read as the same bytes viewed as fp32 quads
@@ -594,6 +600,7 @@ def main():
             # per-rank split of a step at N > 1 (max over ranks): the fold kernels,
             # and the all-gather left exposed after the last fold of the step
             "fold_ms": round(kern_avg, 4),
+            "fold_ms_per_round": round_ms,
             "gather_exposed_ms": round(exposed_avg, 4) if dist_on else None,
             "gather_bytes_per_rank": (lay.padded_total * (4 if wl.dtype == "f32" else 2)
                                       * (world - 1) // world) if dist_on else 0,
