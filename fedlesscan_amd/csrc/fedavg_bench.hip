@@ -179,10 +179,16 @@ constexpr const char* kVariants[] = {
     "even_g4_auto",
     // one wave per 64 columns, LDS-DMA chunks, no barriers (k_fold_f32_w1, round 3): w1_r<rows>s<slots>
     "w1_r32s6", "w1_r64s4", "w1_r16s12", "w1_r32s8",
+    // the column fold with the terms formed by the loaders (LOPT bit 3, k_fold_f32_lds, round 3):
+    // the product's LDS picks, two deeper forms, and the 4-byte-load pick
+    "pm_lds4_w2r32t16", "pm_lds2_w2r32t16", "pm_lds2_w4r32t24", "pm_lds2_w4r32t40", "pm_lds2_w2r16t32",
+    "pm_lds1_w8r64t32", "pm_lds4_w4r32t16", "pm_lds6_w2r32t16", "pm_dw_lds4_w2r32t16",
 };
 constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
 constexpr int kEndAnyAlign = 92;
+constexpr int kPmDw = 118;  // and this one
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+static_assert(kNumVariants == kPmDw + 1, "pm_dw_lds4_w2r32t16 is the last variant");
 
 // Quads per lane of the round-1 row-streaming policy (variant "v4_pickq_nts"):
 // the widest per-block row run (C * 4 KiB) that still leaves >= ~1000 blocks.
@@ -212,6 +218,8 @@ constexpr const char* kPtrsVariants[] = {
     "ptrs_dw_w2t16d4", "ptrs_dw_t40", "ptrs_dw_t32", "ptrs_dw_t24", "ptrs_rows_scalar", "ptrs_generic",
     // two-wave forms of the stacked fold's 32K-256K picks (16-B aligned rows again)
     "ptrs_o0_w2t32", "ptrs_o4_w2t32", "ptrs_o0_w2t16d2", "ptrs_o4_w2t16d2",
+    // the loaders form the terms (LOPT bit 3), with and without the pointer ring (round 3)
+    "ptrs_o12_w2t16d4", "ptrs_o12_w2t16d6", "ptrs_o8_w2t16d6", "ptrs_o8_w2t16d4",
 };
 constexpr int kNumPtrsVariants = sizeof(kPtrsVariants) / sizeof(kPtrsVariants[0]);
 
@@ -280,7 +288,8 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     // unaligned layouts take the product's fold, except the any-alignment variants
-    if ((variant < kFirstAnyAlign || variant >= kEndAnyAlign) && (!aligned16(X) || (ldx % 4) || !aligned16(out)))
+    if ((variant < kFirstAnyAlign || variant >= kEndAnyAlign) && variant != kPmDw &&
+        (!aligned16(X) || (ldx % 4) || !aligned16(out)))
         return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream);
     hipStream_t st = (hipStream_t)stream;
     const bool sc = s != nullptr, acc = false, fin = true;
@@ -431,6 +440,18 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 108: rc = launch_w1<16, 12>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
         case 109: rc = launch_w1<32, 8>(st, sc, X, N, P, ldx, a, s, divisor, out); break;
 #undef FA_VE
+#define FA_VP(NW, R, TQ, D, DW) \
+    launch_lds_flags<NW, R, TQ, D, false, false, true, 8, DW>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 110: rc = FA_VP(2, 32, 16, 4, false); break;
+        case 111: rc = FA_VP(2, 32, 16, 2, false); break;
+        case 112: rc = FA_VP(4, 32, 24, 2, false); break;
+        case 113: rc = FA_VP(4, 32, 40, 2, false); break;
+        case 114: rc = FA_VP(2, 16, 32, 2, false); break;
+        case 115: rc = FA_VP(8, 64, 32, 1, false); break;
+        case 116: rc = FA_VP(4, 32, 16, 4, false); break;
+        case 117: rc = FA_VP(2, 32, 16, 6, false); break;
+        case kPmDw: rc = FA_VP(2, 32, 16, 4, true); break;
+#undef FA_VP
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
 #undef FA_VF
@@ -608,6 +629,10 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
         case 21: rc = FA_PW(2, 16, 32, 2, 4); break;
         case 22: rc = FA_PW(2, 32, 16, 2, 0); break;
         case 23: rc = FA_PW(2, 32, 16, 2, 4); break;
+        case 24: rc = FA_PW(2, 32, 16, 4, 12); break;
+        case 25: rc = FA_PW(2, 32, 16, 6, 12); break;
+        case 26: rc = FA_PW(2, 32, 16, 6, 8); break;
+        case 27: rc = FA_PW(2, 32, 16, 4, 8); break;
         default: return fail(FA_ERR_ARG, "unknown pointer variant %d", variant);
     }
 #undef FA_PV

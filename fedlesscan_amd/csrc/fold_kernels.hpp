@@ -376,6 +376,8 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     // factors; ROWS with the pointer ring: also the row pointers of the chunk
     // this stage loads next
     constexpr bool PRING = ROWS && (LOPT & 4);
+    constexpr bool PRE = (LOPT & 8) != 0;
+    static_assert(!PRE || COLF, "premultiplied stash: column fold only");
     constexpr int LU = DW ? 4 * LQ : LQ;  // loads per thread per chunk
     constexpr int RW = DW ? 4 * TQ : TQ;  // load units per row of the tile
     struct Stage {
@@ -383,6 +385,7 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         float vf[DW ? LU : 1];
         float fv, sv;
         const float* p[PRING ? LU : 1];
+        float pa[PRE ? LU : 1], ps[PRE && SCORED ? LU : 1];  // PRE: the factors of each load's row
     };
     // DW: this lane's float of the tile for its j-th load, clamped to the last
     // column of the full quads
@@ -421,6 +424,12 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     //   pointer ring) only for the pointer-table form of the narrowest pick,
     //   one block per CU (1024 x 16K rows: 20.3 against 26.1 us; 1024 x 67K,
     //   24-quad tiles: 57.3 against 53.8 us, profiles/r02_lds/ptrs_variants.log).
+    //   bit 3 (PRE, column fold only): the loaders form the terms.  Each lane
+    //     also loads its rows' factors and stashes t = fl(fl(x*a)*s) instead of
+    //     x, with all 64 lanes busy, so the fold's per-row chain is one LDS read
+    //     and one add (the same products and the same ordered adds: the same
+    //     bits).  Without it the fold lanes (CPW of 64 per wave) also read the
+    //     factors and multiply, row by row.
     const float* nxt[ROWS && !PRING ? LU : 1];
     auto fetch_ptrs = [&](int64_t c, Stage& g) {  // chunk index clamped, no branch
         if constexpr (ROWS) {
@@ -457,7 +466,14 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
             for (int j = 0; j < LQ; ++j)
                 g.v[j] = __builtin_nontemporal_load(X4 + (c * R + (t + j * NT) / TQ) * ldq + qof(j));
         }
-        if constexpr (LOPT & 1) {
+        if constexpr (PRE) {
+#pragma unroll
+            for (int j = 0; j < LU; ++j) {
+                const int64_t row = c * R + (t + j * NT) / RW;
+                g.pa[j] = a[row];
+                if constexpr (SCORED) g.ps[j] = s[row];
+            }
+        } else if constexpr (LOPT & 1) {
             g.fv = a[c * R + t % R];
             if constexpr (SCORED) g.sv = s[c * R + t % R];
         } else if (t < R) {
@@ -475,9 +491,13 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
             if (row < N) {
                 if constexpr (DW) g.vf[j] = __builtin_nontemporal_load((const gf32*)rowf(row) + fof(j));
                 else g.v[j] = __builtin_nontemporal_load((const gf32x4*)rowf(row) + qof(j));
+                if constexpr (PRE) {
+                    g.pa[j] = a[row];
+                    if constexpr (SCORED) g.ps[j] = s[row];
+                }
             }
         }
-        if (t < R && c * R + t < N) {
+        if (!PRE && t < R && c * R + t < N) {
             g.fv = a[c * R + t];
             if constexpr (SCORED) g.sv = s[c * R + t];
         }
@@ -486,12 +506,18 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
         if constexpr (DW) {
             float* tw = reinterpret_cast<float*>(tile);  // [R][TQ*4] floats, the quad layout's bytes
 #pragma unroll
-            for (int j = 0; j < LU; ++j) tw[t + j * NT] = g.vf[j];
+            for (int j = 0; j < LU; ++j) {
+                if constexpr (PRE) tw[t + j * NT] = term1<SCORED>(g.vf[j], g.pa[j], SCORED ? g.ps[j] : 1.0f);
+                else tw[t + j * NT] = g.vf[j];
+            }
         } else {
 #pragma unroll
-            for (int j = 0; j < LQ; ++j) tile[t + j * NT] = g.v[j];
+            for (int j = 0; j < LQ; ++j) {
+                if constexpr (PRE) tile[t + j * NT] = term4<SCORED>(g.v[j], g.pa[j], SCORED ? g.ps[j] : 1.0f);
+                else tile[t + j * NT] = g.v[j];
+            }
         }
-        if (t < R) {
+        if (!PRE && t < R) {
             fa[t] = g.fv;
             if constexpr (SCORED) fs[t] = g.sv;
         }
@@ -513,7 +539,23 @@ __global__ __launch_bounds__(NW * 64) void k_fold_f32_lds(
     }
     // fold the staged chunk c (rows valid rows) in client order
     auto fold = [&](int64_t c, int rows) {
-        if constexpr (COLF) {
+        if constexpr (PRE) {  // the tile holds the terms
+            if (cfold) {
+                int r = 0;
+                if (!ACC && c == 0) {
+                    acc1 = tilef[ccol];
+                    r = 1;
+                }
+                for (; r + 8 <= rows; r += 8) {
+                    float x[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = tilef[(r + k) * TC + ccol];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc1 = acc1 + x[k];
+                }
+                for (; r < rows; ++r) acc1 = acc1 + tilef[r * TC + ccol];
+            }
+        } else if constexpr (COLF) {
             if (cfold) {
                 int r = 0;
                 if (!ACC && c == 0) {
@@ -2146,10 +2188,14 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
     int rc = FA_OK;
     switch (pick) {  // every (scored, accumulate, finalize) combination
         case F32Pick::kLdsW2T16:
-            // the narrowest models (one block per CU): two-wave blocks, four
-            // chunks ahead (1024 x 16K: 18.9 us against 22.0 for four waves,
-            // 256 x 16K: 6.6 against 7.8; profiles/r02_lds/sweep_small.log)
-            rc = launch_lds_flags<2, 32, 16, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+            // the narrowest models (one block per CU): two-wave blocks (1024 x
+            // 16K: 18.9 us against 22.0 for four waves, 256 x 16K: 6.6 against
+            // 7.8; profiles/r02_lds/sweep_small.log); round 3: the loaders form
+            // the terms (LOPT bit 3) and six chunks are in flight (1024 x 16K
+            // 18.5 -> 16.6 us, 4096 x 16K 65.7 -> 56.3, stall-aware 1024 x 16K
+            // 21.8 -> 18.7; profiles/r03_premul/)
+            rc = launch_lds_flags<2, 32, 16, 6, true, false, true, 8>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                                      divisor, out);
             break;
         case F32Pick::kLdsW2T16D2:
             rc = launch_lds_flags<2, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);

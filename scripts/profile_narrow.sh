@@ -10,6 +10,7 @@ OUT=$ROOT/gpurun_out/narrow
 SHAPES=${*:-"1024:67267 256:67267 100:582026 10:582026 100:1000000"}
 for s in $SHAPES; do mkdir -p "$OUT/n${s%%:*}_p${s##*:}"; done
 cd /tmp && export TMPDIR=/tmp
+export FEDAVG_AUTOTUNE=0  # the policy form, not a tuned one
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD"
 for s in $SHAPES; do
     n=${s%%:*}; p=${s##*:}

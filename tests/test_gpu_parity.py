@@ -790,7 +790,7 @@ def test_accumulate_finalize_equals_batch(dev, lib, P, scored):
 
 def _lds_variants(B):
     return [v for v in range(B.fa_num_variants())
-            if B.fa_variant_name(v).startswith((b"lds", b"ring", b"qf_", b"o0", b"o1", b"o2", b"dw_", b"scalar"))]
+            if B.fa_variant_name(v).startswith((b"lds", b"ring", b"qf_", b"o0", b"o1", b"o2", b"dw_", b"scalar", b"pm_"))]
 
 
 @pytest.mark.parametrize("N", [1, 2, 63, 64, 65, 127, 128, 129, 257, 300])
@@ -841,8 +841,8 @@ def test_any_alignment_variants(dev, lib, N, P, pitch, off):
     st = torch.cuda.current_stream(dev).cuda_stream
     exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)))
     exp_s = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)), s=np.array(sc, np.float32))
-    vs = [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"dw_", b"scalar"))]
-    assert len(vs) >= 5
+    vs = [v for v in range(B.fa_num_variants()) if B.fa_variant_name(v).startswith((b"dw_", b"scalar", b"pm_dw_"))]
+    assert len(vs) >= 6
     for v in [None] + vs:
         for sp, e in ((None, exp), (s, exp_s)):
             o = torch.full((P + 1,), float("nan"), dtype=torch.float32, device=dev)[1:]  # 4-B offset output
