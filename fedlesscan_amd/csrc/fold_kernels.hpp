@@ -1689,7 +1689,7 @@ inline unsigned int* dyn_slot(hipStream_t st) {
 //   otherwise (C2, C3, C5, ...)        grid-stride, balanced passes, 8 rows x 4 quads,
 //                                      in column bands of <= 3 passes x CUs tiles
 // with non-temporal output stores (plain ones in the 4 KiB tile and column forms).
-enum class F32Pick { kLdsW2T16, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
+enum class F32Pick { kLdsW2T16, kLdsW2T16D4, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
                      kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kDynC4, kDynC2 };
@@ -1698,6 +1698,7 @@ inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
         case F32Pick::kLdsW2T16: return "lds_w2_t16";
+        case F32Pick::kLdsW2T16D4: return "lds_w2_t16_d4";
         case F32Pick::kLdsW2T16D2: return "lds_w2_t16_d2";
         case F32Pick::kLdsW2T32: return "lds_w2_t32";
         case F32Pick::kLdsW4T24: return "lds_w4_t24";
@@ -1763,7 +1764,10 @@ inline F32Pick pick_f32(int64_t N, int64_t P, int64_t cus_override = 0) {
     const int64_t nq = P >> 2, cus = cus_override > 0 ? cus_override : cu_count();
     // up to 32K params (32,768 included: 1.23x faster than the CU-fill pick at
     // 1024 clients, profiles/r02_lds/range_32k_80k_after/)
-    if (nq <= (1 << 13)) return F32Pick::kLdsW2T16;
+    // (round 3: the terms formed by the loaders; six chunks in flight up to
+    // 16K params, four above: 1024 x 32K 22.6 against 24.4 us with six,
+    // profiles/r03_premul/check_sweep.log)
+    if (nq <= (1 << 13)) return nq <= (1 << 12) ? F32Pick::kLdsW2T16 : F32Pick::kLdsW2T16D4;
     // 80K-256K params: two-wave blocks over 32-quad tiles, 16-row chunks: best
     // or within 5 % at 100-1024 clients x 82K-246K, where the 4-wave CU-fill
     // pick lost up to 24 % (131,136 params; profiles/r02_lds/range_32k_256k/)
@@ -2069,7 +2073,8 @@ inline const char* ptrs_form_name(PtrsForm f) {
 // ptrs_large.log, ptrs_mid.log), then ~one block per CU over 16 KiB tiles.
 inline PtrsForm pick_ptrs(int64_t N, int64_t P) {
     switch (pick_f32(N, P)) {
-        case F32Pick::kLdsW2T16: return PtrsForm::kLdsW2T16Ring;  // with the pointer ring (LOPT 4)
+        case F32Pick::kLdsW2T16:  // with the pointer ring (LOPT 4)
+        case F32Pick::kLdsW2T16D4: return PtrsForm::kLdsW2T16Ring;
         case F32Pick::kLdsW2T16D2: return PtrsForm::kLdsW2T16D2;  // 1.2-1.6x over the 4-wave 32-quad table fold
                                                                   // at 32K-65K (profiles/r02_lds/ptrs_two_wave/)
         case F32Pick::kLdsW2T32: return PtrsForm::kLdsW2T32;
@@ -2161,8 +2166,8 @@ inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v
     const int64_t nq = P >> 2, cus = cu_count();
     const int64_t tiles4 = (((P + 3) >> 2) + 4 * kBlock - 1) / (4 * kBlock);
     if (nq < (1 << 16)) {  // narrow models: the LDS-staged forms, the 4 KiB tile
-        for (F32Pick p : {F32Pick::kLdsW2T16, F32Pick::kLdsW2T16D2, F32Pick::kLdsW2T32, F32Pick::kLdsW4T24,
-                          F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1})
+        for (F32Pick p : {F32Pick::kLdsW2T16, F32Pick::kLdsW2T16D4, F32Pick::kLdsW2T16D2, F32Pick::kLdsW2T32,
+                          F32Pick::kLdsW4T24, F32Pick::kLdsW4T40, F32Pick::kLdsW8, F32Pick::kLdsQfW4T32, F32Pick::kTileC1})
             add(p);
     } else if (tiles4 < 2 * cus) {  // under two 16 KiB tiles per CU: where the forms swing most
         for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBalC2, F32Pick::kTileC4Plain, F32Pick::kTileC4,
@@ -2195,6 +2200,10 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
             // 18.5 -> 16.6 us, 4096 x 16K 65.7 -> 56.3, stall-aware 1024 x 16K
             // 21.8 -> 18.7; profiles/r03_premul/)
             rc = launch_lds_flags<2, 32, 16, 6, true, false, true, 8>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                                      divisor, out);
+            break;
+        case F32Pick::kLdsW2T16D4:  // the same with four chunks in flight (16K-32K params)
+            rc = launch_lds_flags<2, 32, 16, 4, true, false, true, 8>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
                                                                       divisor, out);
             break;
         case F32Pick::kLdsW2T16D2:

@@ -83,9 +83,10 @@ _PICKS = [
     ((100, 1_500_000), "gs_bal_8k"),       # 1-2 tiles per CU
     ((1024, 582_026), "lds_w8_t32"),       # 256+ clients below 0.7
     ((10, 10_000_000), "tile_16k"),        # < 24 clients above one tile per CU
-    ((1024, 16_384), "lds_w2_t16"),        # < 32K params
+    ((1024, 16_384), "lds_w2_t16"),        # <= 16K params: six chunks in flight
+    ((1024, 16_388), "lds_w2_t16_d4"),     # 16K-32K params: four
     ((1024, 67_267), "lds_w4_t24"),        # 32K-80K: CU-fill tile
-    ((1024, 32_768), "lds_w2_t16"),
+    ((1024, 32_768), "lds_w2_t16_d4"),
     ((1024, 32_772), "lds_w4_t40"),
     ((1024, 65_536), "lds_w2_t16_d2"),
     ((256, 57_344), "lds_w2_t16_d2"),
