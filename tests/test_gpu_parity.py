@@ -213,6 +213,32 @@ def test_chunked_fold_equals_batch(dev, lib):
     assert _bits_equal(acc.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("P", [4096, 16384, 16388, 30000, 32768])
+@pytest.mark.parametrize("scored", [False, True])
+def test_chunked_narrow_pipelined_fold(dev, lib, P, scored):
+    """The narrowest picks (terms formed by the loaders, 4-6 chunks in flight)
+    in their accumulate / finalize forms: chunks long enough for the deep
+    pipeline (N = 700, 32-row chunks), acc carried, divide at the end."""
+    L = lib.load()
+    N = 700
+    X = torch.from_numpy(synth.clients_f32(37 + P, N, 0, P)).to(dev)
+    w = synth.cardinalities(37, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(37, N, 10, 2)]
+    a = torch.tensor(w, dtype=torch.float32, device=dev)
+    s = torch.tensor(sc, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    div = float(np.float32(sum(w)))
+    acc = _sentinel(P, dev)
+    bounds = [0, 1, 250, 251, 699, 700]
+    for k, (r0, r1) in enumerate(zip(bounds[:-1], bounds[1:])):
+        lib.check(L.fa_fold_f32(X[r0].data_ptr(), r1 - r0, P, P, a[r0:].data_ptr(),
+                                s[r0:].data_ptr() if scored else None,
+                                None if k == 0 else acc.data_ptr(), div, int(r1 == N), acc.data_ptr(), st), "fold")
+    exp = OL.fedavg_f32(X.cpu().numpy(), np.array(w, np.float32), np.float32(sum(w)),
+                        s=np.array(sc, np.float32) if scored else None)
+    assert _bits_equal(acc.cpu().numpy(), exp), (P, scored)
+
+
 def test_ptr_rows_equal_stacked(dev):
     from fedlesscan_amd import engine
     N, P = 23, 7001
