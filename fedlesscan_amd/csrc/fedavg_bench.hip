@@ -183,12 +183,14 @@ constexpr const char* kVariants[] = {
     // the product's LDS picks, two deeper forms, and the 4-byte-load pick
     "pm_lds4_w2r32t16", "pm_lds2_w2r32t16", "pm_lds2_w4r32t24", "pm_lds2_w4r32t40", "pm_lds2_w2r16t32",
     "pm_lds1_w8r64t32", "pm_lds4_w4r32t16", "pm_lds6_w2r32t16", "pm_dw_lds4_w2r32t16",
+    // more bytes in flight per block: deeper pipelines, 64-row chunks
+    "pm_lds8_w2r32t16", "pm_lds10_w2r32t16", "pm_lds4_w2r64t16", "pm_lds6_w2r64t16",
 };
 constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
 constexpr int kEndAnyAlign = 92;
 constexpr int kPmDw = 118;  // and this one
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-static_assert(kNumVariants == kPmDw + 1, "pm_dw_lds4_w2r32t16 is the last variant");
+static_assert(kNumVariants > kPmDw, "pm_dw_lds4_w2r32t16 is variant 118");
 
 // Quads per lane of the round-1 row-streaming policy (variant "v4_pickq_nts"):
 // the widest per-block row run (C * 4 KiB) that still leaves >= ~1000 blocks.
@@ -451,6 +453,10 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 116: rc = FA_VP(4, 32, 16, 4, false); break;
         case 117: rc = FA_VP(2, 32, 16, 6, false); break;
         case kPmDw: rc = FA_VP(2, 32, 16, 4, true); break;
+        case 119: rc = FA_VP(2, 32, 16, 8, false); break;
+        case 120: rc = FA_VP(2, 32, 16, 10, false); break;
+        case 121: rc = FA_VP(2, 64, 16, 4, false); break;
+        case 122: rc = FA_VP(2, 64, 16, 6, false); break;
 #undef FA_VP
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
