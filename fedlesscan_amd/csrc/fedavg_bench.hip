@@ -185,6 +185,8 @@ constexpr const char* kVariants[] = {
     "pm_lds1_w8r64t32", "pm_lds4_w4r32t16", "pm_lds6_w2r32t16", "pm_dw_lds4_w2r32t16",
     // more bytes in flight per block: deeper pipelines, 64-row chunks
     "pm_lds8_w2r32t16", "pm_lds10_w2r32t16", "pm_lds4_w2r64t16", "pm_lds6_w2r64t16",
+    // the same with a scheduling barrier after each stage's loads (LOPT 8|2: exact wait counts)
+    "pm_o2_lds6_w2r32t16", "pm_o2_lds4_w2r32t16", "pm_o2_lds4_w4r32t16", "pm_o2_lds8_w2r32t16",
 };
 constexpr int kFirstAnyAlign = 84;  // variants [kFirstAnyAlign, kEndAnyAlign) take any 4-B aligned layout
 constexpr int kEndAnyAlign = 92;
@@ -457,6 +459,13 @@ int fold_f32_variant(const float* X, int64_t N, int64_t P, int64_t ldx, const fl
         case 120: rc = FA_VP(2, 32, 16, 10, false); break;
         case 121: rc = FA_VP(2, 64, 16, 4, false); break;
         case 122: rc = FA_VP(2, 64, 16, 6, false); break;
+#define FA_VP2(NW, R, TQ, D) \
+    launch_lds_flags<NW, R, TQ, D, false, false, true, 10>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out)
+        case 123: rc = FA_VP2(2, 32, 16, 6); break;
+        case 124: rc = FA_VP2(2, 32, 16, 4); break;
+        case 125: rc = FA_VP2(4, 32, 16, 4); break;
+        case 126: rc = FA_VP2(2, 32, 16, 8); break;
+#undef FA_VP2
 #undef FA_VP
         default: return fail(FA_ERR_ARG, "unknown variant %d", variant);
     }
