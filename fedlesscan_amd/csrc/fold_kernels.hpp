@@ -2198,13 +2198,17 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
             // 7.8; profiles/r02_lds/sweep_small.log); round 3: the loaders form
             // the terms (LOPT bit 3) and six chunks are in flight (1024 x 16K
             // 18.5 -> 16.6 us, 4096 x 16K 65.7 -> 56.3, stall-aware 1024 x 16K
-            // 21.8 -> 18.7; profiles/r03_premul/)
-            rc = launch_lds_flags<2, 32, 16, 6, true, false, true, 8>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
-                                                                      divisor, out);
+            // 21.8 -> 18.7; profiles/r03_premul/), with a scheduling barrier
+            // after each stage's loads (LOPT bit 1): without it the compiler
+            // sinks the stall-aware form's factor loads and its stash waits
+            // drain the pipeline to 6 of 72 loads (exact waits: 4096 x 16K
+            // stall-aware 64.8 -> 59.7 us, plain within 1 %)
+            rc = launch_lds_flags<2, 32, 16, 6, true, false, true, 10>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                                       divisor, out);
             break;
         case F32Pick::kLdsW2T16D4:  // the same with four chunks in flight (16K-32K params)
-            rc = launch_lds_flags<2, 32, 16, 4, true, false, true, 8>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
-                                                                      divisor, out);
+            rc = launch_lds_flags<2, 32, 16, 4, true, false, true, 10>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
+                                                                       divisor, out);
             break;
         case F32Pick::kLdsW2T16D2:
             rc = launch_lds_flags<2, 32, 16, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
