@@ -224,6 +224,8 @@ constexpr const char* kPtrsVariants[] = {
     "ptrs_o0_w2t32", "ptrs_o4_w2t32", "ptrs_o0_w2t16d2", "ptrs_o4_w2t16d2",
     // the loaders form the terms (LOPT bit 3), with and without the pointer ring (round 3)
     "ptrs_o12_w2t16d4", "ptrs_o12_w2t16d6", "ptrs_o8_w2t16d6", "ptrs_o8_w2t16d4",
+    // with a scheduling barrier per stage (bit 1: exact stash waits)
+    "ptrs_o14_w2t16d6", "ptrs_o6_w2t16d4", "ptrs_o14_w2t16d4",
 };
 constexpr int kNumPtrsVariants = sizeof(kPtrsVariants) / sizeof(kPtrsVariants[0]);
 
@@ -648,6 +650,9 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P, con
         case 25: rc = FA_PW(2, 32, 16, 6, 12); break;
         case 26: rc = FA_PW(2, 32, 16, 6, 8); break;
         case 27: rc = FA_PW(2, 32, 16, 4, 8); break;
+        case 28: rc = FA_PW(2, 32, 16, 6, 14); break;
+        case 29: rc = FA_PW(2, 32, 16, 4, 6); break;
+        case 30: rc = FA_PW(2, 32, 16, 4, 14); break;
         default: return fail(FA_ERR_ARG, "unknown pointer variant %d", variant);
     }
 #undef FA_PV

@@ -23,6 +23,7 @@ ap.add_argument("--clients", type=int, default=1024)
 ap.add_argument("--params", type=int, default=1_000_000)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--variants", action="store_true", help="also time the tuning library's pointer variants")
+ap.add_argument("--scored", action="store_true", help="variants: the stall-aware fold (tolerance factors)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 N, P = args.clients, args.params
@@ -86,19 +87,23 @@ t_ord_kern = timed(lambda: _lib.check(xrows_fold(ord_tab.data_ptr(), N, P, a_dev
 var = {}
 if args.variants:
     B = _lib.load_bench()
+    sc = [(r + 1) / 11 for r in synth.round_ids(9, N, 10, 2)] if args.scored else None
+    s_dev = torch.tensor(sc, dtype=torch.float32, device=dev) if sc else None
+    s_ptr = s_dev.data_ptr() if sc else None
+    ref_v = engine.fold_stacked(X, w, sc).view(torch.int32)
     for v in range(B.fa_num_ptrs_variants()):
         name = B.fa_ptrs_variant_name(v).decode()
         o2 = torch.empty(P, dtype=torch.float32, device=dev)
-        fn = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), None, div,
+        fn = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ptr_tab.data_ptr(), N, P, a_dev.data_ptr(), s_ptr, div,
                                                              o2.data_ptr(), st, v), "ptrs variant", bench=True)
         var[name] = round(timed(fn), 4)
-        assert torch.equal(o2.view(torch.int32), engine.fold_stacked(X, w).view(torch.int32)), name
+        assert torch.equal(o2.view(torch.int32), ref_v), name
         if name.startswith(("ptrs_dw", "ptrs_rows_scalar", "ptrs_generic")):
             # the same rows through a table of X[i] (16-B aligned only when P % 4 == 0)
-            fu = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ord_tab.data_ptr(), N, P, a_dev.data_ptr(), None,
+            fu = lambda: _lib.check(B.fa_fedavg_f32_ptrs_variant(ord_tab.data_ptr(), N, P, a_dev.data_ptr(), s_ptr,
                                                                  div, o2.data_ptr(), st, v), "ptrs variant", bench=True)
             var[name + "@xrows"] = round(timed(fu), 4)
-            assert torch.equal(o2.view(torch.int32), engine.fold_stacked(X, w).view(torch.int32)), name
+            assert torch.equal(o2.view(torch.int32), ref_v), name
 same_shuf = torch.equal(engine.fold_rows(rs_shuf, w_shuf).view(torch.int32),
                         engine.fold_stacked(X[torch.from_numpy(perm).to(dev)], w_shuf).view(torch.int32))
 ref = engine.fold_stacked(X, w).view(torch.int32)
@@ -110,4 +115,5 @@ print(json.dumps({"clients": N, "params": P, "ptrs_ms": round(t_rows, 4), "ptrs_
                   "shuffled_kernel_ms": round(t_shuf_kern, 4), "inorder_table_kernel_ms": round(t_ord_kern, 4),
                   "ptrs_kernel_ms": round(t_kern, 4), "ptrs_kernel_GBps": round(gb / t_kern * 1e3, 1),
                   "stacked_ms": round(t_stack, 4), "stacked_GBps": round(gb / t_stack * 1e3, 1),
-                  "bit_identical": bool(same and same_shuf), **({"variants_kernel_ms": var} if var else {})}))
+                  "bit_identical": bool(same and same_shuf), "scored_variants": bool(args.scored),
+                  **({"variants_kernel_ms": var} if var else {})}))
