@@ -2108,9 +2108,10 @@ inline int launch_ptrs_form(PtrsForm f, hipStream_t st, const float* const* xi, 
     const bool sc = s != nullptr;
     const float* X = (const float*)xi;
     switch (f) {
-        case PtrsForm::kLdsW2T16Ring:
-            return launch_lds_flags<2, 32, 16, 4, false, true, true, 4>(st, sc, false, true, X, N, P, P, a, s, nullptr,
-                                                                        divisor, out);
+        case PtrsForm::kLdsW2T16Ring:  // + terms by the loaders, exact stash waits (LOPT 4|8|2; round 3:
+            // 1024 x 16K-30K stall-aware 11-14 % faster, plain 1-7 %, profiles/r03_premul/ptrs_exact.log)
+            return launch_lds_flags<2, 32, 16, 4, false, true, true, 14>(st, sc, false, true, X, N, P, P, a, s, nullptr,
+                                                                         divisor, out);
         case PtrsForm::kLdsW2T16D2:
             return launch_lds_flags<2, 32, 16, 2, false, true>(st, sc, false, true, X, N, P, P, a, s, nullptr, divisor,
                                                                out);
