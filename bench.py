@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--splitn", action="store_true",
                     help="time the opt-in split-client fold (fa_fedavg_f32_splitn, NOT bit-exact) instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-lean", action="store_true",
+                    help="skip the full-size one-core reference timing (cpu_baseline.full_lean)")
     ap.add_argument("--unpadded", action="store_true",
                     help="row pitch = the model size exactly (experiments: odd sizes give rows that are not 16-B "
                          "aligned, as a torch.stack of such a model)")
@@ -323,6 +325,36 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
     }
 
 
+def cpu_full_lean(wl: Workload):
+    """The reference algorithm over the WHOLE workload on one core (SURVEY 8(d):
+    "time the lean form at full size"): the inputs copied from HBM to host
+    memory (not timed), then oracle.fedavg_stacked -- the op order of
+    fed_avg_aggregator.py:31-41 / stall_aware_aggregation.py:55-66 with one
+    product temporary instead of N (np.multiply into a [P] buffer, np.add into
+    the running sum, one true_divide; bit-identical to the literal form) --
+    and every output column compared with the GPU's.  fp32 workloads at one
+    rank's single slot only (N = 1 GPU, rounds = 1)."""
+    from oracle import fedavg_oracle as O  # CPU baseline / checker only
+    if wl.dtype != "f32" or len(wl.slots) != 1:
+        return None
+    t0 = time.perf_counter()
+    Xh = torch.empty((wl.N, wl.ldx), dtype=torch.float32)
+    Xh.copy_(wl.X)
+    d2h_s = time.perf_counter() - t0
+    Xn = Xh.numpy()[:, :wl.P]
+    t0 = time.perf_counter()
+    ref = O.fedavg_stacked(Xn, wl.weights, wl.scores)
+    t = time.perf_counter() - t0
+    exact = bool(np.array_equal(ref.view(np.uint32), wl.out[:wl.P].cpu().numpy().view(np.uint32)))
+    nbytes = wl.N * wl.P * 4 + wl.P * 4
+    del Xh, Xn
+    return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "seconds": round(t, 2), "bytes": nbytes,
+            "cores": 1, "kind": "port",
+            "impl": "oracle.fedavg_stacked: the reference op order over the full workload with one [P] product "
+                    "temporary (numpy ufuncs, single-threaded)",
+            "d2h_s": round(d2h_s, 2), "bit_exact_vs_gpu_all_columns": exact}
+
+
 def read_traffic(config: str):
     """PMC HBM bytes per launch from the committed rocprofv3 --pmc passes
     (profiles/pmc_<config>.json, written by scripts/profile_c3.sh): counters
@@ -533,6 +565,11 @@ def main():
             cpu = cpu_baseline(wl, args.cpu_cols, args.cpu_reps)
         except Exception as e:  # the baseline must never hide the GPU result
             cpu = {"error": repr(e)}
+        if world == 1 and not args.no_full_lean:
+            try:
+                cpu["full_lean"] = cpu_full_lean(wl)
+            except Exception as e:
+                cpu["full_lean"] = {"error": repr(e)}
     if dist_on:
         dist.barrier()
     if rank == 0:

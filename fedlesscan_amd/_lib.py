@@ -27,9 +27,10 @@ BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
 HOSTFAST_PATH = os.path.join(PKG, "_native", "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FA_OK, FA_ERR_ARG, FA_ERR_NO_CLIENTS, FA_ERR_SHAPE, FA_ERR_HIP = range(5)
+FA_HINT_SHARED = 1  # fa_fedavg_*_ex: other kernels share the GPU during the fold
 
 _i64 = ctypes.c_int64
 _vp = ctypes.c_void_p
@@ -52,6 +53,14 @@ _PROTOS = {
     "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),
     "fa_finalize_f32": (_int, [_vp, _f32, _vp, _i64, _vp]),
     "fa_fedavg_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
+    "fa_fedavg_f32_ex": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp]),
+    "fa_fedavg_bf16_ex": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp]),
+    "fa_rounds_create": (_int, [_vp, _int]),
+    "fa_rounds_destroy": (_int, [_vp]),
+    "fa_fedavg_f32_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
+    "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
+    "fa_rounds_wait": (_int, [_vp, _int, _vp]),
+    "fa_rounds_timeouts": (_int, [_vp]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i64": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
@@ -68,6 +77,9 @@ _PROTOS = {
     "fa_set_autotune": (_int, [_int]),
     "fa_autotune_pending": (_int, []),
     "fa_fold_form": (ctypes.c_char_p, [_int, _i64, _i64, _i64, _int, _vp]),
+    "fa_tune_cache_path": (_int, [ctypes.c_char_p]),
+    "fa_tune_export": (_i64, [_vp, _i64]),
+    "fa_tune_import": (_int, [ctypes.c_char_p]),
     "fa_ingest_create": (_int, [_vp, _i64, _i64, _int, _int]),
     "fa_ingest_rows_per_chunk": (_int, [_vp]),
     "fa_ingest_begin": (_int, [_vp, _vp, _vp, _i64]),
@@ -102,6 +114,12 @@ _BENCH_PROTOS = {
     "fa_num_bf16_variants": (_int, []),
     "fa_bf16_variant_name": (ctypes.c_char_p, [_int]),
     "fa_fedavg_f32_ptrs_variant": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int]),
+    "fa_num_step_forms": (_int, []),
+    "fa_step_form_name": (ctypes.c_char_p, [_int]),
+    "fa_bench_rounds_create": (_int, [_vp, _int]),
+    "fa_bench_rounds_destroy": (_int, [_vp]),
+    "fa_fedavg_rounds_form": (_int, [_vp, _int, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
+    "fa_bench_rounds_wait": (_int, [_vp, _int, _vp]),
     "fa_num_ptrs_variants": (_int, []),
     "fa_ptrs_variant_name": (ctypes.c_char_p, [_int]),
 }
@@ -172,6 +190,23 @@ def check(rc: int, what: str, bench: bool = False) -> None:
     if rc == FA_ERR_ARG:
         raise ValueError(msg)
     raise AggregationError(msg)
+
+
+def tune_export() -> str:
+    """This process's measured form choices, as tuner cache-file lines."""
+    L = load()
+    n = L.fa_tune_export(None, 0)
+    buf = ctypes.create_string_buffer(int(n) + 1)
+    L.fa_tune_export(buf, n + 1)
+    return buf.value.decode()
+
+
+def tune_import(text: str) -> int:
+    """Apply tuner cache-file lines (e.g. rank 0's choices); returns how many applied."""
+    n = load().fa_tune_import(text.encode())
+    if n < 0:
+        check(n, "fa_tune_import")
+    return int(n)
 
 
 def call(name: str, *args) -> None:

@@ -213,6 +213,99 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const f
     return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
 }
 
+int fa_fedavg_f32_ex(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                     float divisor, float* out, int hints, void* stream) {
+    if (hints & ~FA_HINT_SHARED) return fail(FA_ERR_ARG, "unknown fold hints 0x%x", hints);
+    return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream, hints);
+}
+
+int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
+                      float divisor, float* out_f32, uint16_t* out_bf16, int hints, void* stream) {
+    if (hints & ~FA_HINT_SHARED) return fail(FA_ERR_ARG, "unknown fold hints 0x%x", hints);
+    return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream, hints);
+}
+
+// ---- one launch per exchange step -------------------------------------------
+struct fa_rounds : RoundsState {};
+
+int fa_rounds_create(fa_rounds** r, int device) {
+    if (!r) return fail(FA_ERR_ARG, "fa_rounds_create: null handle");
+    *r = nullptr;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_ERR_ARG, "fa_rounds_create: no device %d", device);
+    }
+    fa_rounds* o = new fa_rounds();
+    o->device = device;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    o->max_ticks = (long long)khz * 1000LL * 10LL;  // a waiter gives up after ~10 s
+    hipError_t e = hipMalloc((void**)&o->sig, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipMemset(o->sig, 0, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        if (o->sig) (void)hipFree(o->sig);
+        delete o;
+        return fail(FA_ERR_HIP, "fa_rounds_create: %s", hipGetErrorString(e));
+    }
+    *r = o;
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+int fa_rounds_destroy(fa_rounds* r) {
+    if (!r) return FA_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(r->device);
+    (void)hipDeviceSynchronize();  // no launch or waiter may still use the words
+    (void)hipFree(r->sig);
+    (void)hipSetDevice(prev);
+    delete r;
+    return FA_OK;
+}
+
+int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx, const float* a, const float* s,
+                          float divisor, float* out_f32, uint16_t* out_bf16, int rounds, const int64_t* offsets,
+                          void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
+    StreamDevice on_stream_device(stream);
+    return launch_step(*r, pick_step(true), (hipStream_t)stream, X, N, ldx, a, s, divisor, out_f32, out_bf16,
+                       rounds, offsets);
+}
+
+int fa_fedavg_f32_rounds(fa_rounds* r, const float* X, int64_t N, int64_t ldx, const float* a, const float* s,
+                         float divisor, float* out, int rounds, const int64_t* offsets, void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
+    StreamDevice on_stream_device(stream);
+    return launch_step(*r, pick_step(false), (hipStream_t)stream, X, N, ldx, a, s, divisor, out, nullptr, rounds,
+                       offsets);
+}
+
+int fa_rounds_wait(fa_rounds* r, int round, void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
+    if (!r->launched) return fail(FA_ERR_ARG, "fa_rounds_wait: the last rounds fold was not launched");
+    if (round < 0 || round >= r->rounds) return fail(FA_ERR_ARG, "fa_rounds_wait: round %d of %d", round, r->rounds);
+    StreamDevice on_stream_device(stream);
+    hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, (hipStream_t)stream, r->sig + kSigFlag + round, r->epoch,
+                       r->sig + kSigTimeout, r->max_ticks);
+    return check_launch("k_wait_round");
+}
+
+int fa_rounds_timeouts(fa_rounds* r) {
+    if (!r) return -fail(FA_ERR_ARG, "null fa_rounds");
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(r->device);
+    unsigned int v = 0;
+    const hipError_t e = hipMemcpy(&v, r->sig + kSigTimeout, sizeof(v), hipMemcpyDeviceToHost);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return -fail(FA_ERR_HIP, "fa_rounds_timeouts: %s", hipGetErrorString(e));
+    return (int)v;
+}
+
 int fa_set_autotune(int mode) { return g_tuner.set_mode(mode); }
 int fa_autotune_pending(void) { return g_tuner.pending(); }
 
@@ -224,11 +317,33 @@ const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored
         (void)hipGetLastError();
         return "";
     }
-    const int tuned = g_tuner.set_mode(-1) ? g_tuner.chosen(dev, kind, N, P, ldx, scored != 0) : -2;
+    const int policy = kind == FA_FOLD_F32 ? (int)pick_f32(N, P)
+                       : kind == FA_FOLD_F32_ROWS ? (int)pick_ptrs(N, P) : (int)pick_bf16(N, P);
+    const int tuned = g_tuner.set_mode(-1) ? g_tuner.chosen(dev, kind, N, policy, P, ldx, scored != 0) : -2;
     if (tuned == -1) return "";
-    if (kind == FA_FOLD_F32) return f32_pick_name(tuned >= 0 ? (F32Pick)tuned : pick_f32(N, P));
-    if (kind == FA_FOLD_F32_ROWS) return ptrs_form_name(tuned >= 0 ? (PtrsForm)tuned : pick_ptrs(N, P));
-    return bf16_form_name(tuned >= 0 ? (Bf16Form)tuned : pick_bf16(N, P));
+    return tune_form_name(kind, tuned >= 0 ? tuned : policy);
+}
+
+int fa_tune_cache_path(const char* path) {
+    g_tuner.set_cache_path(path ? std::string(path) : std::string());
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+int64_t fa_tune_export(char* buf, int64_t cap) {
+    const std::string t = g_tuner.export_text();
+    if (buf && cap > 0) {
+        const size_t n = t.size() < (size_t)(cap - 1) ? t.size() : (size_t)(cap - 1);
+        memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return (int64_t)t.size();
+}
+
+int fa_tune_import(const char* text) {
+    if (!text) return fail(FA_ERR_ARG, "fa_tune_import: null text");
+    g_err[0] = 0;
+    return g_tuner.import_text(std::string(text));
 }
 
 int fa_fedavg_f64(const double* X, int64_t N, int64_t P, int64_t ldx, const double* a, const double* s,

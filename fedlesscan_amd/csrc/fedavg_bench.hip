@@ -524,6 +524,70 @@ int fa_fedavg_f32_ptrs_form(const float* const* xi, int64_t N, int64_t P, const 
     if (rc) return rc;
     return check_launch("fa_fedavg_f32_ptrs_form");
 }
+int fa_num_step_forms(void) { return kNumStepForms; }
+const char* fa_step_form_name(int form) {
+    return (form >= 0 && form < kNumStepForms) ? step_form_name((StepForm)form) : "";
+}
+
+int fa_bench_rounds_create(void** r, int device) {
+    if (!r) return fail(FA_ERR_ARG, "null handle");
+    *r = nullptr;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_ERR_ARG, "no device %d", device);
+    }
+    RoundsState* o = new RoundsState();
+    o->device = device;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    o->max_ticks = (long long)khz * 1000LL * 10LL;
+    hipError_t e = hipMalloc((void**)&o->sig, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipMemset(o->sig, 0, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        if (o->sig) (void)hipFree(o->sig);
+        delete o;
+        return fail(FA_ERR_HIP, "rounds state: %s", hipGetErrorString(e));
+    }
+    *r = o;
+    return FA_OK;
+}
+
+int fa_bench_rounds_destroy(void* r) {
+    RoundsState* o = static_cast<RoundsState*>(r);
+    if (!o) return FA_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(o->device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(o->sig);
+    (void)hipSetDevice(prev);
+    delete o;
+    return FA_OK;
+}
+
+int fa_fedavg_rounds_form(void* r, int form, const void* X, int64_t N, int64_t ldx, const float* a, const float* s,
+                          float divisor, float* out, uint16_t* out_bf16, int rounds, const int64_t* offsets,
+                          void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null rounds state");
+    if (form < 0 || form >= kNumStepForms) return fail(FA_ERR_ARG, "unknown step form %d", form);
+    StreamDevice on_stream_device(stream);
+    const StepForm f = (StepForm)form;
+    return launch_step(*static_cast<RoundsState*>(r), f, (hipStream_t)stream, X, N, ldx, a, s, divisor, out,
+                       step_form_bf16(f) ? out_bf16 : nullptr, rounds, offsets);
+}
+
+int fa_bench_rounds_wait(void* r, int round, void* stream) {
+    RoundsState* o = static_cast<RoundsState*>(r);
+    if (!o || !o->launched || round < 0 || round >= o->rounds) return fail(FA_ERR_ARG, "bad rounds wait");
+    StreamDevice on_stream_device(stream);
+    hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, (hipStream_t)stream, o->sig + kSigFlag + round, o->epoch,
+                       o->sig + kSigTimeout, o->max_ticks);
+    return check_launch("k_wait_round");
+}
+
 int fa_num_bf16_forms(void) { return kNumBf16Forms; }
 const char* fa_bf16_form_name(int form) {
     return (form >= 0 && form < kNumBf16Forms) ? bf16_form_name((Bf16Form)form) : "";

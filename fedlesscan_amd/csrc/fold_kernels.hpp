@@ -40,6 +40,7 @@
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -1362,7 +1363,7 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
     odd = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
 }
 
-template <int U, int C, bool SCORED>
+template <int U, int C, bool SCORED, int B = kBlock>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -1373,7 +1374,7 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             f32x4 e, o;
-            unpack_bf16x8(__builtin_nontemporal_load(p + c * kBlock), e, o);
+            unpack_bf16x8(__builtin_nontemporal_load(p + c * B), e, o);
             ev[c] = term4<SCORED>(e, a0, s0);
             od[c] = term4<SCORED>(o, a0, s0);
         }
@@ -1384,7 +1385,9 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * kBlock);
+            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * B);
+        // deep unrolls: every load of the group issued before the first add
+        if constexpr (U >= 16) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
@@ -1402,7 +1405,7 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             f32x4 e, o;
-            unpack_bf16x8(__builtin_nontemporal_load(p + i * ldo + c * kBlock), e, o);
+            unpack_bf16x8(__builtin_nontemporal_load(p + i * ldo + c * B), e, o);
             ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
             od[c] = add4(od[c], term4<SCORED>(o, ai, si));
         }
@@ -1410,7 +1413,7 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
-        const int64_t oc = o0 + (int64_t)c * kBlock;
+        const int64_t oc = o0 + (int64_t)c * B;
         f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
         __builtin_nontemporal_store(f32x4{e.x, o.x, e.y, o.y}, o4);
         __builtin_nontemporal_store(f32x4{e.z, o.z, e.w, o.w}, o4 + 1);
@@ -1427,24 +1430,24 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
-template <int U, int C, bool SCORED>
+template <int U, int C, bool SCORED, int B = kBlock>
 __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
     const int64_t no = P >> 3;  // full octets
     const int64_t ldo = ldx >> 3;
-    const int64_t o0 = bid * (kBlock * C) + threadIdx.x;
+    const int64_t o0 = bid * (B * C) + threadIdx.x;
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
-    if (o0 + (int64_t)(C - 1) * kBlock < no) {
-        fold_octets<U, C, SCORED>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+    if (o0 + (int64_t)(C - 1) * B < no) {
+        fold_octets<U, C, SCORED, B>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        const int64_t o = o0 + (int64_t)c * kBlock;
-        if (o < no) fold_octets<U, 1, SCORED>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+        const int64_t o = o0 + (int64_t)c * B;
+        if (o < no) fold_octets<U, 1, SCORED, B>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
-    const int64_t tb = no / (kBlock * C), tl = (no % (kBlock * C)) % kBlock;
+    const int64_t tb = no / (B * C), tl = (no % (B * C)) % B;
     if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
         for (int64_t col = no * 8; col < P; ++col) {
             float acc = term1<SCORED>(bf2f(X[col]), a[0], SCORED ? s[0] : 1.0f);
@@ -1473,6 +1476,174 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_gs(
     float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles) {
     for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
         bf16_tile<U, C, SCORED>(bid, X, N, P, ldx, a, s, divisor, out, outb);
+}
+
+// ---------------------------------------------------------------------------
+// Dynamic tiles with the next tile fetched a whole tile ahead (round 4).
+// When another kernel shares some CUs -- at N > 1 the all-gather of round k
+// runs beside the fold of round k+1 -- the fold blocks on those CUs run
+// slower, and a static tile assignment (the balanced grid-stride / band forms)
+// makes the whole launch wait for them: one rank's C4 step went from 0.96 to
+// 1.11-1.17 ms beside a copy kernel on 16-64 blocks
+// (profiles/r03_exchange_proxy/).  Here ~one block per CU takes tiles from a
+// device counter, so a slowed block folds fewer of them.  What that leaves is
+// up to one tile of tail per launch, and a tile's time is (rows / U) x the
+// load latency, independent of its width at a fixed number of bytes in flight
+// per CU: deep row pipelines (U = 16-32 rows ahead) over narrow tiles (one
+// octet or quad per lane, 64-256 lanes) keep it at ~10-40 us for 256 rows.
+// The fetch is issued by lane 0 of the block before the tile's loads and
+// its result is read only after the tile's fold (its latency hides under the
+// tile); the shared index slot alternates between two words, so a write can
+// never race the previous tile's reads.  The first tile is blockIdx.x, and the
+// counter hands out the tiles from gridDim.x on.  ctr = {next, blocks done}:
+// the last block to finish zeroes both for the next launch on the slot.  Every
+// tile runs the same in-order per-lane fold as the static forms: same bits.
+// ---------------------------------------------------------------------------
+template <class Tile>
+__device__ __forceinline__ void dyn_tiles(int64_t ntiles, unsigned int* ctr, Tile tile) {
+    __shared__ unsigned int nxt[2];
+    int64_t bid = blockIdx.x;
+    int p = 0;
+    while (bid < ntiles) {
+        unsigned int nx = 0;
+        if (threadIdx.x == 0) nx = atomicAdd(&ctr[0], 1u);
+        tile(bid);
+        if (threadIdx.x == 0) nxt[p] = nx;
+        __syncthreads();
+        bid = (int64_t)nxt[p] + gridDim.x;
+        p ^= 1;
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
+            atomicExch(&ctr[0], 0u);
+            atomicExch(&ctr[1], 0u);
+        }
+    }
+}
+
+template <int U, int C, bool SCORED, int B>
+__global__ __launch_bounds__(B) void k_fedavg_bf16_dyn(
+    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles, unsigned int* ctr) {
+    dyn_tiles(ntiles, ctr, [&](int64_t bid) { bf16_tile<U, C, SCORED, B>(bid, X, N, P, ldx, a, s, divisor, out, outb); });
+}
+
+// fp32 one-shot fold (no accumulator in, divide at the end) on the same schedule
+template <int U, int C, bool SCORED, int B>
+__global__ __launch_bounds__(B) void k_fold_f32_dynp(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
+    const float* __restrict__ a, const float* __restrict__ s, float divisor,
+    float* __restrict__ out, int64_t ntiles, unsigned int* ctr) {
+    dyn_tiles(ntiles, ctr, [&](int64_t bid) {
+        fold_tile<U, C, true, SCORED, false, true, true, B>(bid, X, N, P, ldx, a, s, nullptr, divisor, out);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// One launch per exchange step (round 4, fa_fedavg_*_rounds).  Per-round
+// dynamic launches pay a tile-time of tail per round (the last tiles of a
+// round run on a few blocks while the others idle; measured: 256 x the C4
+// rank's slots, 1.12 ms per step with 8 KiB dynamic tiles against 0.96 static,
+// profiles/r04_dyn/), and the overlapped exchange needs the rounds' results in
+// order, not each round's fold in its own kernel.  So one launch folds every
+// round's slot, taking the tiles of round 0, then round 1, ... from one
+// counter: a round's last tiles overlap the next round's first ones (no tail
+// until the step's end), slowed blocks fold fewer tiles, and when a round's
+// last tile is done the block that finished it raises the round's flag to
+// the launch's epoch.  The exchange of round k is issued behind
+// k_wait_round on another stream (a one-lane kernel that polls the flag and
+// returns), so it starts mid-launch, as soon as round k is complete.
+//   Ordering: every thread releases its tile's stores (device-scope fence)
+//   before the block counts the tile; the block that counts a round's last
+//   tile fences again (acquire of the other blocks' counts, release of the
+//   flag) before it stores the epoch; the waiter loads the flag with acquire.
+//   A waiter gives up after `max_ticks` of the device wall clock (never an
+//   endless spin), recording the timeout in the signal words.
+// ---------------------------------------------------------------------------
+constexpr int kMaxRounds = 8;
+struct RoundTable {
+    int64_t tile_end[kMaxRounds];  // round k's tiles are [tile_end[k-1], tile_end[k]) of the launch
+    int64_t col0[kMaxRounds];      // its first local column
+    int64_t width[kMaxRounds];     // its columns
+    int rounds;
+};
+// signal words: [0] next tile, [1] blocks done, [2, 2+R) tiles done per round,
+// [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
+constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
+
+template <class Tile>
+__device__ __forceinline__ void step_tiles(const RoundTable& R, unsigned int* sig, unsigned int epoch, Tile tile) {
+    __shared__ unsigned int nxt[2];
+    const int64_t ntiles = R.tile_end[R.rounds - 1];
+    int64_t t = blockIdx.x;
+    int p = 0;
+    while (t < ntiles) {
+        unsigned int nx = 0;
+        if (threadIdx.x == 0) nx = atomicAdd(&sig[0], 1u);
+        int k = 0;
+        while (k + 1 < R.rounds && t >= R.tile_end[k]) ++k;
+        const int64_t t0 = k ? R.tile_end[k - 1] : 0;
+        tile(k, t - t0);
+        __threadfence();  // this thread's stores of the tile, device-wide
+        if (threadIdx.x == 0) nxt[p] = nx;
+        __syncthreads();  // every thread's stores released before the block counts the tile
+        if (threadIdx.x == 0) {
+            const unsigned int nk = (unsigned int)(R.tile_end[k] - t0);
+            if (atomicAdd(&sig[kSigDone + k], 1u) == nk - 1) {  // the round's last tile
+                atomicExch(&sig[kSigDone + k], 0u);
+                __threadfence();
+                atomicExch(&sig[kSigFlag + k], epoch);
+            }
+        }
+        t = (int64_t)nxt[p] + gridDim.x;
+        p ^= 1;
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {
+            atomicExch(&sig[0], 0u);
+            atomicExch(&sig[1], 0u);
+        }
+    }
+}
+
+template <int U, int C, bool SCORED, int B>
+__global__ __launch_bounds__(B) void k_fedavg_bf16_step(
+    const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
+    const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, RoundTable R,
+    unsigned int* sig, unsigned int epoch) {
+    step_tiles(R, sig, epoch, [&](int k, int64_t bid) {
+        const int64_t c0 = R.col0[k];
+        bf16_tile<U, C, SCORED, B>(bid, X + c0, N, R.width[k], ldx, a, s, divisor, out + c0, outb ? outb + c0 : nullptr);
+    });
+}
+
+template <int U, int C, bool SCORED, int B>
+__global__ __launch_bounds__(B) void k_fold_f32_step(
+    const float* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
+    float divisor, float* __restrict__ out, RoundTable R, unsigned int* sig, unsigned int epoch) {
+    step_tiles(R, sig, epoch, [&](int k, int64_t bid) {
+        const int64_t c0 = R.col0[k];
+        fold_tile<U, C, true, SCORED, false, true, true, B>(bid, X + c0, N, R.width[k], ldx, a, s, nullptr, divisor,
+                                                           out + c0);
+    });
+}
+
+// Poll round flag `flag` until it reaches `epoch` (wrapping compare), then
+// return: the kernel a stream runs before an exchange that needs the round.
+__global__ __launch_bounds__(64) void k_wait_round(const unsigned int* flag, unsigned int epoch, unsigned int* timeouts,
+                                                   long long max_ticks) {
+    if (threadIdx.x != 0) return;
+    const long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0) {
+        if (wall_clock64() - t0 > max_ticks) {
+            atomicAdd(timeouts, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
 }
 
 template <bool SCORED>
@@ -1692,8 +1863,10 @@ inline unsigned int* dyn_slot(hipStream_t st) {
 enum class F32Pick { kLdsW2T16, kLdsW2T16D4, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
-                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kDynC4, kDynC2 };
-constexpr int kNumF32Picks = (int)F32Pick::kDynC2 + 1;
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kDynC4, kDynC2,
+                     // dynamic tiles fetched a tile ahead (round 4): the forms for folds that share the CUs
+                     kDynpU32C1B128, kDynpU16C1B256, kDynpU32C1B64, kDynpU16C2B256, kDynpU32C1B256 };
+constexpr int kNumF32Picks = (int)F32Pick::kDynpU32C1B256 + 1;
 inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
@@ -1717,13 +1890,21 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
         case F32Pick::kDynC4: return "dyn_16k";
         case F32Pick::kDynC2: return "dyn_8k";
+        case F32Pick::kDynpU32C1B128: return "dynp_u32c1b128";
+        case F32Pick::kDynpU16C1B256: return "dynp_u16c1b256";
+        case F32Pick::kDynpU32C1B64: return "dynp_u32c1b64";
+        case F32Pick::kDynpU16C2B256: return "dynp_u16c2b256";
+        case F32Pick::kDynpU32C1B256: return "dynp_u32c1b256";
     }
     return "";
 }
 // bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
 enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
-                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
-constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4,
+                      // dynamic tiles fetched a tile ahead (round 4): folds that share the CUs
+                      kDynU32C1B128, kDynU16C1B256, kDynU32C1B64, kDynU16C2B128, kDynU8C2B256, kDynU32C1B256 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kDynU32C1B256 + 1;
+inline bool bf16_dyn_form(Bf16Form f) { return (int)f >= (int)Bf16Form::kDynU32C1B128; }
 inline const char* bf16_form_name(Bf16Form f) {
     switch (f) {
         case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
@@ -1737,6 +1918,12 @@ inline const char* bf16_form_name(Bf16Form f) {
         case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
         case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
         case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
+        case Bf16Form::kDynU32C1B128: return "bf16_dyn_u32c1b128";
+        case Bf16Form::kDynU16C1B256: return "bf16_dyn_u16c1b256";
+        case Bf16Form::kDynU32C1B64: return "bf16_dyn_u32c1b64";
+        case Bf16Form::kDynU16C2B128: return "bf16_dyn_u16c2b128";
+        case Bf16Form::kDynU8C2B256: return "bf16_dyn_u8c2b256";
+        case Bf16Form::kDynU32C1B256: return "bf16_dyn_u32c1b256";
     }
     return "";
 }
@@ -2046,6 +2233,158 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
     }
 }
 
+// Dynamic tiles fetched a tile ahead (k_fedavg_bf16_dyn / k_fold_f32_dynp):
+// per_cu blocks per CU, B threads, C octets (quads) per lane, U rows ahead.
+// Without a counter slot (graph capture, no device memory) the static
+// balanced band form runs instead: same bits.
+template <int U, int C, int B>
+void launch_bf16_dyn(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                     const float* a, const float* s, float d, float* out, uint16_t* outb) {
+    const int64_t per_block = (int64_t)B * C, units = (P >> 3) + ((P & 7) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
+    if (!ctr) {
+        launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, d, out, outb);
+        return;
+    }
+    int64_t g = (int64_t)per_cu * cu_count();
+    if (g > tiles) g = tiles;
+    if (s)
+        hipLaunchKernelGGL((k_fedavg_bf16_dyn<U, C, true, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a, s,
+                           d, out, outb, tiles, ctr);
+    else
+        hipLaunchKernelGGL((k_fedavg_bf16_dyn<U, C, false, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a,
+                           s, d, out, outb, tiles, ctr);
+}
+
+template <int U, int C, int B>
+void launch_f32_dynp(hipStream_t st, int per_cu, bool sc, const float* X, int64_t N, int64_t P, int64_t ldx,
+                     const float* a, const float* s, float d, float* out) {
+    const int64_t per_block = (int64_t)B * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
+    const int64_t tiles = (units + per_block - 1) / per_block;
+    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
+    if (!ctr) {
+        launch_gs_bands<8, 4, true>(st, 3, sc, false, true, X, N, P, ldx, a, s, nullptr, d, out);
+        return;
+    }
+    int64_t g = (int64_t)per_cu * cu_count();
+    if (g > tiles) g = tiles;
+    if (sc)
+        hipLaunchKernelGGL((k_fold_f32_dynp<U, C, true, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a, s,
+                           d, out, tiles, ctr);
+    else
+        hipLaunchKernelGGL((k_fold_f32_dynp<U, C, false, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a,
+                           s, d, out, tiles, ctr);
+}
+
+// ---- one launch per exchange step (k_*_step, fa_fedavg_*_rounds) ---------
+// The step forms: rows ahead x octets (quads) per lane, 256-thread blocks,
+// one block per CU.
+enum class StepForm { kBf16U8C2, kBf16U16C2, kBf16U8C4, kBf16U4C4, kF32U8C4, kF32U8C2, kF32U16C2, kF32U16C1 };
+constexpr int kNumStepForms = (int)StepForm::kF32U16C1 + 1;
+inline const char* step_form_name(StepForm f) {
+    switch (f) {
+        case StepForm::kBf16U8C2: return "bf16_step_u8c2";
+        case StepForm::kBf16U16C2: return "bf16_step_u16c2";
+        case StepForm::kBf16U8C4: return "bf16_step_u8c4";
+        case StepForm::kBf16U4C4: return "bf16_step_u4c4";
+        case StepForm::kF32U8C4: return "f32_step_u8c4";
+        case StepForm::kF32U8C2: return "f32_step_u8c2";
+        case StepForm::kF32U16C2: return "f32_step_u16c2";
+        case StepForm::kF32U16C1: return "f32_step_u16c1";
+    }
+    return "";
+}
+inline bool step_form_bf16(StepForm f) { return (int)f <= (int)StepForm::kBf16U4C4; }
+inline int step_form_lanes_units(StepForm f) {  // column units (octets / quads) per tile
+    switch (f) {
+        case StepForm::kBf16U8C2: case StepForm::kBf16U16C2: case StepForm::kF32U8C2: case StepForm::kF32U16C2:
+            return kBlock * 2;
+        case StepForm::kBf16U8C4: case StepForm::kBf16U4C4: case StepForm::kF32U8C4: return kBlock * 4;
+        case StepForm::kF32U16C1: return kBlock;
+    }
+    return kBlock;
+}
+// The policy's step form (profiles/r04_dyn/): bf16 C4 rank slots, fp32 C3 rank slots.
+inline StepForm pick_step(bool bf16) { return bf16 ? StepForm::kBf16U8C2 : StepForm::kF32U8C4; }
+
+// The per-launch state of fa_fedavg_*_rounds: the signal words in device
+// memory and the host epoch (fa_rounds in fedavg_hip.h).
+struct RoundsState {
+    int device = 0;
+    unsigned int* sig = nullptr;  // kSigWords, zeroed at creation
+    unsigned int epoch = 0;       // of the last launch (0: none yet)
+    int rounds = 0;               // of the last launch
+    bool launched = false;        // the last launch was enqueued
+    long long max_ticks = 0;      // a waiter's give-up time in wall-clock ticks
+};
+
+// Enqueue one step launch: rounds slots at local columns [offsets[k], offsets[k+1]).
+inline int launch_step(RoundsState& R, StepForm f, hipStream_t st, const void* X, int64_t N, int64_t ldx,
+                       const float* a, const float* s, float divisor, float* out, uint16_t* outb, int rounds,
+                       const int64_t* offsets) {
+    R.launched = false;
+    if (rounds < 1 || rounds > kMaxRounds || !offsets) return fail(FA_ERR_ARG, "rounds must be 1..%d", kMaxRounds);
+    const bool bf = step_form_bf16(f);
+    const int64_t col_align = bf ? 8 : 4;
+    if (!X || !a || !out || N < 1) return fail(FA_ERR_ARG, "null X/a/out or N < 1");
+    if (ldx % col_align || !aligned16(X) || !aligned16(out) || (outb && !aligned16(outb)))
+        return fail(FA_ERR_ARG, "rounds fold needs 16-B aligned X/out and ldx %% %lld == 0", (long long)col_align);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return fail(FA_ERR_ARG, "rounds fold cannot be captured (its epochs would replay)");
+    }
+    RoundTable T{};
+    T.rounds = rounds;
+    const int64_t per_tile = step_form_lanes_units(f);
+    int64_t total = 0;
+    for (int k = 0; k < rounds; ++k) {
+        const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
+        if (c0 < 0 || w < 1 || c0 % col_align || offsets[k + 1] > ldx)
+            return fail(FA_ERR_ARG, "round %d: columns [%lld, %lld) (every round non-empty, %lld-aligned, within ldx)",
+                        k, (long long)c0, (long long)offsets[k + 1], (long long)col_align);
+        const int64_t units = bf ? (w >> 3) + ((w & 7) ? 1 : 0) : (w >> 2) + ((w & 3) ? 1 : 0);
+        total += (units + per_tile - 1) / per_tile;
+        T.tile_end[k] = total;
+        T.col0[k] = c0;
+        T.width[k] = w;
+    }
+    if (total > 0x7FFFFFFF) return fail(FA_ERR_ARG, "rounds fold: too many tiles");
+    int64_t grid = cu_count();
+    if (grid > total) grid = total;
+    const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
+    const uint16_t* Xb = static_cast<const uint16_t*>(X);
+    const float* Xf = static_cast<const float*>(X);
+#define FA_STB(U, C)                                                                                           \
+    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<U, C, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
+                              Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);                          \
+    else hipLaunchKernelGGL((k_fedavg_bf16_step<U, C, false, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
+                            Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
+#define FA_STF(U, C)                                                                                          \
+    if (s) hipLaunchKernelGGL((k_fold_f32_step<U, C, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
+                              Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);                               \
+    else hipLaunchKernelGGL((k_fold_f32_step<U, C, false, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
+                            Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch)
+    switch (f) {
+        case StepForm::kBf16U8C2: FA_STB(8, 2); break;
+        case StepForm::kBf16U16C2: FA_STB(16, 2); break;
+        case StepForm::kBf16U8C4: FA_STB(8, 4); break;
+        case StepForm::kBf16U4C4: FA_STB(4, 4); break;
+        case StepForm::kF32U8C4: FA_STF(8, 4); break;
+        case StepForm::kF32U8C2: FA_STF(8, 2); break;
+        case StepForm::kF32U16C2: FA_STF(16, 2); break;
+        case StepForm::kF32U16C1: FA_STF(16, 1); break;
+    }
+#undef FA_STB
+#undef FA_STF
+    const int rc = check_launch("rounds fold");
+    if (rc) return rc;
+    R.epoch = epoch;
+    R.rounds = rounds;
+    R.launched = true;
+    return FA_OK;
+}
 
 // ---- the pointer-table fold's forms (fa_fedavg_f32_ptrs_aligned) ----------
 // Row bases come from a device table; the LDS-staged forms mirror the stacked
@@ -2153,7 +2492,25 @@ inline const char* tune_form_name(int kind, int form) {
     if (kind == kTunePtrs) return ptrs_form_name((PtrsForm)form);
     return kind == kTuneF32 ? f32_pick_name((F32Pick)form) : bf16_form_name((Bf16Form)form);
 }
-fa_tune::Tuner g_tuner(tune_form_name);
+// a form's index from its name (the tuner's cache file and fa_tune_import)
+inline int tune_form_from_name(int kind, const char* name) {
+    const int n = kind == kTuneF32 ? kNumF32Picks : kind == kTuneBf16 ? kNumBf16Forms : kind == kTunePtrs ? kNumPtrsForms : 0;
+    for (int f = 0; f < n; ++f)
+        if (strcmp(tune_form_name(kind, f), name) == 0) return f;
+    return -1;
+}
+// the cache file's device identity: gfx arch and CU count ("" = unknown: not persisted)
+inline std::string tune_device_ident(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return std::string();
+    }
+    char buf[128];
+    snprintf(buf, sizeof(buf), "%s:%d", prop.gcnArchName, prop.multiProcessorCount);
+    return buf;
+}
+fa_tune::Tuner g_tuner(tune_form_name, tune_form_from_name, tune_device_ident, FA_ABI_VERSION);
 
 // fp32 candidates: the policy pick first, then the forms that won somewhere
 // near this shape in the sweeps (profiles/r02_small_n/, r03_even/, r03_slot_sweep/).
@@ -2176,6 +2533,11 @@ inline void f32_candidates(int64_t N, int64_t P, int policy, std::vector<int>& v
                           F32Pick::kLdsW8, F32Pick::kGs1C4, F32Pick::kGsBands6})
             add(p);
         add(F32Pick::kColumn);
+    } else if (policy == (int)F32Pick::kGsBalC4 && tiles4 >= 3 * cus) {
+        // 3+ tiles per CU with the band form: every sweep and tuner decision at
+        // 2.5M-25M params (C3, C5, their multi-GPU slots) kept the policy
+        // (profiles/r03_tuner/, r03_c5_c3_sweep/: within 0.5 % of the best of 106
+        // forms), so measuring there only costs the first call (C3: 132 ms)
     } else {  // large models: the grid-stride forms, the 16 KiB tile, the even split
         for (F32Pick p : {F32Pick::kGsBalC4, F32Pick::kGsBands6, F32Pick::kGsBalC2, F32Pick::kGs1C4,
                           F32Pick::kTileC4Plain, F32Pick::kEvenU4C4, F32Pick::kLdsQfW4T32})
@@ -2276,15 +2638,51 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
         case F32Pick::kDynC2:  // dynamic 8 KiB tiles (twice the tiles: finer balance)
             launch_dyn_flags<8, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
             break;
+        case F32Pick::kDynpU32C1B128:
+            launch_f32_dynp<32, 1, 128>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
+        case F32Pick::kDynpU16C1B256:
+            launch_f32_dynp<16, 1, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
+        case F32Pick::kDynpU32C1B64:
+            launch_f32_dynp<32, 1, 64>(st, 2, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
+        case F32Pick::kDynpU16C2B256:
+            launch_f32_dynp<16, 2, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
+        case F32Pick::kDynpU32C1B256:
+            launch_f32_dynp<32, 1, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
+            break;
     }
     return rc;
+}
+
+// Forms for a fold that shares the GPU with other kernels (FA_HINT_SHARED:
+// the overlapped rounds of the multi-GPU exchange): dynamic tiles fetched a
+// tile ahead, deep row pipelines over narrow tiles (tools/exchange_interference.py,
+// DESIGN.md 8).  Only where the static policy runs a grid-stride / band launch
+// over many tiles (large models); narrower shapes keep their policy form.
+inline bool shared_applies_f32(F32Pick p) { return p == F32Pick::kGsBalC4 || p == F32Pick::kGsBalC2; }
+inline F32Pick pick_f32_shared(int64_t N, int64_t P) {
+    (void)N;
+    (void)P;
+    return F32Pick::kDynpU32C1B128;
+}
+inline bool shared_applies_bf16(Bf16Form f) {
+    return f == Bf16Form::kBandsU8C4 || f == Bf16Form::kBandsU8C2 || f == Bf16Form::kBandsU2C8;
+}
+inline Bf16Form pick_bf16_shared(int64_t N, int64_t P) {
+    (void)N;
+    (void)P;
+    return Bf16Form::kDynU32C1B128;
 }
 
 // The product fp32 fold: checks, then the scalar fallback for unaligned input
 // or the shape-picked vector fold (pick_f32).  acc_in continues a fold
 // (fa_fold_f32); with acc_in and N == 0 it only finalises.
 inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                         const float* acc_in, float divisor, int finalize, float* out, void* stream) {
+                         const float* acc_in, float divisor, int finalize, float* out, void* stream,
+                         int hints = 0) {
     if (!(acc_in && N == 0)) {
         int rc = check_common(N, P, ldx, X, a, out);
         if (rc) return rc;
@@ -2326,6 +2724,13 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
         return check_launch("k_fold_f32_scalar");
     }
     const F32Pick policy = pick_f32(N, P);
+    if ((hints & FA_HINT_SHARED) && !acc && fin && shared_applies_f32(policy)) {
+        // one launch: each tile's block reads every row of its columns before
+        // it writes them, so an in-place fold is fine here too
+        int rc = launch_f32_pick(pick_f32_shared(N, P), st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
+        if (rc) return rc;
+        return check_launch("fold_f32 (shared)");
+    }
     // a plain one-shot fold (no accumulator in, with the divide) takes the
     // form the tuner measured fastest on this device.  Not when `out` overlaps
     // the rows: the measuring call runs several launches, and a later one
@@ -2379,6 +2784,10 @@ inline void bf16_candidates(int64_t N, int64_t P, int policy, std::vector<int>& 
         v.push_back((int)f);
     };
     v.push_back(policy);
+    // 1M+ octets (8.4M+ params: C4's per-GPU bucket, the whole model): the
+    // band forms kept the policy at every measured shape (profiles/r03_tuner/)
+    if ((P >> 3) >= ((int64_t)1 << 20) && (policy == (int)Bf16Form::kBandsU8C2 || policy == (int)Bf16Form::kBandsU2C8))
+        return;
     if ((P >> 3) >= ((int64_t)1 << 17))
         for (Bf16Form f : {Bf16Form::kBandsU8C2, Bf16Form::kBandsU8C4, Bf16Form::kBandsU4C4, Bf16Form::kGsBalU8C2,
                            Bf16Form::kGs1U8C4, Bf16Form::kBandsU2C8, Bf16Form::kBandsU16C2, Bf16Form::kV8U8C1})
@@ -2416,13 +2825,31 @@ inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int6
             break;
         case Bf16Form::kGsBalU8C2: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case Bf16Form::kGs1U8C4: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kDynU32C1B128:
+            launch_bf16_dyn<32, 1, 128>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kDynU16C1B256:
+            launch_bf16_dyn<16, 1, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kDynU32C1B64:
+            launch_bf16_dyn<32, 1, 64>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kDynU16C2B128:
+            launch_bf16_dyn<16, 2, 128>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kDynU8C2B256:
+            launch_bf16_dyn<8, 2, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
+        case Bf16Form::kDynU32C1B256:
+            launch_bf16_dyn<32, 1, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+            break;
     }
 #undef FA_BF
 }
 
 // The product bf16 fold (exact upcast, fp32 fold in order, optional RNE bf16 copy).
 inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                     float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
+                     float divisor, float* out_f32, uint16_t* out_bf16, void* stream, int hints = 0) {
     int rc = check_common(N, P, ldx, X, a, out_f32);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
@@ -2439,6 +2866,10 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
         return check_launch("k_fedavg_bf16_scalar");
     }
     const Bf16Form policy = pick_bf16(N, P);
+    if ((hints & FA_HINT_SHARED) && shared_applies_bf16(policy)) {  // one launch (in place is fine)
+        launch_bf16_form(pick_bf16_shared(N, P), st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
+        return check_launch("fedavg_bf16 (shared)");
+    }
     const size_t xbytes = ((size_t)(N - 1) * ldx + P) * 2;
     if (overlaps(out_f32, (size_t)P * 4, X, xbytes) || (out_bf16 && overlaps(out_bf16, (size_t)P * 2, X, xbytes))) {
         launch_bf16_form(policy, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);  // in place: one launch

@@ -5,13 +5,19 @@
 #pragma once
 
 #include <hip/hip_runtime_api.h>
+#include <fcntl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -28,31 +34,68 @@ constexpr int kTuneOk = 0;  // FA_OK: launch() returns an FA status
 // the CUs (1024 x 909K params: the policy's form 0.70 ms, the even split
 // 0.53 ms; 256 x 3.57M bf16: 0.337 against 0.295 ms; profiles/r03_slot_sweep/).
 // Every form computes the same bits, and a plain one-shot fold overwrites its
-// whole output, so the FIRST call of a new (device, dtype, N, P, pitch,
-// scored) shape runs every candidate form on the caller's own data, on the
-// caller's stream: one untimed launch of each (code-object load, cold TLBs,
-// clocks up from idle), then two timed passes in opposite orders, `batch`
-// back-to-back launches of a form between two events (batch sized to ~0.3 ms,
-// so launch gaps do not decide between forms of a 20 us kernel: timing single
-// launches between events misranked them,
+// whole output, so the FIRST call of a new shape runs every candidate form on
+// the caller's own data, on the caller's stream: one untimed launch of each
+// (code-object load, cold TLBs, clocks up from idle), then two timed passes in
+// opposite orders, `batch` back-to-back launches of a form between two events
+// (batch sized to ~0.3 ms, so launch gaps do not decide between forms of a
+// 20 us kernel: timing single launches between events misranked them,
 // profiles/r03_tuner/probe_single_launch.log); a form's time is its faster
 // pass.  Whichever form ran last, the output is the fold.  Nothing
 // synchronises: later calls read the events with hipEventQuery and run the
 // policy's pick until they are complete; from then on the shape runs the
 // fastest form -- the policy's own pick unless another beats it by more than
 // 3 % (box-to-box spread is ~2-5 %).
+//
+// A shape is (device, kind, client-count bucket, policy form, P, pitch,
+// scored).  The client count enters as its power-of-two bucket (round 4): in
+// FL the number of results per round moves with stragglers and failures, and
+// the forms' ranking follows the column tiling, not the exact row count, so a
+// round with 1000 clients reuses the decision measured at 1024 (the policy
+// form is part of the key, so a bucket never spans two policy picks).
+//
+// Decisions persist across processes (round 4): the reference builds a fresh
+// strategy per FaaS invocation (aggregation.py:71-75) under a 60 s OpenWhisk
+// limit (deploy.sh:9-10), and every cold process used to re-pay the sweep.
+// A text cache file -- one line per decided shape, keyed by the device's
+// identity (gfx arch and CU count) and the library's ABI version, forms by
+// NAME -- is read on the first tuned call and rewritten under an exclusive
+// flock(2) through a temp file + rename(2) after each new decision, merged
+// with what other processes wrote meanwhile.  Lines that do not parse, carry
+// another ABI or name an unknown form are ignored, so a stale or corrupt
+// file only costs a re-measurement.  FEDAVG_TUNE_CACHE=<path> moves it, =0
+// (or fa_tune_cache_path("")) turns it off; default
+// $XDG_CACHE_HOME/fedlesscan_amd/tuner.txt or ~/.cache/fedlesscan_amd/tuner.txt.
+// The same lines move decisions between processes (fa_tune_export /
+// fa_tune_import: a multi-GPU job runs rank 0's forms on every rank).
+//
 // FEDAVG_AUTOTUNE=0 (or fa_set_autotune(0)) keeps the policy pick;
 // FEDAVG_AUTOTUNE_LOG=1 prints every decision with each candidate's time.
 // ---------------------------------------------------------------------------
 constexpr float kTuneMargin = 0.97f;
 constexpr double kTuneBatchMs = 0.3;  // timed span per candidate
 constexpr int kTuneMaxBatch = 32;
+constexpr const char* kCacheMagic = "fedavg-tune";
+constexpr int kCacheFormat = 1;
+constexpr size_t kCacheMaxLines = 4096;
+
+// power-of-two bucket of a client count (1, 2, 4, ..., the next >= N)
+inline int64_t n_bucket(int64_t N) {
+    int64_t b = 1;
+    while (b < N && b < ((int64_t)1 << 62)) b <<= 1;
+    return b;
+}
 
 class Tuner {
   public:
-    // names a (kind, form) pair for the decision log
+    // names a (kind, form) pair; resolves a name back (-1: unknown); the
+    // identity of a device for the cache ("gfx950:256"; "" = do not persist)
     typedef const char* (*FormName)(int kind, int form);
-    explicit Tuner(FormName name = nullptr) : name_(name) {}
+    typedef int (*FormFromName)(int kind, const char* name);
+    typedef std::string (*DeviceIdent)(int dev);
+    explicit Tuner(FormName name = nullptr, FormFromName from_name = nullptr, DeviceIdent ident = nullptr,
+                   int abi = 0)
+        : name_(name), from_name_(from_name), ident_(ident), abi_(abi) {}
     static int env_mode() {
         const char* e = getenv("FEDAVG_AUTOTUNE");
         return (e && e[0] == '0') ? 0 : 1;
@@ -62,10 +105,23 @@ class Tuner {
         if (m >= 0) mode_.store(m ? 1 : 0);
         return prev;
     }
+    // The cache file ("" = none).  Takes effect for devices not yet loaded;
+    // decisions already made stay in memory.
+    void set_cache_path(const std::string& p) {
+        std::lock_guard<std::mutex> lk(mu_);
+        path_ = p;
+        path_set_ = true;
+        loaded_.clear();
+    }
+    std::string cache_path() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return path_locked();
+    }
     // Run this call's fold: launch(form) enqueues one fold of that form and
     // returns an FA status.  `cands(v)` fills the candidate forms (v[0] = the
-    // policy pick) the first time the shape is seen; `bytes` sizes the batch.
-    // Runs on the stream's device (the callers hold a StreamDevice).
+    // policy pick) the first time the shape is seen; a single candidate means
+    // the shape is not measured; `bytes` sizes the batch.  Runs on the
+    // stream's device (the callers hold a StreamDevice).
     template <class Cands, class Launch>
     int run(int kind, int64_t N, int64_t P, int64_t ldx, bool scored, int policy, double bytes, hipStream_t st,
             Cands cands, Launch launch) {
@@ -75,7 +131,7 @@ class Tuner {
             (void)hipGetLastError();
             return launch(policy);
         }
-        const Key key{dev, kind, N, P, ldx, scored ? 1 : 0};
+        const Key key{dev, kind, n_bucket(N), policy, P, ldx, scored ? 1 : 0};
         // no event calls inside a graph capture: neither the measurement nor
         // the queries of an earlier one (hipEventQuery is not capture-safe)
         auto capturing = [&] {
@@ -95,12 +151,14 @@ class Tuner {
                 if (capturing()) return launch(policy);
                 Entry fresh;
                 cands(fresh.cand);
-                fresh.kind = kind;
+                fresh.key = key;
                 fresh.N = N;
-                fresh.P = P;
-                fresh.ldx = ldx;
-                fresh.scored = scored;
                 if (fresh.cand.size() <= 1) fresh.chosen = policy;
+                if (fresh.chosen < 0) {  // a decision from the cache file or another process
+                    load_locked(dev);
+                    auto pr = preset_.find(disk_key(key));
+                    if (pr != preset_.end()) fresh.chosen = pr->second;
+                }
                 it = map_.emplace(key, std::move(fresh)).first;
                 explore = it->second.chosen < 0;
             }
@@ -161,29 +219,201 @@ class Tuner {
         return n;
     }
     // chosen form (>= 0), -1 while the shape is being measured, -2 unknown shape
-    int chosen(int dev, int kind, int64_t N, int64_t P, int64_t ldx, bool scored) {
+    int chosen(int dev, int kind, int64_t N, int policy, int64_t P, int64_t ldx, bool scored) {
         std::lock_guard<std::mutex> lk(mu_);
-        auto it = map_.find(Key{dev, kind, N, P, ldx, scored ? 1 : 0});
+        auto it = map_.find(Key{dev, kind, n_bucket(N), policy, P, ldx, scored ? 1 : 0});
         if (it == map_.end()) return -2;
         if (it->second.chosen < 0) harvest(it->second);
         return it->second.chosen;
     }
+    // Every decided shape of this process, as cache-file lines.
+    std::string export_text() {
+        std::lock_guard<std::mutex> lk(mu_);
+        std::string out;
+        for (auto& kv : map_) {
+            if (kv.second.chosen < 0) continue;
+            const std::string id = ident_of(std::get<0>(kv.first));
+            if (!id.empty()) out += line_of(id, kv.first, kv.second.chosen);
+        }
+        return out;
+    }
+    // Apply decisions given as cache-file lines (every device whose identity
+    // matches a line takes it, now and for shapes it has not seen yet).
+    // Returns the number of lines applied.
+    int import_text(const std::string& text) {
+        std::lock_guard<std::mutex> lk(mu_);
+        int applied = 0;
+        size_t pos = 0;
+        while (pos < text.size()) {
+            size_t nl = text.find('\n', pos);
+            if (nl == std::string::npos) nl = text.size();
+            DiskKey dk;
+            int form = -1;
+            if (parse_line(text.substr(pos, nl - pos), dk, form)) {
+                preset_[dk] = form;
+                for (auto& kv : map_) {
+                    if (disk_key(kv.first) != dk) continue;
+                    // a measurement in flight is dropped: its events now (armed), or by the
+                    // thread still issuing it, which releases them when it sees a decision
+                    if (kv.second.armed) release(kv.second);
+                    kv.second.chosen = form;
+                }
+                ++applied;
+            }
+            pos = nl + 1;
+        }
+        return applied;
+    }
 
   private:
-    typedef std::tuple<int, int, int64_t, int64_t, int64_t, int> Key;
+    // (dev, kind, client bucket, policy form, P, ldx, scored)
+    typedef std::tuple<int, int, int64_t, int, int64_t, int64_t, int> Key;
+    // (device identity, kind, client bucket, policy NAME, P, ldx, scored)
+    typedef std::tuple<std::string, int, int64_t, std::string, int64_t, int64_t, int> DiskKey;
     struct Entry {
         std::vector<int> cand;
         std::vector<hipEvent_t> events;  // [2(pass*n + c)] start, [... + 1] end of candidate c's batch
         int batch = 1, chosen = -1;
         bool armed = false;  // the exploring call has recorded every event
-        int kind = 0;
-        int64_t N = 0, P = 0, ldx = 0;
-        bool scored = false;
+        Key key;
+        int64_t N = 0;       // the client count measured (the log)
     };
     void release(Entry& e) {
         for (hipEvent_t x : e.events)
             if (x) (void)hipEventDestroy(x);
         e.events.clear();
+    }
+    // ---- the cache file -------------------------------------------------------
+    std::string ident_of(int dev) {
+        auto it = ident_cache_.find(dev);
+        if (it != ident_cache_.end()) return it->second;
+        std::string id = ident_ ? ident_(dev) : std::string();
+        for (char& c : id)
+            if (c == ' ' || c == '\n' || c == '\t') c = '_';
+        ident_cache_[dev] = id;
+        return id;
+    }
+    DiskKey disk_key(const Key& k) {
+        return DiskKey{ident_of(std::get<0>(k)), std::get<1>(k), std::get<2>(k),
+                       form_name(std::get<1>(k), std::get<3>(k)), std::get<4>(k), std::get<5>(k), std::get<6>(k)};
+    }
+    std::string line_of(const std::string& id, const Key& k, int form) {
+        char buf[512];
+        snprintf(buf, sizeof(buf), "%s %d %s %d %d %lld %s %lld %lld %d %s\n", kCacheMagic, kCacheFormat, id.c_str(),
+                 abi_, std::get<1>(k), (long long)std::get<2>(k), form_name(std::get<1>(k), std::get<3>(k)),
+                 (long long)std::get<4>(k), (long long)std::get<5>(k), std::get<6>(k),
+                 form_name(std::get<1>(k), form));
+        return buf;
+    }
+    // One cache line -> key + form, or false (malformed, other format or ABI,
+    // a form this library does not know).
+    bool parse_line(const std::string& line, DiskKey& dk, int& form) const {
+        char magic[32], id[128], pol[96], fname[96];
+        int fmt = 0, abi = 0, kind = 0, scored = 0;
+        long long nb = 0, P = 0, ldx = 0;
+        char tail = 0;
+        if (line.size() > 400) return false;
+        const int got = sscanf(line.c_str(), "%31s %d %127s %d %d %lld %95s %lld %lld %d %95s %c", magic, &fmt, id,
+                               &abi, &kind, &nb, pol, &P, &ldx, &scored, fname, &tail);
+        if (got != 11 || strcmp(magic, kCacheMagic) != 0 || fmt != kCacheFormat || abi != abi_) return false;
+        if (kind < 1 || kind > 16 || nb < 1 || (nb & (nb - 1)) || P < 1 || ldx < P || (scored != 0 && scored != 1))
+            return false;
+        if (!from_name_ || from_name_(kind, pol) < 0) return false;
+        form = from_name_(kind, fname);
+        if (form < 0) return false;
+        dk = DiskKey{std::string(id), kind, (int64_t)nb, std::string(pol), (int64_t)P, (int64_t)ldx, scored};
+        return true;
+    }
+    std::string path_locked() {
+        if (!path_set_) {
+            path_set_ = true;
+            const char* e = getenv("FEDAVG_TUNE_CACHE");
+            if (e) {
+                path_ = (e[0] == '0' && e[1] == 0) ? std::string() : std::string(e);
+            } else {
+                const char* x = getenv("XDG_CACHE_HOME");
+                const char* h = getenv("HOME");
+                if (x && x[0]) path_ = std::string(x) + "/fedlesscan_amd/tuner.txt";
+                else if (h && h[0]) path_ = std::string(h) + "/.cache/fedlesscan_amd/tuner.txt";
+            }
+        }
+        return path_;
+    }
+    static std::string read_file(const std::string& p) {
+        std::string s;
+        FILE* f = fopen(p.c_str(), "rb");
+        if (!f) return s;
+        char buf[65536];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof(buf), f)) > 0 && s.size() < ((size_t)8 << 20)) s.append(buf, k);
+        fclose(f);
+        return s;
+    }
+    // Under mu_: read the file's decisions for this device's identity once.
+    void load_locked(int dev) {
+        const std::string id = ident_of(dev);
+        if (id.empty() || loaded_.count(id)) return;
+        loaded_[id] = true;
+        const std::string p = path_locked();
+        if (p.empty()) return;
+        const std::string text = read_file(p);
+        size_t pos = 0;
+        while (pos < text.size()) {
+            size_t nl = text.find('\n', pos);
+            if (nl == std::string::npos) nl = text.size();
+            DiskKey dk;
+            int form = -1;
+            if (parse_line(text.substr(pos, nl - pos), dk, form) && std::get<0>(dk) == id) preset_[dk] = form;
+            pos = nl + 1;
+        }
+    }
+    static void make_dirs(const std::string& p) {
+        for (size_t i = 1; i < p.size(); ++i)
+            if (p[i] == '/') (void)mkdir(p.substr(0, i).c_str(), 0755);
+    }
+    // Under mu_: merge one new decision into the file (never fails the caller).
+    void persist_locked(const Entry& e) {
+        const std::string p = path_locked();
+        const std::string id = ident_of(std::get<0>(e.key));
+        if (p.empty() || id.empty() || e.chosen < 0) return;
+        const std::string mine = line_of(id, e.key, e.chosen);
+        DiskKey dk;
+        int form = -1;
+        if (!parse_line(mine.substr(0, mine.size() - 1), dk, form)) return;
+        make_dirs(p);
+        const int lk = open((p + ".lock").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+        if (lk < 0) return;
+        if (flock(lk, LOCK_EX) == 0) {
+            // keep every other line that parses (other shapes, devices,
+            // processes); lines of another ABI or format and corrupt lines go
+            std::string out;
+            size_t kept = 0;
+            const std::string text = read_file(p);
+            size_t pos = 0;
+            while (pos < text.size()) {
+                size_t nl = text.find('\n', pos);
+                if (nl == std::string::npos) nl = text.size();
+                const std::string ln = text.substr(pos, nl - pos);
+                DiskKey k2;
+                int f2 = -1;
+                if (parse_line(ln, k2, f2) && k2 != dk && kept + 1 < kCacheMaxLines) {
+                    out += ln + "\n";
+                    ++kept;
+                }
+                pos = nl + 1;
+            }
+            out += mine;
+            char tmp_suffix[64];
+            snprintf(tmp_suffix, sizeof(tmp_suffix), ".tmp.%ld", (long)getpid());
+            const std::string tmp = p + tmp_suffix;
+            FILE* f = fopen(tmp.c_str(), "wb");
+            bool ok = f && fwrite(out.data(), 1, out.size(), f) == out.size();
+            if (f) ok = (fclose(f) == 0) && ok;
+            if (ok) ok = rename(tmp.c_str(), p.c_str()) == 0;
+            if (!ok) (void)unlink(tmp.c_str());
+            (void)flock(lk, LOCK_UN);
+        }
+        close(lk);
     }
     // Decide once the last candidate's end event has completed (the events
     // complete in stream order).  Under mu_.
@@ -213,20 +443,31 @@ class Tuner {
             if (ms[c] < ms[b]) b = c;
         e.chosen = (ms[b] < kTuneMargin * ms[0]) ? e.cand[b] : e.cand[0];
         if (log_) {
+            const int kind = std::get<1>(e.key);
             char line[1024];
             int k = snprintf(line, sizeof(line), "fedavg tuner: %s N=%lld P=%lld ldx=%lld%s batch=%d -> %s |",
-                             e.kind == 1 ? "f32" : e.kind == 2 ? "bf16" : "f32 rows", (long long)e.N, (long long)e.P, (long long)e.ldx,
-                             e.scored ? " scored" : "", e.batch, form_name(e.kind, e.chosen));
+                             kind == 1 ? "f32" : kind == 2 ? "bf16" : "f32 rows", (long long)e.N,
+                             (long long)std::get<4>(e.key), (long long)std::get<5>(e.key),
+                             std::get<6>(e.key) ? " scored" : "", e.batch, form_name(kind, e.chosen));
             for (int c = 0; c < n && k > 0 && k < (int)sizeof(line); ++c)
-                k += snprintf(line + k, sizeof(line) - k, " %s %.4f", form_name(e.kind, e.cand[c]), ms[c]);
+                k += snprintf(line + k, sizeof(line) - k, " %s %.4f", form_name(kind, e.cand[c]), ms[c]);
             fprintf(stderr, "%s ms\n", line);
         }
         release(e);
+        persist_locked(e);
     }
     const char* form_name(int kind, int form) const { return name_ ? name_(kind, form) : "?"; }
     FormName name_;
+    FormFromName from_name_;
+    DeviceIdent ident_;
+    const int abi_;
     std::mutex mu_;
     std::map<Key, Entry> map_;
+    std::map<DiskKey, int> preset_;         // decisions from the file / other processes
+    std::map<std::string, bool> loaded_;    // device identities whose file lines are in preset_
+    std::map<int, std::string> ident_cache_;
+    std::string path_;
+    bool path_set_ = false;
     std::atomic<int> mode_{env_mode()};
     const bool log_ = getenv("FEDAVG_AUTOTUNE_LOG") && getenv("FEDAVG_AUTOTUNE_LOG")[0] == '1';
 };

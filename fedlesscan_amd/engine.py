@@ -353,13 +353,22 @@ class RowSet:
         self.N, self.P, self.device, self.dtype = N, P, dev, dt
         self.view = None
         self.ptrs = None
+        self.host_ptrs = None
         self.aligned = False
         if dt == torch.float32 and P > 0:
-            host_ptrs = np.fromiter(map(torch.Tensor.data_ptr, rows), dtype=np.int64, count=N)
+            host_ptrs = self.host_ptrs = np.fromiter(map(torch.Tensor.data_ptr, rows), dtype=np.int64, count=N)
             self.view = _equal_stride_view(rows, host_ptrs, P)
             if self.view is None:
                 self.ptrs = torch.from_numpy(host_ptrs).to(dev)
                 self.aligned = not (host_ptrs % 16).any()
+
+    def overlaps(self, t: torch.Tensor) -> bool:
+        """Does tensor t share a byte with any row?"""
+        if self.host_ptrs is None or self.P == 0 or t.numel() == 0:
+            return False
+        lo = t.data_ptr()
+        hi = lo + t.numel() * t.element_size()
+        return bool(np.any((self.host_ptrs < hi) & (lo < self.host_ptrs + self.P * 4)))
 
     def stacked(self) -> torch.Tensor:
         """The rows copied into one [N, P] tensor (the non-fp32 fallbacks)."""
@@ -385,10 +394,20 @@ def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
         return fold_stacked(X, weights, scores, out=out, total=total)
     dev = rs.device
     f = fw or Factors(weights, scores, np.dtype(np.float32), total=total)
+    dst = out
+    if out is not None and rs.overlaps(out):
+        # out over a client row: the row table lives in device memory, so the
+        # library cannot see the alias, and the tuner's first call of a shape
+        # runs several launches into out (a later one would read what an earlier
+        # wrote).  Fold into a fresh buffer, then copy.
+        out = None
     out = out if out is not None else torch.empty(rs.P, dtype=torch.float32, device=dev)
     aligned = rs.aligned and out.data_ptr() % 16 == 0
     _lib.call("fa_fedavg_f32_ptrs_hostf", rs.ptrs.data_ptr(), rs.N, rs.P, *f.host(), float(f.div), int(aligned),
               out.data_ptr(), stream_ptr(dev))
+    if dst is not None and dst is not out:
+        dst.copy_(out)
+        return dst
     return out
 
 
@@ -577,6 +596,7 @@ def aggregate_decoded(items, scores: Optional[Sequence] = None, device: Optional
                 outs.append(flat[off:off + n].reshape(shp))
                 off += n
             return outs
+        sf.abandon()  # release the pipe now: no DMA or fold left running for GC to join
     for layers, w in it:
         rows.append(layers)
         weights.append(w)
@@ -594,8 +614,9 @@ def to_host(t: torch.Tensor) -> np.ndarray:
 
 
 def _stream_group(parameters, n, lis, P, w, sc, total, dev) -> torch.Tensor:
-    from .ingest import make_streaming_fold
-    sf = make_streaming_fold(P, dev, min(STREAM_CHUNK_BYTES, max(1, n) * 4 * P), direct=DIRECT_DMA, expected_rows=n)
+    from .ingest import chunk_class, make_streaming_fold
+    sf = make_streaming_fold(P, dev, chunk_class(max(1, n) * 4 * P, STREAM_CHUNK_BYTES), direct=DIRECT_DMA,
+                             expected_rows=n)
     for i in range(n):
         sf.add([parameters[i][li] for li in lis], w[i], None if sc is None else sc[i])
     return sf.finish(total=total)

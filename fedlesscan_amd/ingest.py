@@ -211,6 +211,12 @@ class StreamingFold:
             self.keep = [[] for _ in range(self.K)]
         return self.acc
 
+    def abandon(self):
+        """Give up this round (a caller falling back to another path): wait for
+        the copies already issued, drop the row references."""
+        self.copy_stream.synchronize()
+        self.keep = [[] for _ in range(self.K)]
+
 
 class _PipeCache:
     """Native ingest pipes (fa_ingest_*) kept across rounds: a pipe owns
@@ -343,6 +349,16 @@ class NativeStreamingFold:
         self.keep = []
         return self.acc
 
+    def abandon(self):
+        """Give up this round now (a caller that falls back to another path):
+        the pipe is destroyed here -- its copies waited for, its issuer thread
+        joined -- rather than left issuing for an accumulator nobody reads until
+        garbage collection runs __del__."""
+        if self.pipe is not None:
+            _pipes.drop(self.pipe)
+            self.pipe = None
+        self.keep = []
+
     def __del__(self):
         if getattr(self, "pipe", None) is not None:  # abandoned mid-round
             try:
@@ -354,6 +370,18 @@ class NativeStreamingFold:
 # native pipe by default; FEDAVG_NATIVE_INGEST=0 selects the Python-driven StreamingFold
 NATIVE_INGEST = os.environ.get("FEDAVG_NATIVE_INGEST", "1") == "1"
 STREAM_SLOTS = int(os.environ.get("FEDAVG_STREAM_SLOTS", "0"))  # 0: the form's default
+
+
+def chunk_class(nbytes: int, cap: int) -> int:
+    """The chunk size a pipe is made (and cached) for: the next power of two
+    >= nbytes, at least 1 MiB, at most cap.  A round whose rows need less than
+    a full chunk rounds up to a few size classes, so rounds whose client count
+    varies (stragglers, failures) reuse the same pipe instead of each creating
+    and destroying its own page-locked slots and issuer thread."""
+    c = 1 << 20
+    while c < nbytes and c < cap:
+        c <<= 1
+    return min(c, cap)
 
 
 def make_streaming_fold(P: int, device, chunk_bytes: int, direct: bool = False, expected_rows: int = 0):

@@ -119,6 +119,12 @@ class MultiStreamingFold:
                 sf.add(_bucket_pieces(flat, offs, lo, hi), weight, score)
         self.rows += 1
 
+    def abandon(self):
+        """Give up the round on every GPU (see NativeStreamingFold.abandon)."""
+        for sf in self.folds:
+            if sf is not None:
+                sf.abandon()
+
     def finish_device(self, total=None) -> List[torch.Tensor]:
         """Divide on every GPU; the per-GPU bucket results (device tensors)."""
         if self.rows == 0:

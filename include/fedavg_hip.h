@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 2
+#define FA_ABI_VERSION 3
 
 enum fa_status {
     FA_OK = 0,
@@ -111,6 +111,60 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                    const float* a, const float* s, float divisor,
                    float* out_f32, uint16_t* out_bf16, void* stream);
 
+/* The same folds with hints (ABI 3).  FA_HINT_SHARED: other kernels run on
+ * the GPU beside this fold -- at N > 1 the all-gather of exchange round k
+ * overlaps the fold of round k+1 (fedlesscan_amd/sharding.py).  A static tile
+ * schedule waits at its end for the blocks that share a CU with them; with
+ * the hint a large fold takes its column tiles from a device counter, fetched
+ * a tile ahead, with deep row pipelines over narrow tiles, so the slowed
+ * blocks fold fewer tiles.  Narrow models keep their usual
+ * form.  Same bits with or without hints; hints = 0 is exactly fa_fedavg_f32
+ * / fa_fedavg_bf16.  Unknown hint bits are FA_ERR_ARG. */
+#define FA_HINT_SHARED 1
+int fa_fedavg_f32_ex(const float* X, int64_t N, int64_t P, int64_t ldx,
+                     const float* a, const float* s, float divisor,
+                     float* out, int hints, void* stream);
+int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
+                      const float* a, const float* s, float divisor,
+                      float* out_f32, uint16_t* out_bf16, int hints, void* stream);
+
+/* ---- one launch per exchange step (ABI 3) -----------------------------------
+ * At N > 1 a rank folds its columns in `rounds` slots and all-gathers each
+ * slot while the next one folds (fedlesscan_amd/sharding.py).  Folding each
+ * slot in its own launch leaves a tail per launch, and the launches beside the
+ * exchange lose blocks to the collective's kernels.  fa_fedavg_*_rounds folds
+ * every slot of a step in ONE launch: column tiles are taken from a device
+ * counter (round 0's first, then round 1's, ...), so a round's last tiles
+ * overlap the next round's first ones and blocks that share a CU with other
+ * kernels fold fewer tiles; when round k's last tile is done the launch
+ * raises round k's flag.  fa_rounds_wait(r, k, stream) enqueues on another
+ * stream a one-lane kernel that returns once round k of r's last launch is
+ * complete (its results visible device-wide): the exchange of round k
+ * enqueued behind it on that stream starts mid-launch.  Same bits as
+ * fa_fedavg_f32 / fa_fedavg_bf16 on each slot.
+ *   fa_rounds_create / _destroy: the launch state (device signal words) for
+ *     one device; launches with one object must be ordered (one stream), and
+ *     destroy synchronises the device.
+ *   offsets [host] rounds + 1 local columns: round k folds columns
+ *     [offsets[k], offsets[k+1]) of X (and writes the same columns of out);
+ *     every round non-empty, 16-B aligned (offsets % 4, bf16 % 8), ldx too;
+ *     1 <= rounds <= 8.  Not under graph capture (FA_ERR_ARG).
+ *   fa_rounds_wait: round < the last launch's rounds; a waiter that sees no
+ *     completion within ~10 s returns anyway and counts a timeout;
+ *     fa_rounds_timeouts (synchronous) returns that count. */
+typedef struct fa_rounds fa_rounds;
+int fa_rounds_create(fa_rounds** r, int device);
+int fa_rounds_destroy(fa_rounds* r);
+int fa_fedavg_f32_rounds(fa_rounds* r, const float* X, int64_t N, int64_t ldx,
+                         const float* a, const float* s, float divisor, float* out,
+                         int rounds, const int64_t* offsets, void* stream);
+int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx,
+                          const float* a, const float* s, float divisor,
+                          float* out_f32, uint16_t* out_bf16,
+                          int rounds, const int64_t* offsets, void* stream);
+int fa_rounds_wait(fa_rounds* r, int round, void* stream);
+int fa_rounds_timeouts(fa_rounds* r);
+
 /* The same folds with the per-client factors a[0..N), s[0..N) (s may be
  * NULL) in HOST memory, as the reference's caller holds them (Python numbers,
  * fed_avg_aggregator.py:32-41).  The library copies them into a page-locked
@@ -159,6 +213,29 @@ enum fa_fold_kind {
 int fa_set_autotune(int mode);
 int fa_autotune_pending(void);
 const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored, void* stream);
+/* Decisions outlive the process (ABI 3).  A shape's key takes the client
+ * count as its power-of-two bucket (a round with 1000 results reuses what
+ * 1024 measured) plus the policy's form.  Every decision is merged into a
+ * text cache file (one line per shape: device arch and CU count, ABI version,
+ * kind, client bucket, policy form, P, ldx, scored, chosen form -- forms by
+ * name), written under an exclusive lock through a temp file and a rename;
+ * the first tuned call of a process reads it, so a cold process (one FaaS
+ * invocation: aggregation.py:71-75) runs a known shape's form on its first
+ * call.  Unparseable lines, another ABI or an unknown form are ignored.
+ * Default path $XDG_CACHE_HOME/fedlesscan_amd/tuner.txt or
+ * ~/.cache/fedlesscan_amd/tuner.txt; FEDAVG_TUNE_CACHE=<path> or =0 (off).
+ *   fa_tune_cache_path: set the file at run time ("" or NULL: off)
+ *   fa_tune_export:     [host] this process's decisions as those lines into
+ *                       buf (NUL-terminated, truncated to cap - 1); returns
+ *                       the full length
+ *   fa_tune_import:     [host] apply such lines (a decision made elsewhere
+ *                       replaces this process's own for the same shape);
+ *                       returns the number of lines applied.  A multi-GPU job
+ *                       broadcasts rank 0's export so that every rank runs the
+ *                       same forms. */
+int fa_tune_cache_path(const char* path);
+int64_t fa_tune_export(char* buf, int64_t cap);
+int fa_tune_import(const char* text);
 
 /* float64 updates (the reference unit-test fixture is float64,
  * test/test_aggregation.py:23-38). */

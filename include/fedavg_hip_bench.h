@@ -85,6 +85,19 @@ int fa_fedavg_f32_ptrs_variant(const float* const* xi, int64_t N, int64_t P,
 int fa_num_ptrs_variants(void);
 const char* fa_ptrs_variant_name(int variant);
 
+/* One launch per exchange step with a chosen step form (fa_step_form_name;
+ * the product's fa_fedavg_*_rounds runs the policy's form): a bench-library
+ * launch state, the launch and its waiter.  X/out_bf16 are bf16 for the
+ * bf16_* forms (out_bf16 may be NULL), fp32 otherwise (out_bf16 ignored). */
+int fa_num_step_forms(void);
+const char* fa_step_form_name(int form);
+int fa_bench_rounds_create(void** r, int device);
+int fa_bench_rounds_destroy(void* r);
+int fa_fedavg_rounds_form(void* r, int form, const void* X, int64_t N, int64_t ldx, const float* a, const float* s,
+                          float divisor, float* out, uint16_t* out_bf16, int rounds, const int64_t* offsets,
+                          void* stream);
+int fa_bench_rounds_wait(void* r, int round, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

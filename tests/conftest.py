@@ -9,6 +9,11 @@ if REPO not in sys.path:
 HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
+# The library's tuner persists its decisions (FEDAVG_TUNE_CACHE); tests start
+# from an empty cache of their own so that they see every shape measured.
+if "FEDAVG_TUNE_CACHE" not in os.environ:
+    import tempfile
+    os.environ["FEDAVG_TUNE_CACHE"] = os.path.join(tempfile.mkdtemp(prefix="fa_tune_test_"), "tuner.txt")
 
 
 def pytest_configure(config):

@@ -279,3 +279,25 @@ def test_fold_inside_a_graph_capture(dev, L):
         g.replay()
         torch.cuda.synchronize()
         assert G.same_bits(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("k", [0, 5])
+def test_row_table_fold_into_one_of_its_rows(dev, L, k):
+    """engine.fold_rows with out = rows[k]: the row table lives in
+    device memory, so the library cannot see the alias, and the tuner's first
+    call of a shape runs every candidate form into `out`.  fold_rows sees it
+    on the host (RowSet.overlaps), folds into a fresh buffer and copies: the
+    exploring call and the decided one are both bit-exact."""
+    from fedlesscan_amd import engine
+    N, P, seed = 12, 150_001 + 64 * k, 800 + k  # a shape of its own: its first call measures
+    X = synth.clients_f32(seed, N, 0, P)
+    w = synth.cardinalities(seed, N)
+    exp = OL.fedavg_f32(X, np.array(w, np.float32), np.float32(sum(w)))
+    for call in range(3):
+        rows = [torch.from_numpy(X[i].copy()).to(dev) for i in range(N)]  # separate allocations: the table path
+        rs = engine.RowSet(rows)
+        assert rs.view is None and rs.overlaps(rows[k]) and not rs.overlaps(torch.empty(P, device=dev))
+        got = engine.fold_rows(rs, w, out=rows[k])
+        assert got.data_ptr() == rows[k].data_ptr()
+        assert G.same_bits(rows[k].cpu().numpy(), exp), (k, call)
+        torch.cuda.synchronize()

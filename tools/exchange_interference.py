@@ -39,8 +39,16 @@ def main():
     ap.add_argument("--copy-on-free", action="store_true",
                     help="with --fold-free: the copy stream gets exactly the CUs the fold leaves (the ideal "
                          "placement); otherwise the copy stream has every CU, as RCCL's")
-    ap.add_argument("--forms", default="", help="fp32 only: comma-separated fold forms (fa_f32_form_name) to force "
-                                              "instead of the product's tuned choice")
+    ap.add_argument("--forms", default="", help="comma-separated fold forms (fa_f32_form_name / fa_bf16_form_name) "
+                                              "to force instead of the product's tuned choice")
+    ap.add_argument("--forced-rounds", default="all", choices=["all", "overlapped"],
+                    help="rounds that run the forced form: all, or only those after round 0 (the rounds an "
+                         "exchange overlaps; round 0 keeps the tuned form)")
+    ap.add_argument("--step-forms", default="",
+                    help="comma-separated step forms (fa_step_form_name; 'product' = fa_fedavg_*_rounds): the whole "
+                         "step in ONE launch, each round's copy queued behind fa_*_rounds_wait on the copy stream")
+    ap.add_argument("--hint", action="store_true",
+                    help="the product's shared-CU hint (fa_fedavg_*_ex, FA_HINT_SHARED) on the overlapped rounds")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L, B = _lib.load(), _lib.load_bench()
@@ -87,16 +95,34 @@ def main():
         fs = fold_stream(dev)
         xs = torch.cuda.Stream(device=dev)  # normal priority, like RCCL's stream
 
-    names = {B.fa_f32_form_name(i).decode(): i for i in range(B.fa_num_f32_forms())}
+    if dt == "f32":
+        names = {B.fa_f32_form_name(i).decode(): i for i in range(B.fa_num_f32_forms())}
+    else:
+        names = {B.fa_bf16_form_name(i).decode(): i for i in range(B.fa_num_bf16_forms())}
     form = [None]
 
     def fold(k):
         off, width = lay.offset(k), lay.width(k)
         x = X.data_ptr() + off * esz
-        if dt == "f32" and form[0] is not None:
+        forced = form[0] is not None and (args.forced_rounds == "all" or k > 0)
+        if forced and dt == "f32":
             rc = B.fa_fedavg_f32_form(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
                                       fs.cuda_stream, form[0])
             _lib.check(rc, "form", bench=True)
+            return
+        if forced:
+            rc = B.fa_fedavg_bf16_form(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+                                       outb.data_ptr() + off * 2, fs.cuda_stream, form[0])
+            _lib.check(rc, "form", bench=True)
+            return
+        if args.hint and k > 0:
+            if dt == "f32":
+                rc = L.fa_fedavg_f32_ex(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, 1,
+                                        fs.cuda_stream)
+            else:
+                rc = L.fa_fedavg_bf16_ex(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+                                         outb.data_ptr() + off * 2, 1, fs.cuda_stream)
+            _lib.check(rc, "fold (shared hint)")
             return
         if dt == "f32":
             rc = L.fa_fedavg_f32(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, fs.cuda_stream)
@@ -117,6 +143,42 @@ def main():
                            bench=True)
         fs.wait_stream(xs)
 
+    import ctypes as _ct
+    offs = (_ct.c_int64 * (lay.rounds + 1))(*[lay.offset(k) for k in range(lay.rounds + 1)])
+    step_names = {B.fa_step_form_name(i).decode(): i for i in range(B.fa_num_step_forms())}
+    rs_bench = _ct.c_void_p()
+    _lib.check(B.fa_bench_rounds_create(_ct.byref(rs_bench), 0), "rounds state", bench=True)
+    rs_prod = _ct.c_void_p()
+    _lib.check(L.fa_rounds_create(_ct.byref(rs_prod), 0), "rounds state")
+
+    def step_one_launch(sform, blocks, ev):
+        """The whole step in one launch; round k's copy behind a waiter for round k."""
+        ev[0][0].record(fs)
+        if sform == "product":
+            if dt == "f32":
+                rc = L.fa_fedavg_f32_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, out.data_ptr(),
+                                            lay.rounds, offs, fs.cuda_stream)
+            else:
+                rc = L.fa_fedavg_bf16_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, out.data_ptr(),
+                                             outb.data_ptr(), lay.rounds, offs, fs.cuda_stream)
+            _lib.check(rc, "rounds fold")
+        else:
+            rc = B.fa_fedavg_rounds_form(rs_bench, step_names[sform], X.data_ptr(), N, W, a.data_ptr(), None, div,
+                                         out.data_ptr(), None if outb is None else outb.data_ptr(), lay.rounds, offs,
+                                         fs.cuda_stream)
+            _lib.check(rc, "rounds form", bench=True)
+        ev[0][1].record(fs)
+        if blocks:
+            for k in range(lay.rounds):
+                if sform == "product":
+                    _lib.check(L.fa_rounds_wait(rs_prod, k, xs.cuda_stream), "rounds wait")
+                else:
+                    _lib.check(B.fa_bench_rounds_wait(rs_bench, k, xs.cuda_stream), "rounds wait", bench=True)
+                n = int(lay.width(k) * (args.world - 1) * out_esz * args.scale) // 16 * 4
+                _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
+                           bench=True)
+        fs.wait_stream(xs)
+
     for _ in range(3):  # the tuner's first calls, warm-up
         step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                  for _ in range(lay.rounds)])
@@ -124,13 +186,33 @@ def main():
     print(f"{args.config} rank of {args.world}: widths {lay.widths}, fold CUs {cus - args.fold_free}"
           f"{' (copy on the others)' if args.copy_on_free else ''}, copy source "
           f"{'host (PCIe)' if args.host_src else 'HBM'}, {args.scale:g} of the received bytes")
+    for sform in [f for f in args.step_forms.split(",") if f]:
+        for _ in range(3):
+            step_one_launch(sform, 0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))])
+        torch.cuda.synchronize()
+        for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
+            folds = []
+            for _ in range(args.steps):
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+                step_one_launch(sform, blocks, ev)
+                torch.cuda.synchronize()
+                folds.append(ev[0][0].elapsed_time(ev[0][1]))
+            folds.sort()
+            print(f"  {'one launch ' + sform:24s} copy blocks {blocks:3d}: fold per step median "
+                  f"{folds[len(folds) // 2]:.4f} ms (min {folds[0]:.4f})", flush=True)
+    tmo = L.fa_rounds_timeouts(rs_prod)
+    if tmo:
+        print(f"  WARNING: {tmo} round waits timed out", flush=True)
+    if args.step_forms and not args.forms:
+        return
     for fname in [f for f in args.forms.split(",") if f] or [None]:
         form[0] = None if fname is None else names[fname]
         for _ in range(2):  # warm the forced form
             step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in range(lay.rounds)])
         torch.cuda.synchronize()
-        label = fname or "tuned"
+        label = (fname or ("hint" if args.hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all"
+                                                                  else "")
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
             folds = []
             for _ in range(args.steps):
@@ -140,7 +222,7 @@ def main():
                 torch.cuda.synchronize()
                 folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
             folds.sort()
-            print(f"  {label:14s} copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
+            print(f"  {label:24s} copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
                   f"(min {folds[0]:.4f})", flush=True)
 
 

@@ -8,6 +8,9 @@
 // measuring, and many threads tuning many shapes at once agree (run under
 // TSan and ASan + UBSan by tools/tuner_stress.sh; no events leak).
 #include <cassert>
+#include <cstring>
+#include <string>
+#include <unistd.h>
 #include <cmath>
 #include <cstdio>
 #include <random>
@@ -31,6 +34,38 @@ static const char* name(int kind, int form) {
     static const char* n[] = {"f0", "f1", "f2", "f3", "f4", "f5", "f6", "f7"};
     (void)kind;
     return form >= 0 && form < 8 ? n[form] : "?";
+}
+static int from_name(int kind, const char* nm) {
+    (void)kind;
+    for (int f = 0; f < 8; ++f)
+        if (strcmp(name(1, f), nm) == 0) return f;
+    return -1;
+}
+static std::string ident(int dev) { return "sim:" + std::to_string(dev); }
+static std::string slurp(const std::string& p) {
+    std::string s;
+    FILE* f = fopen(p.c_str(), "rb");
+    if (!f) return s;
+    char b[4096];
+    size_t k;
+    while ((k = fread(b, 1, sizeof(b), f)) > 0) s.append(b, k);
+    fclose(f);
+    return s;
+}
+static void spit(const std::string& p, const std::string& text) {
+    FILE* f = fopen(p.c_str(), "wb");
+    fwrite(text.data(), 1, text.size(), f);
+    fclose(f);
+}
+static int count_lines(const std::string& s) {
+    int n = 0;
+    for (char c : s) n += c == '\n';
+    return n;
+}
+// settle every measurement in flight
+static void drain(Tuner& t) {
+    while (t.pending()) {
+    }
 }
 
 // One call of shape (N, P) whose forms cost cost[form] ms per launch on stream s.
@@ -59,13 +94,13 @@ int main() {
         tunersim::not_ready_queries() = 6;  // the last event completes at its 7th query
         CHECK(call(t, &s, 10, 1000, cost, &launches) == 0);
         CHECK(launches == 4 + 2 * 4 * 1);  // bytes 1e12: batch 1
-        CHECK(t.chosen(0, 1, 10, 1000, 1000, false) == -1);  // events still "in flight"
+        CHECK(t.chosen(0, 1, 10, 0, 1000, 1000, false) == -1);  // events still "in flight"
         CHECK(t.pending() == 1);
         // calls while the events are in flight run one launch each (the policy's form)
         int later = 0;
         for (int i = 0; i < 3; ++i) call(t, &s, 10, 1000, cost, &later);
-        CHECK(later == 3 && t.chosen(0, 1, 10, 1000, 1000, false) == -1);
-        CHECK(t.chosen(0, 1, 10, 1000, 1000, false) == 3);  // 7th query: decided
+        CHECK(later == 3 && t.chosen(0, 1, 10, 0, 1000, 1000, false) == -1);
+        CHECK(t.chosen(0, 1, 10, 0, 1000, 1000, false) == 3);  // 7th query: decided
         CHECK(t.pending() == 0);
         tunersim::not_ready_queries() = 2;
     }
@@ -77,7 +112,7 @@ int main() {
         call(t, &s, 5, 77, cost, nullptr);
         while (t.pending()) {
         }
-        CHECK(t.chosen(0, 1, 5, 77, 77, false) == 0);
+        CHECK(t.chosen(0, 1, 5, 0, 77, 77, false) == 0);
     }
     // 3. small folds are timed in batches (~0.3 ms per candidate, at most 32)
     {
@@ -93,14 +128,14 @@ int main() {
         CHECK(launches == 2 + 2 * 2 * 32);
         while (t.pending()) {
         }
-        CHECK(t.chosen(0, 1, 4, 100, 100, false) == 1);
+        CHECK(t.chosen(0, 1, 4, 0, 100, 100, false) == 1);
     }
     // 4. a failing launch: its status comes back, the shape keeps the policy
     {
         Tuner t(name);
         SimStream s;
         CHECK(call(t, &s, 3, 30, {1.0, 0.2, 0.3}, nullptr, /*fail_form=*/2) == 4);
-        CHECK(t.chosen(0, 1, 3, 30, 30, false) == 0);
+        CHECK(t.chosen(0, 1, 3, 0, 30, 30, false) == 0);
         CHECK(t.pending() == 0);
     }
     // 5. graph capture and the off switch: no measurement, the policy runs
@@ -110,12 +145,12 @@ int main() {
         s.capturing = true;
         int launches = 0;
         call(t, &s, 3, 31, {1.0, 0.2}, &launches);
-        CHECK(launches == 1 && t.chosen(0, 1, 3, 31, 31, false) == -2);
+        CHECK(launches == 1 && t.chosen(0, 1, 3, 0, 31, 31, false) == -2);
         s.capturing = false;
         CHECK(t.set_mode(0) == 1);
         launches = 0;
         call(t, &s, 3, 31, {1.0, 0.2}, &launches);
-        CHECK(launches == 1 && t.chosen(0, 1, 3, 31, 31, false) == -2);
+        CHECK(launches == 1 && t.chosen(0, 1, 3, 0, 31, 31, false) == -2);
         CHECK(t.set_mode(1) == 0);
     }
     // 5b. a capture that starts while a measurement is in flight: no event queries
@@ -131,7 +166,7 @@ int main() {
         CHECK(launches == 5);
         s.capturing = false;
         call(t, &s, 4, 44, {1.0, 0.3}, nullptr);  // first query after the capture: still in flight
-        CHECK(t.chosen(0, 1, 4, 44, 44, false) == 1);
+        CHECK(t.chosen(0, 1, 4, 0, 44, 44, false) == 1);
         tunersim::not_ready_queries() = 2;
     }
     // 6. many threads, many shapes, each thread on its own stream and device
@@ -166,10 +201,145 @@ int main() {
         }
         for (int dev = 0; dev < 2; ++dev)
             for (int k = 0; k < kShapes; ++k) {
-                const int c = t.chosen(dev, 1, 8 + k, 1000 + k, 1000 + k, false);
+                const int c = t.chosen(dev, 1, 8 + k, 0, 1000 + k, 1000 + k, false);
                 CHECK(c == -2 || c == expect[k]);  // -2: this device never saw the shape
             }
     }
+    // 7. client counts share a power-of-two bucket: a shape measured at 1000
+    //    clients runs its decision at 1024 without a measurement; 1025 measures
+    {
+        Tuner t(name);
+        SimStream s;
+        const std::vector<double> cost = {1.0, 0.4};
+        call(t, &s, 1000, 500, cost, nullptr);
+        drain(t);
+        int launches = 0;
+        call(t, &s, 1024, 500, cost, &launches);
+        CHECK(launches == 1 && t.chosen(0, 1, 513, 0, 500, 500, false) == 1);
+        launches = 0;
+        call(t, &s, 1025, 500, cost, &launches);
+        CHECK(launches > 1);
+        drain(t);
+    }
+    // 8. the cache file: a decision of one process is the first call's form in the next
+    char dir[] = "/tmp/fa_tuner_stress_XXXXXX";
+    CHECK(mkdtemp(dir) != nullptr);
+    const std::string path = std::string(dir) + "/sub/tuner.txt";  // the directory is created
+    {
+        Tuner a(name, from_name, ident, 3);
+        a.set_cache_path(path);
+        SimStream s;
+        call(a, &s, 64, 7000, {1.0, 0.9, 0.3}, nullptr);
+        drain(a);
+        CHECK(a.chosen(0, 1, 64, 0, 7000, 7000, false) == 2);
+        CHECK(count_lines(slurp(path)) == 1);
+        Tuner b(name, from_name, ident, 3);
+        b.set_cache_path(path);
+        int launches = 0;
+        call(b, &s, 60, 7000, {1.0, 0.9, 0.3}, &launches);  // same bucket
+        CHECK(launches == 1 && b.chosen(0, 1, 64, 0, 7000, 7000, false) == 2);
+        // another device identity does not take it
+        tunersim::current_device() = 1;
+        launches = 0;
+        call(b, &s, 64, 7000, {1.0, 0.9, 0.3}, &launches);
+        CHECK(launches > 1);
+        drain(b);
+        tunersim::current_device() = 0;
+        CHECK(count_lines(slurp(path)) == 2);
+    }
+    // 9. a stale ABI: the lines are ignored (measured again), and dropped on rewrite
+    {
+        Tuner c(name, from_name, ident, 4);
+        c.set_cache_path(path);
+        SimStream s;
+        int launches = 0;
+        call(c, &s, 64, 7000, {1.0, 0.2, 0.3}, &launches);
+        CHECK(launches > 1);
+        drain(c);
+        CHECK(c.chosen(0, 1, 64, 0, 7000, 7000, false) == 1);
+        const std::string after = slurp(path);
+        CHECK(count_lines(after) == 1 && after.find(" 4 1 64 f0 7000 7000 0 f1") != std::string::npos);
+    }
+    // 10. a corrupt file: garbage, truncated and out-of-range lines are skipped,
+    //     the valid line is used, and the rewrite keeps only valid lines
+    {
+        spit(path, std::string("garbage \x01\x02 here\n") + "fedavg-tune 1 sim:0 5 1 64 f0 9000 9000 0 f2\n" +
+                       "fedavg-tune 1 sim:0 5 1 64 f0 900\n" + "fedavg-tune 1 sim:0 5 1 63 f0 100 100 0 f1\n" +
+                       "fedavg-tune 1 sim:0 5 1 64 f0 100 50 0 f1\n" + "fedavg-tune 1 sim:0 5 1 64 f0 100 100 0 f9\n" +
+                       std::string(5000, 'x') + "\nfedavg-tune 1 sim:0 5 1 64 f0 800 800 0 f1 extra\n");
+        Tuner d(name, from_name, ident, 5);
+        d.set_cache_path(path);
+        SimStream s;
+        int launches = 0;
+        call(d, &s, 64, 9000, {1.0, 0.9, 0.95}, &launches);
+        CHECK(launches == 1 && d.chosen(0, 1, 64, 0, 9000, 9000, false) == 2);
+        call(d, &s, 64, 100, {1.0, 0.5}, &launches);  // the malformed lines for P = 100 did not count
+        CHECK(launches > 2);
+        drain(d);
+        const std::string after = slurp(path);
+        CHECK(count_lines(after) == 2 && after.find("garbage") == std::string::npos);
+    }
+    // 11. export / import: another process's decisions replace this one's
+    {
+        Tuner e(name, from_name, ident, 6), f(name, from_name, ident, 6);
+        e.set_cache_path("");
+        f.set_cache_path("");
+        SimStream s;
+        call(e, &s, 32, 3000, {1.0, 0.5, 0.2}, nullptr);
+        call(f, &s, 32, 3000, {1.0, 0.2, 0.5}, nullptr);
+        drain(e);
+        drain(f);
+        CHECK(e.chosen(0, 1, 32, 0, 3000, 3000, false) == 2 && f.chosen(0, 1, 32, 0, 3000, 3000, false) == 1);
+        const std::string text = e.export_text();
+        CHECK(count_lines(text) == 1);
+        CHECK(f.import_text(text + "not a line\n") == 1);
+        CHECK(f.chosen(0, 1, 32, 0, 3000, 3000, false) == 2);
+        // an imported shape this process has not seen runs without measuring
+        CHECK(f.import_text("fedavg-tune 1 sim:0 6 1 32 f0 4000 4000 1 f3\n") == 1);
+        int launches = 0;
+        f.run(1, 20, 4000, 4000, true, 0, 1e12, &s, [](std::vector<int>& v) { v = {0, 1, 2, 3}; },
+              [&](int form) {
+                  ++launches;
+                  CHECK(form == 3);
+                  return 0;
+              });
+        CHECK(launches == 1);
+        // import while a measurement is in flight: the events are released, the import wins
+        tunersim::not_ready_queries() = 50;
+        call(f, &s, 8, 5000, {1.0, 0.5}, nullptr);
+        CHECK(f.chosen(0, 1, 8, 0, 5000, 5000, false) == -1);
+        CHECK(f.import_text("fedavg-tune 1 sim:0 6 1 8 f0 5000 5000 0 f0\n") == 1);
+        CHECK(f.chosen(0, 1, 8, 0, 5000, 5000, false) == 0);
+        tunersim::not_ready_queries() = 2;
+    }
+    // 12. several processes (tuners) deciding shapes at once: every line survives the merges
+    {
+        const std::string p2 = std::string(dir) + "/many.txt";
+        std::vector<std::thread> th;
+        for (int i = 0; i < 6; ++i)
+            th.emplace_back([&, i] {
+                Tuner t(name, from_name, ident, 7);
+                t.set_cache_path(p2);
+                SimStream s;
+                for (int k = 0; k < 10; ++k) call(t, &s, 16, 20000 + 10 * i + k, {1.0, 0.3}, nullptr);
+                drain(t);
+            });
+        for (auto& x : th) x.join();
+        CHECK(count_lines(slurp(p2)) == 60);
+        Tuner g(name, from_name, ident, 7);
+        g.set_cache_path(p2);
+        SimStream s;
+        int launches = 0;
+        for (int i = 0; i < 6; ++i)
+            for (int k = 0; k < 10; ++k) call(g, &s, 16, 20000 + 10 * i + k, {1.0, 0.3}, &launches);
+        CHECK(launches == 60);
+        unlink(p2.c_str());
+        unlink((p2 + ".lock").c_str());
+    }
+    unlink(path.c_str());
+    unlink((path + ".lock").c_str());
+    rmdir((std::string(dir) + "/sub").c_str());
+    rmdir(dir);
     CHECK(tunersim::live_events().load() == 0);  // every measurement's events are released
     if (g_fail) {
         fprintf(stderr, "%d failures\n", g_fail);
