@@ -101,6 +101,9 @@ def parse():
                     help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
                          "left exposed after the step's folds); 1 = equal rounds.  Default with several rounds: "
                          "the layout for the dtype (DEFAULT_TAIL)")
+    ap.add_argument("--per-round-launches", action="store_true",
+                    help="at N > 1: one fold launch per exchange round (round 3's step) instead of the whole step in "
+                         "one launch with each round's all-gather started behind its completion flag")
     ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
                          "rounds: shares 1, 1, 0.5, 0.25)")
@@ -408,13 +411,30 @@ def main():
     # the first aggregation rounds of a deployment would
     L = _lib.load()
     tune_calls = 0
-    if args.variant == 0 and L.fa_set_autotune(-1) == 1:
+    one_launch = dist_on and rounds > 1 and args.variant == 0 and not args.per_round_launches
+    if args.variant == 0 and L.fa_set_autotune(-1) == 1 and not one_launch:
         for tune_calls in range(1, 201):
             for k in range(rounds):
                 wl.launch(0, k)
             torch.cuda.synchronize()
             if L.fa_autotune_pending() == 0:
                 break
+
+    # every rank runs rank 0's measured forms (the tuner measures per process:
+    # ranks could otherwise fold the same slot shape with different kernels);
+    # what each rank had chosen on its own is reported
+    forms_by_rank, forms_agree = None, None
+    if dist_on and world > 1 and args.variant == 0 and not one_launch:
+        kind = 1 if wl.dtype == "f32" else 2
+        mine = {str(w): L.fa_fold_form(kind, wl.N, w, wl.ldx, 1 if wl.scored else 0, stream.cuda_stream).decode()
+                for w in dict.fromkeys(lay.widths)}
+        forms_by_rank = [None] * world
+        dist.all_gather_object(forms_by_rank, mine)
+        forms_agree = all(f == forms_by_rank[0] for f in forms_by_rank)
+        text = [_lib.tune_export() if rank == 0 else None]
+        dist.broadcast_object_list(text, src=0)
+        if rank != 0:
+            _lib.tune_import(text[0])
 
     if args.sweep and rank == 0:
         nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()
@@ -448,9 +468,39 @@ def main():
     # the exchanged model: fp32 result for fp32 updates, the RNE bf16 result
     # for bf16 updates (2 B/param over xGMI: half the bytes of the fp32 result)
     send = wl.out if wl.dtype == "f32" else wl.out_bf16
+    if one_launch:
+        from fedlesscan_amd import engine
+        from fedlesscan_amd.sharding import gather_stream
+        gs = gather_stream(dev)
+        offs = [lay.offset(k) for k in range(rounds + 1)]
+
+    def step_one_launch(ev=None):
+        """The whole step in one fold launch; round k's all-gather on the gather
+        stream behind a wait for round k's completion flag (mid-launch)."""
+        if ev is not None:
+            ev[0][0][0].record(stream)
+        r = engine.fold_rounds(wl.X, wl.weights, wl.scores, offs, out=wl.out, out_bf16=wl.out_bf16)
+        if ev is not None:
+            ev[0][0][1].record(stream)
+        works = []
+        for k in range(rounds):
+            engine.wait_round(r, k, gs)
+            lo, hi = lay.round_range(k)
+            with torch.cuda.stream(gs):
+                w = gather_into(full[lo:hi], send[lay.offset(k):lay.offset(k + 1)], None, async_op=True)
+            if w is not None:
+                works.append(w)
+        for w in works:
+            w.wait()  # the fold stream waits for the RCCL stream
+        stream.wait_stream(gs)
+        if ev is not None:
+            ev[1].record(stream)
 
     def step(ev=None):
         """ev = (fold events per round, end event) for the timed steps."""
+        if one_launch:
+            step_one_launch(ev)
+            return
         works = []
         for k in range(rounds):
             if ev is not None:
@@ -504,7 +554,15 @@ def main():
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
-    if dist_on:
+    if dist_on and one_launch:
+        # one fold launch per step: its span (events around it), and the
+        # exchange left exposed after it (from the launch's end to the step's)
+        kern_ms = [folds[0][0].elapsed_time(folds[0][1]) for folds, _ in evs]
+        exposed_ms = [folds[0][1].elapsed_time(end) for folds, end in evs]
+        kern_avg = float(np.mean(kern_ms))
+        exposed_avg = float(np.mean(exposed_ms))
+        round_ms = [float(np.median(kern_ms))]
+    elif dist_on:
         kern_ms = [sum(e0.elapsed_time(e1) for e0, e1 in folds) for folds, _ in evs]
         # the exchange left exposed: from the last fold's end to the end of the step
         exposed_ms = [folds[-1][1].elapsed_time(end) for folds, end in evs]
@@ -518,11 +576,16 @@ def main():
         kern_avg = region[0].elapsed_time(region[1]) / args.steps  # per fold call, launch gaps included
         exposed_avg = 0.0
         round_ms = None
+    timeouts = None
     if dist_on:
         t = torch.tensor([kern_avg, exposed_avg, *round_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
+    if one_launch:  # a round wait that gave up (never expected) would make the gather unordered
+        t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev)))], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        timeouts = int(t.item())
 
     # streaming-read ceiling over the same HBM bytes (contiguous, no fold)
     # byte-level sweep: bf16 input is read as the same bytes viewed as fp32 quads
@@ -599,12 +662,19 @@ def main():
                 "rounds": rounds,
                 "round_widths": lay.widths,
                 "fold_stream": "high priority" if dist_on else "default",
+                "fold_launch": ("one launch per step (fa_fedavg_*_rounds), each round's all-gather behind its "
+                                "completion flag" if one_launch else
+                                "one launch per round" if dist_on else "one launch"),
+                "fold_form_by_rank_own_choice": forms_by_rank,
+                "fold_form_ranks_agreed": forms_agree,
+                "fold_form_rank0_broadcast": bool(dist_on and world > 1 and args.variant == 0 and not one_launch),
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
                 # the kernel form the product's fp32 auto fold takes for one launch of this rank
                 # the kernel form each distinct slot width ran (the tuner's measured choice), and the
                 # shape policy's form for the first slot (what runs with FEDAVG_AUTOTUNE=0)
-                "fold_form": ({str(w): L.fa_fold_form(1 if wl.dtype == "f32" else 2, wl.N, w, wl.ldx,
+                "fold_form": (L.fa_rounds_form(1 if wl.dtype == "bf16" else 0).decode() if one_launch else
+                              {str(w): L.fa_fold_form(1 if wl.dtype == "f32" else 2, wl.N, w, wl.ldx,
                                                       1 if wl.scored else 0, stream.cuda_stream).decode()
                                for w in dict.fromkeys(lay.widths)} if args.variant == 0 else None),
                 "fold_policy": (B.fa_f32_pick_name(wl.N, lay.sub, 0).decode()
@@ -637,7 +707,9 @@ def main():
             # per-rank split of a step at N > 1 (max over ranks): the fold kernels,
             # and the all-gather left exposed after the last fold of the step
             "fold_ms": round(kern_avg, 4),
-            "fold_ms_per_round": round_ms,
+            "fold_ms_per_round": round_ms if not one_launch else None,
+            "fold_ms_per_step_launch_median": round_ms[0] if one_launch else None,
+            "round_wait_timeouts": timeouts,
             "gather_exposed_ms": round(exposed_avg, 4) if dist_on else None,
             "gather_bytes_per_rank": (lay.padded_total * (4 if wl.dtype == "f32" else 2)
                                       * (world - 1) // world) if dist_on else 0,

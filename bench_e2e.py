@@ -50,6 +50,7 @@ MNIST_LIKE = [(5, 5, 1, 32), (32,), (5, 5, 32, 64), (64,), (1024, 512), (512,), 
 
 def make_blobs(N, P, seed):
     from oracle import oracle_lib as OL  # fast host generator (test/bench infrastructure)
+    from fedlesscan_amd.npz import write_npz  # byte-identical to np.savez, threaded CRC
     blobs = []
     for i in range(N):
         row = OL.synth_f32(seed, 1, P, row0=i)[0]
@@ -57,10 +58,28 @@ def make_blobs(N, P, seed):
         cuts = [0, P // 64, P // 8, P // 2, P]
         layers = [row[cuts[k]:cuts[k + 1]].reshape(-1, 1) if k % 2 else row[cuts[k]:cuts[k + 1]]
                   for k in range(4)]
-        f = io.BytesIO()
-        np.savez(f, *layers)
-        blobs.append(f.getvalue())
+        blob = write_npz(layers)
+        if blob is None:
+            f = io.BytesIO()
+            np.savez(f, *layers)
+            blob = f.getvalue()
+        blobs.append(blob)
     return blobs
+
+
+def check_columns(out, N, P, seed, cards, ncols):
+    """GPU result vs the C oracle (the reference op order, fed_avg_aggregator.py:31-41)
+    on the first and the last `ncols` columns, regenerated on the host."""
+    from oracle import oracle_lib as OL
+    flat = np.concatenate([np.asarray(x).reshape(-1) for x in out])
+    a = np.array(cards, np.float32)
+    div = np.float32(sum(cards))
+    ok = True
+    for c0 in sorted({0, max(0, P - ncols)}):
+        nc = min(ncols, P - c0)
+        exp = OL.fedavg_f32(OL.synth_f32(seed, N, nc, col0=c0), a, div)
+        ok &= bool(np.array_equal(flat[c0:c0 + nc].view(np.uint32), exp.view(np.uint32)))
+    return ok
 
 
 def results(blobs, cards):
@@ -76,6 +95,8 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check-cols", type=int, default=0,
+                    help="with --no-cpu: check the first and last K output columns against the C oracle")
     ap.add_argument("--bson", action="store_true", help="start from BSON documents in the result store")
     ap.add_argument("--pinned-store", action="store_true", help="with --bson: documents in page-locked memory")
     ap.add_argument("--devices", default="",
@@ -158,6 +179,11 @@ def main():
         "ingest_rows": routes,
         "devices": a.devices or "current GPU",
     }
+    if a.no_cpu and a.check_cols > 0:
+        t0 = time.perf_counter()
+        res["bit_exact_column_sample"] = check_columns(out, N, P, a.seed, cards, a.check_cols)
+        res["column_sample"] = f"first and last {min(a.check_cols, P)} columns vs the C oracle"
+        res["check_s"] = round(time.perf_counter() - t0, 1)
     if not a.no_cpu:
         if store is not None:
             import bson  # pymongo's codec: the reference's own decode (CPU leg only)

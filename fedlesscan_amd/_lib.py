@@ -61,6 +61,7 @@ _PROTOS = {
     "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
     "fa_rounds_wait": (_int, [_vp, _int, _vp]),
     "fa_rounds_timeouts": (_int, [_vp]),
+    "fa_rounds_form": (ctypes.c_char_p, [_int]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i64": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),

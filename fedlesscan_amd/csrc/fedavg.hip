@@ -284,6 +284,8 @@ int fa_fedavg_f32_rounds(fa_rounds* r, const float* X, int64_t N, int64_t ldx, c
                        offsets);
 }
 
+const char* fa_rounds_form(int bf16) { return step_form_name(pick_step(bf16 != 0)); }
+
 int fa_rounds_wait(fa_rounds* r, int round, void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
     if (!r->launched) return fail(FA_ERR_ARG, "fa_rounds_wait: the last rounds fold was not launched");

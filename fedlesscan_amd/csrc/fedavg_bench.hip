@@ -525,9 +525,7 @@ int fa_fedavg_f32_ptrs_form(const float* const* xi, int64_t N, int64_t P, const 
     return check_launch("fa_fedavg_f32_ptrs_form");
 }
 int fa_num_step_forms(void) { return kNumStepForms; }
-const char* fa_step_form_name(int form) {
-    return (form >= 0 && form < kNumStepForms) ? step_form_name((StepForm)form) : "";
-}
+const char* fa_step_form_name(int form) { return step_form_name(form); }
 
 int fa_bench_rounds_create(void** r, int device) {
     if (!r) return fail(FA_ERR_ARG, "null handle");
@@ -574,9 +572,8 @@ int fa_fedavg_rounds_form(void* r, int form, const void* X, int64_t N, int64_t l
     if (!r) return fail(FA_ERR_ARG, "null rounds state");
     if (form < 0 || form >= kNumStepForms) return fail(FA_ERR_ARG, "unknown step form %d", form);
     StreamDevice on_stream_device(stream);
-    const StepForm f = (StepForm)form;
-    return launch_step(*static_cast<RoundsState*>(r), f, (hipStream_t)stream, X, N, ldx, a, s, divisor, out,
-                       step_form_bf16(f) ? out_bf16 : nullptr, rounds, offsets);
+    return launch_step(*static_cast<RoundsState*>(r), form, (hipStream_t)stream, X, N, ldx, a, s, divisor, out,
+                       kStepSpecs[form].bf16 ? out_bf16 : nullptr, rounds, offsets);
 }
 
 int fa_bench_rounds_wait(void* r, int round, void* stream) {

@@ -1555,53 +1555,101 @@ __global__ __launch_bounds__(B) void k_fold_f32_dynp(
 // the launch's epoch.  The exchange of round k is issued behind
 // k_wait_round on another stream (a one-lane kernel that polls the flag and
 // returns), so it starts mid-launch, as soon as round k is complete.
-//   Ordering: every thread releases its tile's stores (device-scope fence)
-//   before the block counts the tile; the block that counts a round's last
-//   tile fences again (acquire of the other blocks' counts, release of the
-//   flag) before it stores the epoch; the waiter loads the flag with acquire.
-//   A waiter gives up after `max_ticks` of the device wall clock (never an
-//   endless spin), recording the timeout in the signal words.
+//   Publication is per block and round, not per tile: when a block's next
+//   tile belongs to a later round, every wave waits for its stores, and one
+//   lane writes the XCD's L2 back (agent-scope release), waits for that, and
+//   adds the block's tile count of the round to the round's counter; the add
+//   that completes the round stores the epoch into the round's flag (an
+//   agent-scope atomic).  A release per tile cost 0.3-0.6 ms per C4 rank step
+//   (profiles/r04_step/).  The waiter polls the flag with relaxed agent-scope
+//   loads; the exchange kernels behind it read the results after their own
+//   launch acquire.  A waiter gives up after `max_ticks` of the device wall
+//   clock (never an endless spin), counting a timeout in the signal words.
 // ---------------------------------------------------------------------------
-constexpr int kMaxRounds = 8;
-struct RoundTable {
-    int64_t tile_end[kMaxRounds];  // round k's tiles are [tile_end[k-1], tile_end[k]) of the launch
-    int64_t col0[kMaxRounds];      // its first local column
-    int64_t width[kMaxRounds];     // its columns
-    int rounds;
+constexpr int kMaxRounds = 8, kMaxSegs = 2 * kMaxRounds;
+// The launch's tiles, in column order: segment g covers local columns
+// [col0[g], col0[g] + width[g]) of round round[g] with wide tiles (small[g] = 0)
+// or narrow ones (1); its tiles are [seg_end[g-1], seg_end[g]) of the launch.
+// Tiles [0, static_tiles) are dealt statically -- block b folds b, b + G, ...
+// (G blocks: every block's share of every round, rounds in order, blocks in
+// lock-step over adjacent tiles as in the grid-stride forms) -- and the rest,
+// the step's last columns in narrow tiles, go to whichever block asks the
+// counter next.  A block that lags (it shares its CU with other kernels)
+// finishes its static share late and takes few or none of the dynamic tiles.
+struct StepTable {
+    int64_t seg_end[kMaxSegs];
+    int64_t col0[kMaxSegs];
+    int64_t width[kMaxSegs];
+    int32_t round[kMaxSegs];
+    int32_t small[kMaxSegs];
+    int64_t round_tiles[kMaxRounds];
+    int64_t static_tiles;
+    int32_t segs;
+    int32_t rounds;
 };
-// signal words: [0] next tile, [1] blocks done, [2, 2+R) tiles done per round,
+// signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
 // [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
 constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
 
 template <class Tile>
-__device__ __forceinline__ void step_tiles(const RoundTable& R, unsigned int* sig, unsigned int epoch, Tile tile) {
+__device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Tile tile) {
     __shared__ unsigned int nxt[2];
-    const int64_t ntiles = R.tile_end[R.rounds - 1];
-    int64_t t = blockIdx.x;
+    const int64_t ntiles = T.seg_end[T.segs - 1];
+    const int64_t Ts = T.static_tiles;
+    const int64_t G = gridDim.x;
     int p = 0;
-    while (t < ntiles) {
-        unsigned int nx = 0;
-        if (threadIdx.x == 0) nx = atomicAdd(&sig[0], 1u);
-        int k = 0;
-        while (k + 1 < R.rounds && t >= R.tile_end[k]) ++k;
-        const int64_t t0 = k ? R.tile_end[k - 1] : 0;
-        tile(k, t - t0);
-        __threadfence();  // this thread's stores of the tile, device-wide
-        if (threadIdx.x == 0) nxt[p] = nx;
-        __syncthreads();  // every thread's stores released before the block counts the tile
-        if (threadIdx.x == 0) {
-            const unsigned int nk = (unsigned int)(R.tile_end[k] - t0);
-            if (atomicAdd(&sig[kSigDone + k], 1u) == nk - 1) {  // the round's last tile
-                atomicExch(&sig[kSigDone + k], 0u);
-                __threadfence();
-                atomicExch(&sig[kSigFlag + k], epoch);
-            }
-        }
-        t = (int64_t)nxt[p] + gridDim.x;
+    int64_t t = blockIdx.x;
+    if (t >= Ts) {  // no static tile for this block: its first tile from the counter
+        if (threadIdx.x == 0) nxt[p] = atomicAdd(&sig[0], 1u);
+        __syncthreads();
+        t = Ts + nxt[p];
         p ^= 1;
     }
+    int g = 0;
+    while (g + 1 < T.segs && t >= T.seg_end[g]) ++g;
+    int k = T.round[g];
+    unsigned int cnt = 0;  // this block's tiles of round k so far
+    while (t < ntiles) {
+        const bool dyn_next = t + G >= Ts;  // the next tile comes from the counter
+        unsigned int nx = 0;
+        if (dyn_next && threadIdx.x == 0) nx = atomicAdd(&sig[0], 1u);  // fetched a tile ahead
+        tile(g, t - (g ? T.seg_end[g - 1] : 0));
+        ++cnt;
+        int64_t tn = t + G;
+        if (dyn_next) {
+            if (threadIdx.x == 0) nxt[p] = nx;
+            __syncthreads();
+            tn = Ts + nxt[p];
+            p ^= 1;
+        }
+        int gn = g;
+        while (gn < T.segs && tn >= T.seg_end[gn]) ++gn;  // T.segs: no tile left
+        const int kn = gn < T.segs ? T.round[gn] : kMaxRounds;
+        if (kn != k) {
+            // The block leaves round k (its tiles come in round order): publish
+            // its tiles of the round once (MI355X_MICROARCH.md, valid producer
+            // form): every storing wave waits for its stores, a barrier, then
+            // one lane writes the XCD's L2 back (agent release) and, after
+            // waiting for that, counts the tiles with an agent-scope add.  The
+            // add that completes the round raises its flag.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned int nk = (unsigned int)T.round_tiles[k];
+                if (atomicAdd(&sig[kSigDone + k], cnt) + cnt == nk) {  // the round's last tiles
+                    atomicExch(&sig[kSigDone + k], 0u);
+                    atomicExch(&sig[kSigFlag + k], epoch);
+                }
+            }
+            cnt = 0;
+            k = kn;
+        }
+        t = tn;
+        g = gn < T.segs ? gn : g;
+    }
     if (threadIdx.x == 0) {
-        __threadfence();
         if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {
             atomicExch(&sig[0], 0u);
             atomicExch(&sig[1], 0u);
@@ -1609,25 +1657,32 @@ __device__ __forceinline__ void step_tiles(const RoundTable& R, unsigned int* si
     }
 }
 
-template <int U, int C, bool SCORED, int B>
+// wide tiles: UB rows ahead x CB octets (quads) per lane; narrow: US x CS
+template <int UB, int CB, int US, int CS, bool SCORED, int B>
 __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
-    const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, RoundTable R,
+    const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
     unsigned int* sig, unsigned int epoch) {
-    step_tiles(R, sig, epoch, [&](int k, int64_t bid) {
-        const int64_t c0 = R.col0[k];
-        bf16_tile<U, C, SCORED, B>(bid, X + c0, N, R.width[k], ldx, a, s, divisor, out + c0, outb ? outb + c0 : nullptr);
+    step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        uint16_t* ob = outb ? outb + c0 : nullptr;
+        if (T.small[g]) bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
+        else bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
     });
 }
 
-template <int U, int C, bool SCORED, int B>
+template <int UB, int CB, int US, int CS, bool SCORED, int B>
 __global__ __launch_bounds__(B) void k_fold_f32_step(
     const float* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
-    float divisor, float* __restrict__ out, RoundTable R, unsigned int* sig, unsigned int epoch) {
-    step_tiles(R, sig, epoch, [&](int k, int64_t bid) {
-        const int64_t c0 = R.col0[k];
-        fold_tile<U, C, true, SCORED, false, true, true, B>(bid, X + c0, N, R.width[k], ldx, a, s, nullptr, divisor,
-                                                           out + c0);
+    float divisor, float* __restrict__ out, StepTable T, unsigned int* sig, unsigned int epoch) {
+    step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        if (T.small[g])
+            fold_tile<US, CS, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                                 divisor, out + c0);
+        else
+            fold_tile<UB, CB, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                                 divisor, out + c0);
     });
 }
 
@@ -1637,7 +1692,9 @@ __global__ __launch_bounds__(64) void k_wait_round(const unsigned int* flag, uns
                                                    long long max_ticks) {
     if (threadIdx.x != 0) return;
     const long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0) {
+    // relaxed agent-scope (L2-served) polls: the exchange kernels that follow
+    // this one read the round's results after their own launch acquire
+    while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0) {
         if (wall_clock64() - t0 > max_ticks) {
             atomicAdd(timeouts, 1u);
             return;
@@ -2278,35 +2335,41 @@ void launch_f32_dynp(hipStream_t st, int per_cu, bool sc, const float* X, int64_
 }
 
 // ---- one launch per exchange step (k_*_step, fa_fedavg_*_rounds) ---------
-// The step forms: rows ahead x octets (quads) per lane, 256-thread blocks,
-// one block per CU.
-enum class StepForm { kBf16U8C2, kBf16U16C2, kBf16U8C4, kBf16U4C4, kF32U8C4, kF32U8C2, kF32U16C2, kF32U16C1 };
-constexpr int kNumStepForms = (int)StepForm::kF32U16C1 + 1;
-inline const char* step_form_name(StepForm f) {
-    switch (f) {
-        case StepForm::kBf16U8C2: return "bf16_step_u8c2";
-        case StepForm::kBf16U16C2: return "bf16_step_u16c2";
-        case StepForm::kBf16U8C4: return "bf16_step_u8c4";
-        case StepForm::kBf16U4C4: return "bf16_step_u4c4";
-        case StepForm::kF32U8C4: return "f32_step_u8c4";
-        case StepForm::kF32U8C2: return "f32_step_u8c2";
-        case StepForm::kF32U16C2: return "f32_step_u16c2";
-        case StepForm::kF32U16C1: return "f32_step_u16c1";
-    }
-    return "";
-}
-inline bool step_form_bf16(StepForm f) { return (int)f <= (int)StepForm::kBf16U4C4; }
-inline int step_form_lanes_units(StepForm f) {  // column units (octets / quads) per tile
-    switch (f) {
-        case StepForm::kBf16U8C2: case StepForm::kBf16U16C2: case StepForm::kF32U8C2: case StepForm::kF32U16C2:
-            return kBlock * 2;
-        case StepForm::kBf16U8C4: case StepForm::kBf16U4C4: case StepForm::kF32U8C4: return kBlock * 4;
-        case StepForm::kF32U16C1: return kBlock;
-    }
-    return kBlock;
-}
-// The policy's step form (profiles/r04_dyn/): bf16 C4 rank slots, fp32 C3 rank slots.
-inline StepForm pick_step(bool bf16) { return bf16 ? StepForm::kBf16U8C2 : StepForm::kF32U8C4; }
+// A step form: wide tiles (UB rows ahead x CB octets / quads per lane) dealt
+// statically, and a dynamic pool of narrow tiles (US x CS) over the step's
+// last columns, sized in passes of the grid over wide tiles (pool100 = 100:
+// one pass; -1: every tile dynamic, wide).  256-thread blocks, one per CU.
+struct StepSpec {
+    const char* name;
+    bool bf16;
+    int ub, cb, us, cs, pool100;
+    int grid100;  // blocks per 100 CUs (100: one per CU)
+};
+constexpr StepSpec kStepSpecs[] = {
+    {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
+    {"bf16_step_sd_u8c4_p75", true, 8, 4, 16, 1, 75, 100},
+    {"bf16_step_sd_u8c4w_p100", true, 8, 4, 8, 4, 100, 100},
+    {"bf16_step_sd_u16c2_p150", true, 16, 2, 16, 2, 150, 100},
+    {"bf16_step_sd_u8c2w_p150", true, 8, 2, 8, 2, 150, 100},
+    {"bf16_step_u8c4", true, 8, 4, 8, 4, -1, 100},
+    {"bf16_step_u16c2", true, 16, 2, 16, 2, -1, 100},
+    {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75, 100},
+    {"f32_step_sd_u8c4_p150", false, 8, 4, 16, 1, 150, 100},
+    {"f32_step_sd_u8c4_p300", false, 8, 4, 16, 1, 300, 100},
+    {"f32_step_u8c4", false, 8, 4, 8, 4, -1, 100},
+    // fewer blocks than CUs: the band forms' balanced launches run C4's slots on
+    // ~200 blocks and were faster there than a block on every CU
+    {"bf16_step_sd_u8c4w_p100_g80", true, 8, 4, 8, 4, 100, 80},
+    {"bf16_step_sd_u8c4w_p100_g90", true, 8, 4, 8, 4, 100, 90},
+    {"bf16_step_u8c4_g80", true, 8, 4, 8, 4, -1, 80},
+    {"bf16_step_sd_u8c4_p150_g80", true, 8, 4, 16, 1, 150, 80},
+    {"f32_step_sd_u8c4_p75_g80", false, 8, 4, 16, 1, 75, 80},
+    {"f32_step_sd_u8c4_p75_g90", false, 8, 4, 16, 1, 75, 90},
+};
+constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
+inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
+// The policy's step form (profiles/r04_step/): bf16 C4 rank slots, fp32 C3 rank slots.
+inline int pick_step(bool bf16) { return bf16 ? 0 : 7; }
 
 // The per-launch state of fa_fedavg_*_rounds: the signal words in device
 // memory and the host epoch (fa_rounds in fedavg_hip.h).
@@ -2319,14 +2382,66 @@ struct RoundsState {
     long long max_ticks = 0;      // a waiter's give-up time in wall-clock ticks
 };
 
-// Enqueue one step launch: rounds slots at local columns [offsets[k], offsets[k+1]).
-inline int launch_step(RoundsState& R, StepForm f, hipStream_t st, const void* X, int64_t N, int64_t ldx,
+// The segments of one step launch over `rounds` slots at local columns
+// [offsets[k], offsets[k+1]): every round's columns in wide tiles, except the
+// last pool columns of the step (cut at wide-tile boundaries, walking back
+// from the last round) in narrow tiles.  FA status.
+inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offsets, int64_t ldx, int64_t grid,
+                            StepTable& T) {
+    const int64_t ucols = sp.bf16 ? 8 : 4;  // columns per octet / quad
+    const int64_t wide_cols = (int64_t)kBlock * sp.cb * ucols, narrow_cols = (int64_t)kBlock * sp.cs * ucols;
+    T = StepTable{};
+    T.rounds = rounds;
+    int64_t pool = sp.pool100 < 0 ? INT64_MAX : (sp.pool100 * grid * wide_cols) / 100;  // columns
+    int64_t split[kMaxRounds];  // round k: columns [0, split) wide-static, [split, width) narrow-dynamic
+    for (int k = rounds - 1; k >= 0; --k) {
+        const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
+        if (c0 < 0 || w < 1 || c0 % ucols || offsets[k + 1] > ldx)
+            return fail(FA_ERR_ARG, "round %d: columns [%lld, %lld) (every round non-empty, %lld-aligned, within ldx)",
+                        k, (long long)c0, (long long)offsets[k + 1], (long long)ucols);
+        if (pool <= 0) { split[k] = w; continue; }
+        if (pool >= w) { split[k] = 0; pool -= w; continue; }
+        split[k] = ((w - pool) / wide_cols) * wide_cols;  // the static part ends on a wide-tile boundary
+        pool = 0;
+    }
+    if (sp.pool100 < 0)
+        for (int k = 0; k < rounds; ++k) split[k] = 0;
+    auto units = [&](int64_t w) { return sp.bf16 ? (w >> 3) + ((w & 7) ? 1 : 0) : (w >> 2) + ((w & 3) ? 1 : 0); };
+    int64_t total = 0;
+    // static segments first (all of them precede every dynamic one in column
+    // order: only a suffix of the step is dynamic), then the dynamic ones
+    const bool wide_dyn = sp.pool100 < 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int k = 0; k < rounds; ++k) {
+            const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
+            const int64_t lo = pass == 0 ? 0 : split[k], hi = pass == 0 ? split[k] : w;
+            if (hi <= lo) continue;
+            const int64_t per = (pass == 0 || wide_dyn) ? (int64_t)kBlock * sp.cb : (int64_t)kBlock * sp.cs;
+            const int g = T.segs++;
+            total += (units(hi - lo) + per - 1) / per;
+            T.seg_end[g] = total;
+            T.col0[g] = c0 + lo;
+            T.width[g] = hi - lo;
+            T.round[g] = k;
+            T.small[g] = (pass == 1 && !wide_dyn) ? 1 : 0;
+            T.round_tiles[k] += (units(hi - lo) + per - 1) / per;
+            if (pass == 0) T.static_tiles = total;
+        }
+    (void)narrow_cols;
+    if (total > 0x7FFFFFFF) return fail(FA_ERR_ARG, "rounds fold: too many tiles");
+    return FA_OK;
+}
+
+// Enqueue one step launch of form f over `rounds` slots at local columns
+// [offsets[k], offsets[k+1]).
+inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int64_t N, int64_t ldx,
                        const float* a, const float* s, float divisor, float* out, uint16_t* outb, int rounds,
                        const int64_t* offsets) {
     R.launched = false;
+    if (f < 0 || f >= kNumStepForms) return fail(FA_ERR_ARG, "unknown step form %d", f);
     if (rounds < 1 || rounds > kMaxRounds || !offsets) return fail(FA_ERR_ARG, "rounds must be 1..%d", kMaxRounds);
-    const bool bf = step_form_bf16(f);
-    const int64_t col_align = bf ? 8 : 4;
+    const StepSpec& sp = kStepSpecs[f];
+    const int64_t col_align = sp.bf16 ? 8 : 4;
     if (!X || !a || !out || N < 1) return fail(FA_ERR_ARG, "null X/a/out or N < 1");
     if (ldx % col_align || !aligned16(X) || !aligned16(out) || (outb && !aligned16(outb)))
         return fail(FA_ERR_ARG, "rounds fold needs 16-B aligned X/out and ldx %% %lld == 0", (long long)col_align);
@@ -2335,50 +2450,36 @@ inline int launch_step(RoundsState& R, StepForm f, hipStream_t st, const void* X
         (void)hipGetLastError();
         return fail(FA_ERR_ARG, "rounds fold cannot be captured (its epochs would replay)");
     }
-    RoundTable T{};
-    T.rounds = rounds;
-    const int64_t per_tile = step_form_lanes_units(f);
-    int64_t total = 0;
-    for (int k = 0; k < rounds; ++k) {
-        const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
-        if (c0 < 0 || w < 1 || c0 % col_align || offsets[k + 1] > ldx)
-            return fail(FA_ERR_ARG, "round %d: columns [%lld, %lld) (every round non-empty, %lld-aligned, within ldx)",
-                        k, (long long)c0, (long long)offsets[k + 1], (long long)col_align);
-        const int64_t units = bf ? (w >> 3) + ((w & 7) ? 1 : 0) : (w >> 2) + ((w & 3) ? 1 : 0);
-        total += (units + per_tile - 1) / per_tile;
-        T.tile_end[k] = total;
-        T.col0[k] = c0;
-        T.width[k] = w;
-    }
-    if (total > 0x7FFFFFFF) return fail(FA_ERR_ARG, "rounds fold: too many tiles");
-    int64_t grid = cu_count();
+    int64_t grid = (cu_count() * sp.grid100 + 99) / 100;
+    StepTable T;
+    int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
+    if (rc) return rc;
+    const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
     const float* Xf = static_cast<const float*>(X);
-#define FA_STB(U, C)                                                                                           \
-    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<U, C, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
-                              Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);                          \
-    else hipLaunchKernelGGL((k_fedavg_bf16_step<U, C, false, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
-                            Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
-#define FA_STF(U, C)                                                                                          \
-    if (s) hipLaunchKernelGGL((k_fold_f32_step<U, C, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
-                              Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);                               \
-    else hipLaunchKernelGGL((k_fold_f32_step<U, C, false, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
-                            Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch)
+#define FA_STB(UB, CB, US, CS)                                                                                 \
+    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), \
+                              0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);                  \
+    else hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
+                            dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
+#define FA_STF(UB, CB, US, CS)                                                                                \
+    if (s) hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), \
+                              0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);                       \
+    else hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),             \
+                            dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch)
     switch (f) {
-        case StepForm::kBf16U8C2: FA_STB(8, 2); break;
-        case StepForm::kBf16U16C2: FA_STB(16, 2); break;
-        case StepForm::kBf16U8C4: FA_STB(8, 4); break;
-        case StepForm::kBf16U4C4: FA_STB(4, 4); break;
-        case StepForm::kF32U8C4: FA_STF(8, 4); break;
-        case StepForm::kF32U8C2: FA_STF(8, 2); break;
-        case StepForm::kF32U16C2: FA_STF(16, 2); break;
-        case StepForm::kF32U16C1: FA_STF(16, 1); break;
+        case 0: case 1: case 14: FA_STB(8, 4, 16, 1); break;
+        case 2: case 5: case 11: case 12: case 13: FA_STB(8, 4, 8, 4); break;
+        case 3: case 6: FA_STB(16, 2, 16, 2); break;
+        case 4: FA_STB(8, 2, 8, 2); break;
+        case 7: case 8: case 9: case 15: case 16: FA_STF(8, 4, 16, 1); break;
+        default: FA_STF(8, 4, 8, 4); break;
     }
 #undef FA_STB
 #undef FA_STF
-    const int rc = check_launch("rounds fold");
+    rc = check_launch("rounds fold");
     if (rc) return rc;
     R.epoch = epoch;
     R.rounds = rounds;

@@ -17,6 +17,7 @@ computed by libfedavg_hip.so on the GPU, or the call raises.
 """
 from __future__ import annotations
 
+import ctypes
 import operator
 import os
 import threading
@@ -288,6 +289,61 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
         _lib.call("fa_fedavg_f64", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
                   out.data_ptr(), st)
     return out
+
+
+_rounds_states: dict = {}
+_rounds_lock = threading.Lock()
+
+
+def rounds_state(device: torch.device) -> ctypes.c_void_p:
+    """The library's one-launch-per-step state (fa_rounds) of a device: its
+    launches must be ordered, so callers issue them on one stream per device
+    (sharding.fold_stream)."""
+    dev = torch.device(device)
+    with _rounds_lock:
+        h = _rounds_states.get(dev)
+        if h is None:
+            h = ctypes.c_void_p()
+            _lib.call("fa_rounds_create", ctypes.byref(h), dev.index if dev.index is not None else 0)
+            _rounds_states[dev] = h
+        return h
+
+
+def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], offsets: Sequence[int], *,
+                out: torch.Tensor, out_bf16: Optional[torch.Tensor] = None, total=None) -> ctypes.c_void_p:
+    """Every exchange round of a step in ONE launch (fa_fedavg_*_rounds): round
+    k folds the columns [offsets[k], offsets[k+1]) of X (fp32 or bf16 rows)
+    into the same columns of out (and of out_bf16, the RNE copy, for bf16 X),
+    on the current stream.  Returns the device's rounds state for
+    `wait_round`: the exchange of round k may start, on another stream, as soon
+    as round k is complete, while the launch goes on.  Same bits as
+    fold_stacked on each round's columns."""
+    N, W, ldx = _check_matrix(X)
+    if len(weights) != N or (scores is not None and len(scores) != N):
+        raise InvalidParameterShapeError(f"{N} rows but {len(weights)} weights")
+    dev = X.device
+    f = Factors.weak_f32(weights, scores, total) or Factors(weights, scores, np.dtype(np.float32), total=total)
+    if result_dtype(np.dtype(np.float32), list(weights), scores, total) != np.float32:
+        raise InvalidParameterShapeError("the rounds fold takes float32 factors (Python-number weights)")
+    a, s = f.to(dev)
+    rounds = len(offsets) - 1
+    offs = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    r = rounds_state(dev)
+    st = stream_ptr(dev)
+    if X.dtype == torch.bfloat16:
+        _lib.call("fa_fedavg_bf16_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                  out.data_ptr(), _ptr(out_bf16), rounds, offs, st)
+    elif X.dtype == torch.float32:
+        _lib.call("fa_fedavg_f32_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                  out.data_ptr(), rounds, offs, st)
+    else:
+        raise InvalidParameterShapeError(f"the rounds fold takes float32 or bfloat16 rows, got {X.dtype}")
+    return r
+
+
+def wait_round(state: ctypes.c_void_p, k: int, stream: torch.cuda.Stream) -> None:
+    """Enqueue on `stream` a wait for round k of the last fold_rounds launch."""
+    _lib.call("fa_rounds_wait", state, int(k), stream.cuda_stream)
 
 
 def _equal_stride_view(rows, host_ptrs: np.ndarray, P: int) -> Optional[torch.Tensor]:

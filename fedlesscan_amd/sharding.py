@@ -146,6 +146,7 @@ class SlotLayout:
 
 
 _fold_streams: dict = {}
+_gather_streams: dict = {}
 
 
 def fold_stream(device) -> torch.cuda.Stream:
@@ -159,6 +160,16 @@ def fold_stream(device) -> torch.cuda.Stream:
     s = _fold_streams.get(dev)
     if s is None:
         s = _fold_streams[dev] = torch.cuda.Stream(device=dev, priority=-1)
+    return s
+
+
+def gather_stream(device) -> torch.cuda.Stream:
+    """The stream a one-launch step issues its exchanges from (behind each
+    round's wait, sharding.ShardedAggregator.aggregate_slots)."""
+    dev = torch.device(device)
+    s = _gather_streams.get(dev)
+    if s is None:
+        s = _gather_streams[dev] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -188,14 +199,20 @@ class ShardedAggregator:
     fed_avg_aggregator.py:31-35).
     """
 
-    def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None):
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None,
+                 one_launch: bool = True):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        from . import engine
+        self.default_fold = fold is None
         if fold is None:
-            from . import engine
             fold = engine.fold_stacked
         self.fold = fold
+        # aggregate_slots folds every round of a step in one launch
+        # (engine.fold_rounds) and starts each round's exchange behind that
+        # round's completion flag; False: one fold launch per round
+        self.one_launch = one_launch
 
     def bounds(self, P: int) -> Tuple[int, int]:
         return bucket_bounds(P, self.world)[self.rank]
@@ -255,6 +272,15 @@ class ShardedAggregator:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
         if not X_local.is_cuda or layout.rounds == 1:
             return self._aggregate_slots(X_local, weights, scores, layout, out, total)
+        if self._one_launch_ok(X_local, weights, scores, layout, total):
+            caller = torch.cuda.current_stream(X_local.device)
+            fs = fold_stream(X_local.device)
+            fs.wait_stream(caller)
+            with torch.cuda.stream(fs):
+                full = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
+            caller.wait_stream(fs)
+            full.record_stream(caller)
+            return full
         # the rounds' folds on a high-priority stream of their own (fold_stream), ordered after
         # the caller's work and before the caller's later work
         caller = torch.cuda.current_stream(X_local.device)
@@ -265,6 +291,59 @@ class ShardedAggregator:
         caller.wait_stream(fs)
         full.record_stream(caller)
         return full
+
+    def _one_launch_ok(self, X_local, weights, scores, layout, total) -> bool:
+        import numpy as np
+
+        from .engine import result_dtype
+        if not (self.one_launch and self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
+            return False
+        if X_local.dtype not in (torch.float32, torch.bfloat16) or X_local.stride(1) != 1:
+            return False
+        if X_local.shape[0] < 1 or min(layout.widths) < 1:
+            return False
+        align = 8 if X_local.dtype == torch.bfloat16 else 4
+        if any(layout.offset(k) % align for k in range(layout.rounds)) or X_local.stride(0) % align:
+            return False
+        if X_local.data_ptr() % 16:
+            return False
+        return result_dtype(np.dtype(np.float32), list(weights), scores, total) == np.float32
+
+    def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total):
+        """Every round's fold in ONE launch on the current (fold) stream; round
+        k's exchange issued on the gather stream behind a wait for round k, so
+        it runs while the launch folds the later rounds."""
+        from . import engine
+        dev = X_local.device
+        bf16 = X_local.dtype == torch.bfloat16
+        odt = torch.bfloat16 if bf16 else torch.float32
+        full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
+        if full.dtype != odt or full.numel() < layout.padded_total:
+            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
+        local = torch.empty(layout.local_width, dtype=torch.float32, device=dev)
+        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=dev) if bf16 else None
+        offs = [layout.offset(k) for k in range(layout.rounds + 1)]
+        r = engine.fold_rounds(X_local, weights, scores, offs, out=local, out_bf16=local_b, total=total)
+        fs = torch.cuda.current_stream(dev)
+        gs = gather_stream(dev)
+        send_all = local_b if bf16 else local
+        send_all.record_stream(gs)
+        works = []
+        for k in range(layout.rounds):
+            engine.wait_round(r, k, gs)
+            lo, hi = layout.round_range(k)
+            send = send_all[layout.offset(k):layout.offset(k + 1)]
+            with torch.cuda.stream(gs):
+                if self.world == 1:
+                    full[lo:hi].copy_(send)
+                    continue
+                w = gather_into(full[lo:hi], send, self.group, async_op=True)
+            if w is not None:
+                works.append(w)
+        for w in works:
+            w.wait()  # the fold stream waits for the collectives
+        fs.wait_stream(gs)
+        return full[: layout.P]
 
     def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
         bf16 = X_local.dtype == torch.bfloat16

@@ -164,6 +164,8 @@ int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ld
                           int rounds, const int64_t* offsets, void* stream);
 int fa_rounds_wait(fa_rounds* r, int round, void* stream);
 int fa_rounds_timeouts(fa_rounds* r);
+/* [host] the kernel form fa_fedavg_bf16_rounds (bf16 != 0) / _f32_rounds runs */
+const char* fa_rounds_form(int bf16);
 
 /* The same folds with the per-client factors a[0..N), s[0..N) (s may be
  * NULL) in HOST memory, as the reference's caller holds them (Python numbers,

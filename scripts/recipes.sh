@@ -1,38 +1,72 @@
 #!/bin/bash
-# Named GPU recipes: one parameterised entry point for the gpurun calls of a
-# round (replaces the per-check wrapper scripts of rounds 2-3).  Each recipe is
-# a list of "name:seconds:command" steps for scripts/gpu_steps.sh (own time
-# limit per step, logs in gpurun_out/<name>.log, stops after a timeout/abort).
-#   /usr/local/graft/bin/gpurun --timeout 1200 -- scripts/recipes.sh <recipe> [extra steps...]
+# Named GPU recipes: the one parameterised entry point for gpurun calls (it
+# replaces the per-check wrapper scripts of rounds 2-3).  Each recipe is a list
+# of "name:seconds:command" steps for scripts/gpu_steps.sh: each step has its
+# own time limit, logs to gpurun_out/<name>.log, and a timeout / abort / fault
+# stops the call.  Extra steps may follow the recipe name.
+#   /usr/local/graft/bin/gpurun --timeout 1500 -- scripts/recipes.sh <recipe> ["name:secs:cmd" ...]
+# Recipes:
+#   gpu_suite     the whole -m gpu suite + smoke (the driver's round-end checks)
+#   bench         the default bench line (C3, the headline)
+#   bench_lines   every BASELINE bench line (scripts/bench_lines.sh)
+#   prof_c3       C3 bench line + kernel trace + FETCH/WRITE_SIZE passes (scripts/profile_c3.sh TAG COMMIT)
+#   rehearse_w8   8 ranks sharing the one GPU over gloo: C3 weak and C4 strong (the driver's 8-GPU recipe
+#                 is `python bench.py --gpus 8` and `python bench.py --gpus 8 --config c4`)
+#   c4_rank       one 8-GPU C4 rank on one GPU under nccl at world 1: one launch per step vs per round
+#   exchange      the exchange-interference proxy (tools/exchange_interference.py), C4 and C3 ranks
+#   e2e           end-to-end from host NPZ blobs: config-1 shapes, C2, 1024 x 1M, and C3 (1024 x 10M)
+#   tuner         the tuner's first-call cost, cold and with a warm cache file; varying client counts
+#   final         gpu_suite + bench + prof_c3 (the end-of-round evidence)
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 XI="python3 tools/exchange_interference.py"
-BF16_DYN="bf16_dyn_u32c1b128,bf16_dyn_u16c1b256,bf16_dyn_u32c1b64,bf16_dyn_u16c2b128,bf16_dyn_u8c2b256,bf16_dyn_u32c1b256"
-F32_DYN="gs_bands_16k,dyn_8k,dynp_u32c1b128,dynp_u16c1b256,dynp_u32c1b64,dynp_u16c2b256,dynp_u32c1b256"
+TAG=${TAG:-r04}
+COMMIT=${COMMIT:-unknown}
+S_BF="bf16_step_sd_u8c4w_p100,bf16_step_sd_u8c4w_p100_g80,bf16_step_sd_u8c4w_p100_g90,bf16_step_u8c4_g80,bf16_step_sd_u8c4_p150_g80"
+S_F32="product,f32_step_sd_u8c4_p75_g80,f32_step_sd_u8c4_p75_g90"
+C4R="--config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5 --no-cpu-baseline"
 recipe=${1:-}
 shift || true
 case "$recipe" in
-  gpu_suite)  # the whole -m gpu suite + smoke
+  gpu_suite)
     steps=("pytest_gpu:1100:$T -m gpu tests" "smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'") ;;
-  bench)      # the default bench line
-    steps=("bench_default:400:python3 bench.py") ;;
-  dyn_forms)  # round 4: the dynamic-tile forms, parity and the exchange proxy
-    steps=("pytest_shared:700:$T tests/test_gpu_shared_fold.py tests/test_gpu_tuner.py"
-           "xi_c4_host:300:$XI --config c4 --host-src --scale 0.15 --forms $BF16_DYN"
-           "xi_c4_host_r1:300:$XI --config c4 --host-src --scale 0.15 --forced-rounds overlapped --forms $BF16_DYN"
-           "xi_c4_hbm:300:$XI --config c4 --forms $BF16_DYN"
-           "xi_c3_host:400:$XI --config c3 --host-src --scale 0.15 --forms $F32_DYN") ;;
-  step_forms)  # round 4: the whole step in one launch, parity and the exchange proxy
-    S_BF="product,bf16_step_u8c2,bf16_step_u16c2,bf16_step_u8c4,bf16_step_u4c4"
-    S_F32="product,f32_step_u8c4,f32_step_u8c2,f32_step_u16c2,f32_step_u16c1"
-    steps=("pytest_shared:700:$T tests/test_gpu_shared_fold.py"
-           "xi_c4_host_step:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF --forms bf16_bands4_u8c4"
-           "xi_c4_hbm_step:300:$XI --config c4 --step-forms $S_BF --forms bf16_bands4_u8c4"
-           "xi_c3_host_step:400:$XI --config c3 --host-src --scale 0.15 --step-forms $S_F32 --forms gs_bands_16k"
-           "tuner_cold:200:python3 tools/tuner_probe.py --clients 256 --params 3454464 --bf16 --cache gpurun_out/tc.txt"
+  bench)
+    steps=("bench_default:500:python3 bench.py") ;;
+  bench_lines)
+    steps=("bench_lines:1100:scripts/bench_lines.sh") ;;
+  prof_c3)
+    steps=("prof_c3:900:scripts/profile_c3.sh $TAG $COMMIT") ;;
+  rehearse_w8)
+    steps=("rehearse_c3_w8:400:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c3 --clients 16 --steps 2 --warmup 1 --no-cpu-baseline"
+           "rehearse_c4_w8:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline"
+           "rehearse_c4_w8_perround:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline --per-round-launches") ;;
+  c4_rank)
+    steps=("c4_rank_one:300:python3 bench.py --rccl-world1 $C4R"
+           "c4_rank_perround:300:python3 bench.py --rccl-world1 $C4R --per-round-launches"
+           "c3_rank_one:300:python3 bench.py --rccl-world1 --config c3 --rounds 4 --steps 10 --no-cpu-baseline"
+           "c3_rank_perround:300:python3 bench.py --rccl-world1 --config c3 --rounds 4 --steps 10 --no-cpu-baseline --per-round-launches") ;;
+  exchange)
+    steps=("xi_c4_host:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF"
+           "xi_c4_hbm:300:$XI --config c4 --step-forms $S_BF"
+           "xi_c3_host:400:$XI --config c3 --host-src --scale 0.15 --step-forms $S_F32") ;;
+  e2e)
+    steps=("e2e_small:600:python3 bench_e2e.py --clients 10 --params 582026 --reps 20 && python3 bench_e2e.py --clients 100 --params 1000000 --reps 15 && python3 bench_e2e.py --clients 1024 --params 1000000 --reps 5"
+           "e2e_c3:900:python3 bench_e2e.py --clients 1024 --params 10000000 --reps 3 --no-cpu --check-cols 1000000") ;;
+  tuner)
+    steps=("tuner_cold:200:python3 tools/tuner_probe.py --clients 256 --params 3454464 --bf16 --cache gpurun_out/tc.txt"
            "tuner_warm:200:python3 tools/tuner_probe.py --clients 256 --params 3454464 --bf16 --cache gpurun_out/tc.txt"
            "tuner_c3:200:python3 tools/tuner_probe.py --clients 1024 --params 10000000 --cache 0"
            "tuner_vary:200:python3 tools/tuner_probe.py --params 909000 --vary-clients 1000,1024,990,700,1010,512,1000 --cache 0") ;;
+  step_forms)  # round 4: the one-launch step, its parity and the proxy
+    steps=("pytest_shared:700:$T tests/test_gpu_shared_fold.py tests/test_gpu_sharding.py tests/test_gpu_rccl.py"
+           "xi_c4_host_step:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF"
+           "xi_c4_hbm_step:300:$XI --config c4 --step-forms $S_BF"
+           "xi_c3_host_step:400:$XI --config c3 --host-src --scale 0.15 --step-forms $S_F32"
+           "c4_rank_one:300:python3 bench.py --rccl-world1 $C4R"
+           "c4_rank_perround:300:python3 bench.py --rccl-world1 $C4R --per-round-launches") ;;
+  final)
+    steps=("pytest_gpu:1100:$T -m gpu tests" "smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'"
+           "bench_default:500:python3 bench.py" "prof_c3:900:scripts/profile_c3.sh $TAG $COMMIT") ;;
   none) steps=() ;;
   *) echo "unknown recipe '$recipe'" >&2; exit 2 ;;
 esac

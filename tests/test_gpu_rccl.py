@@ -47,7 +47,6 @@ def _rccl_worker(port, q):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
         out = {"backend": dist.get_backend()}
-        agg = ShardedAggregator()
         w = synth.cardinalities(SEED, N)
         sc = _scores(SEED, N)
         for dt, P, rounds, tail in CASES:
@@ -60,10 +59,13 @@ def _rccl_worker(port, q):
                             else synth.clients_f32(SEED, N, lo, hi - lo))
                     X[:, lay.offset(k):lay.offset(k) + hi - lo] = T.from_numpy(part).to(dev)
             for scored in (False, True):
-                full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
-                out[(dt, P, tail, scored)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
+                # one launch per step (each round's all-gather behind its wait) and one launch per round
+                for one in (True, False):
+                    agg = ShardedAggregator(one_launch=one)
+                    full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
+                    out[(dt, P, tail, scored, one)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
         m = G.manifest()["f32_small"]
-        layers = agg.aggregate_layers(G.parameters("f32_small"), m["weights"])
+        layers = ShardedAggregator().aggregate_layers(G.parameters("f32_small"), m["weights"])
         out["layers"] = [np.array(a) for a in layers]
         q.put(out)
     finally:
@@ -86,14 +88,14 @@ def test_rccl_world1_slots_and_layers_bit_exact():
     for dt, P, _, tail in CASES:
         for scored in (False, True):
             s = sc if scored else None
-            if dt == "bf16":
-                _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(SEED, N, 0, P), w, s)
-                assert np.array_equal(np.frombuffer(got[(dt, P, tail, scored)], dtype=np.uint16), exp), \
-                    (dt, P, tail, scored)
-            else:
-                exp = O.fedavg_stacked(synth.clients_f32(SEED, N, 0, P), w, s)
-                assert np.array_equal(np.frombuffer(got[(dt, P, tail, scored)], dtype=np.uint32),
-                                      exp.view(np.uint32)), (dt, P, tail, scored)
+            for one in (True, False):
+                key = (dt, P, tail, scored, one)
+                if dt == "bf16":
+                    _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(SEED, N, 0, P), w, s)
+                    assert np.array_equal(np.frombuffer(got[key], dtype=np.uint16), exp), key
+                else:
+                    exp = O.fedavg_stacked(synth.clients_f32(SEED, N, 0, P), w, s)
+                    assert np.array_equal(np.frombuffer(got[key], dtype=np.uint32), exp.view(np.uint32)), key
     exp_layers = G.expected("f32_small", "fedavg")
     assert len(got["layers"]) == len(exp_layers)
     assert all(a.shape == b.shape and G.same_bits(a, b) for a, b in zip(got["layers"], exp_layers))

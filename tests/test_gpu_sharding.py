@@ -26,8 +26,9 @@ def _scores(seed, n):
     return [(r + 1) / 11 for r in synth.round_ids(seed, n, 10, 2)]
 
 
-@pytest.mark.parametrize("P,rounds,scored", [(10007, 3, False), (4096, 4, True), (1, 1, False)])
-def test_slots_world1_fp32(P, rounds, scored):
+@pytest.mark.parametrize("one_launch", [True, False])
+@pytest.mark.parametrize("P,rounds,scored", [(10007, 3, False), (4096, 4, True), (1, 1, False), (300001, 8, True)])
+def test_slots_world1_fp32(P, rounds, scored, one_launch):
     from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
     from oracle import oracle_lib as OL
     dev = torch.device("cuda", 0)
@@ -40,14 +41,15 @@ def test_slots_world1_fp32(P, rounds, scored):
             X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(Xh[:, lo:hi]).to(dev)
     w = synth.cardinalities(seed, N)
     sc = _scores(seed, N) if scored else None
-    full = ShardedAggregator().aggregate_slots(X, w, sc, lay)
+    full = ShardedAggregator(one_launch=one_launch).aggregate_slots(X, w, sc, lay)
     exp = OL.fedavg_f32(Xh, np.array(w, np.float32), np.float32(sum(w)),
                         s=None if sc is None else np.array(sc, np.float32))
     assert G.same_bits(full.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("P,rounds", [(8 * 1000 + 3, 2), (65536, 4)])
-def test_slots_world1_bf16_exchange(P, rounds):
+@pytest.mark.parametrize("one_launch", [True, False])
+@pytest.mark.parametrize("P,rounds", [(8 * 1000 + 3, 2), (65536, 4), (1_000_003, 5)])
+def test_slots_world1_bf16_exchange(P, rounds, one_launch):
     from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
     from oracle import fedavg_oracle as O
     dev = torch.device("cuda", 0)
@@ -60,7 +62,7 @@ def test_slots_world1_bf16_exchange(P, rounds):
             X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(Xb[:, lo:hi].view(np.int16)).to(dev)
     w = synth.cardinalities(seed, N)
     sc = _scores(seed, N)
-    full = ShardedAggregator().aggregate_slots(X.view(torch.bfloat16), w, sc, lay)
+    full = ShardedAggregator(one_launch=one_launch).aggregate_slots(X.view(torch.bfloat16), w, sc, lay)
     assert full.dtype == torch.bfloat16
     _, expb = O.fedavg_stacked_bf16(Xb, w, sc)
     assert np.array_equal(full.view(torch.int16).cpu().numpy().view(np.uint16), expb)

@@ -210,7 +210,8 @@ def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,rounds,tail", [(2, 4099, 4, 1.0), (3, 1000, 2, 1.0), (2, 9000, 4, 0.25)])
+@pytest.mark.parametrize("world,P,rounds,tail", [(2, 4099, 4, 1.0), (3, 1000, 2, 1.0), (2, 9000, 4, 0.25),
+                                                  (8, 40011, 4, 0.343)])  # 8 ranks: the C4 exchange in miniature
 def test_bf16_slot_gather_gloo_matches_oracle(world, P, rounds, tail):
     from oracle import fedavg_oracle as O
     N, seed = 6, 29

@@ -203,8 +203,6 @@ def main():
     tmo = L.fa_rounds_timeouts(rs_prod)
     if tmo:
         print(f"  WARNING: {tmo} round waits timed out", flush=True)
-    if args.step_forms and not args.forms:
-        return
     for fname in [f for f in args.forms.split(",") if f] or [None]:
         form[0] = None if fname is None else names[fname]
         for _ in range(2):  # warm the forced form
