@@ -309,6 +309,8 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
     visible = len(os.sched_getaffinity(0))
     return {
         "value": round(sample_bytes / t_np / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+        "form": "literal: every client's `layer * n` product kept, then reduce(np.add) and one divide "
+                "(fed_avg_aggregator.py:31-41), on a column sample (the full workload: full_lean)",
         "sample": f"{wl.N} clients x first {ncols} params of the same workload (rank 0's first slot, columns "
                   f"{wl.col0}..{wl.col0 + ncols}); numpy literal restatement of fed_avg_aggregator.py:24-42 "
                   f"(1 core, numpy ufuncs single-threaded), median of {len(t_np_all)} runs {t_np:.2f} s "
@@ -424,17 +426,21 @@ def main():
     # ranks could otherwise fold the same slot shape with different kernels);
     # what each rank had chosen on its own is reported
     forms_by_rank, forms_agree = None, None
-    if dist_on and world > 1 and args.variant == 0 and not one_launch:
+    if dist_on and world > 1 and args.variant == 0:
         kind = 1 if wl.dtype == "f32" else 2
-        mine = {str(w): L.fa_fold_form(kind, wl.N, w, wl.ldx, 1 if wl.scored else 0, stream.cuda_stream).decode()
-                for w in dict.fromkeys(lay.widths)}
+        if one_launch:  # one fixed step form per dtype
+            mine = {"step": L.fa_rounds_form(1 if wl.dtype == "bf16" else 0).decode()}
+        else:
+            mine = {str(w): L.fa_fold_form(kind, wl.N, w, wl.ldx, 1 if wl.scored else 0, stream.cuda_stream).decode()
+                    for w in dict.fromkeys(lay.widths)}
         forms_by_rank = [None] * world
         dist.all_gather_object(forms_by_rank, mine)
         forms_agree = all(f == forms_by_rank[0] for f in forms_by_rank)
-        text = [_lib.tune_export() if rank == 0 else None]
-        dist.broadcast_object_list(text, src=0)
-        if rank != 0:
-            _lib.tune_import(text[0])
+        if not one_launch:
+            text = [_lib.tune_export() if rank == 0 else None]
+            dist.broadcast_object_list(text, src=0)
+            if rank != 0:
+                _lib.tune_import(text[0])
 
     if args.sweep and rank == 0:
         nvar = B.fa_num_variants() if wl.dtype == "f32" else B.fa_num_bf16_variants()

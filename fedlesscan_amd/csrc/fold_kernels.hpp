@@ -1363,7 +1363,21 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
     odd = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
 }
 
-template <int U, int C, bool SCORED, int B = kBlock>
+// A 16-byte output store: non-temporal, or (SC1) two 8-byte agent-scope
+// stores, which leave no dirty line in the XCD's L2 (the one-launch step's
+// per-round release then writes back nothing; MI355X_MICROARCH.md, stores)
+template <bool SC1>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+    if constexpr (SC1) {
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+        __hip_atomic_store(q, ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    }
+}
+
+template <int U, int C, bool SCORED, int B = kBlock, bool SC1 = false>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -1415,22 +1429,22 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
         const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
         const int64_t oc = o0 + (int64_t)c * B;
         f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
-        __builtin_nontemporal_store(f32x4{e.x, o.x, e.y, o.y}, o4);
-        __builtin_nontemporal_store(f32x4{e.z, o.z, e.w, o.w}, o4 + 1);
+        st16<SC1>(o4, __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y}));
+        st16<SC1>(o4 + 1, __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w}));
         if (outb) {
             u32x4 b;
             b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
             b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
             b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
             b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
-            __builtin_nontemporal_store(b, reinterpret_cast<u32x4*>(outb) + oc);
+            st16<SC1>(reinterpret_cast<u32x4*>(outb) + oc, b);
         }
     }
 }
 
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
-template <int U, int C, bool SCORED, int B = kBlock>
+template <int U, int C, bool SCORED, int B = kBlock, bool SC1 = false>
 __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
@@ -1439,13 +1453,13 @@ __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restric
     const int64_t o0 = bid * (B * C) + threadIdx.x;
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
     if (o0 + (int64_t)(C - 1) * B < no) {
-        fold_octets<U, C, SCORED, B>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+        fold_octets<U, C, SCORED, B, SC1>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int64_t o = o0 + (int64_t)c * B;
-        if (o < no) fold_octets<U, 1, SCORED, B>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+        if (o < no) fold_octets<U, 1, SCORED, B, SC1>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
     const int64_t tb = no / (B * C), tl = (no % (B * C)) % B;
     if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
@@ -1658,7 +1672,7 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
 }
 
 // wide tiles: UB rows ahead x CB octets (quads) per lane; narrow: US x CS
-template <int UB, int CB, int US, int CS, bool SCORED, int B>
+template <int UB, int CB, int US, int CS, bool SCORED, int B, bool SC1 = false>
 __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
     const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
@@ -1666,8 +1680,10 @@ __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
         uint16_t* ob = outb ? outb + c0 : nullptr;
-        if (T.small[g]) bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
-        else bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
+        if (T.small[g])
+            bf16_tile<US, CS, SCORED, B, SC1>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
+        else
+            bf16_tile<UB, CB, SCORED, B, SC1>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
     });
 }
 
@@ -2365,11 +2381,20 @@ constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4_p150_g80", true, 8, 4, 16, 1, 150, 80},
     {"f32_step_sd_u8c4_p75_g80", false, 8, 4, 16, 1, 75, 80},
     {"f32_step_sd_u8c4_p75_g90", false, 8, 4, 16, 1, 75, 90},
+    // outputs stored sc1 (no dirty L2 lines for the per-round release to write back)
+    {"bf16_step_sd_u8c4w_p100_sc1", true, 8, 4, 8, 4, 100, 100},
+    {"bf16_step_u8c4_sc1", true, 8, 4, 8, 4, -1, 100},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
-// The policy's step form (profiles/r04_step/): bf16 C4 rank slots, fp32 C3 rank slots.
-inline int pick_step(bool bf16) { return bf16 ? 0 : 7; }
+// The policy's step forms (profiles/r04_step/): for a C4 rank's bf16 slots,
+// wide 8 x 4-octet tiles dealt statically over the step with one pass of them
+// left to the counter (1.01-1.02 ms alone, 1.06-1.13 beside the proxy copy,
+// against 0.96 / 1.06-1.18 for per-round static launches); for a C3 rank's
+// fp32 slots, 8 x 4-quad static tiles and a pool of 0.75 passes in 16 x
+// 1-quad tiles (5.84-5.94 alone, 5.91-6.05 beside the copy, against 5.81-5.85
+// / 6.05-6.19).
+inline int pick_step(bool bf16) { return bf16 ? 2 : 7; }
 
 // The per-launch state of fa_fedavg_*_rounds: the signal words in device
 // memory and the host epoch (fa_rounds in fedavg_hip.h).
@@ -2464,6 +2489,11 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
                               0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);                  \
     else hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
                             dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
+#define FA_STB1(UB, CB, US, CS)                                                                                \
+    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, true>), dim3((unsigned)grid),   \
+                              dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
+    else hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, true>), dim3((unsigned)grid),    \
+                            dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
 #define FA_STF(UB, CB, US, CS)                                                                                \
     if (s) hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), \
                               0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);                       \
@@ -2475,8 +2505,10 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         case 3: case 6: FA_STB(16, 2, 16, 2); break;
         case 4: FA_STB(8, 2, 8, 2); break;
         case 7: case 8: case 9: case 15: case 16: FA_STF(8, 4, 16, 1); break;
+        case 17: case 18: FA_STB1(8, 4, 8, 4); break;
         default: FA_STF(8, 4, 8, 4); break;
     }
+#undef FA_STB1
 #undef FA_STB
 #undef FA_STF
     rc = check_launch("rounds fold");

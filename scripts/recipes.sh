@@ -22,8 +22,8 @@ T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 XI="python3 tools/exchange_interference.py"
 TAG=${TAG:-r04}
 COMMIT=${COMMIT:-unknown}
-S_BF="bf16_step_sd_u8c4w_p100,bf16_step_sd_u8c4w_p100_g80,bf16_step_sd_u8c4w_p100_g90,bf16_step_u8c4_g80,bf16_step_sd_u8c4_p150_g80"
-S_F32="product,f32_step_sd_u8c4_p75_g80,f32_step_sd_u8c4_p75_g90"
+S_BF="product,bf16_step_sd_u8c4w_p100_sc1,bf16_step_u8c4,bf16_step_u8c4_sc1"
+S_F32="product"
 C4R="--config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5 --no-cpu-baseline"
 recipe=${1:-}
 shift || true
