@@ -589,7 +589,8 @@ def main():
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
     if one_launch:  # a round wait that gave up (never expected) would make the gather unordered
-        t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev)))], dtype=torch.int64, device=dev)
+        t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))],
+                         dtype=torch.int64, device=dev)
         dist.all_reduce(t)
         timeouts = int(t.item())
 

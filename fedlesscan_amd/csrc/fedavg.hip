@@ -231,24 +231,11 @@ struct fa_rounds : RoundsState {};
 int fa_rounds_create(fa_rounds** r, int device) {
     if (!r) return fail(FA_ERR_ARG, "fa_rounds_create: null handle");
     *r = nullptr;
-    int prev = 0;
-    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(FA_ERR_ARG, "fa_rounds_create: no device %d", device);
-    }
     fa_rounds* o = new fa_rounds();
-    o->device = device;
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
-    o->max_ticks = (long long)khz * 1000LL * 10LL;  // a waiter gives up after ~10 s
-    hipError_t e = hipMalloc((void**)&o->sig, kSigWords * sizeof(unsigned int));
-    if (e == hipSuccess) e = hipMemset(o->sig, 0, kSigWords * sizeof(unsigned int));
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    (void)hipSetDevice(prev);
-    if (e != hipSuccess) {
-        if (o->sig) (void)hipFree(o->sig);
+    const int rc = rounds_state_init(*o, device);
+    if (rc) {
         delete o;
-        return fail(FA_ERR_HIP, "fa_rounds_create: %s", hipGetErrorString(e));
+        return rc;
     }
     *r = o;
     g_err[0] = 0;
@@ -257,12 +244,7 @@ int fa_rounds_create(fa_rounds** r, int device) {
 
 int fa_rounds_destroy(fa_rounds* r) {
     if (!r) return FA_OK;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(r->device);
-    (void)hipDeviceSynchronize();  // no launch or waiter may still use the words
-    (void)hipFree(r->sig);
-    (void)hipSetDevice(prev);
+    rounds_state_free(*r);
     delete r;
     return FA_OK;
 }
@@ -288,12 +270,8 @@ const char* fa_rounds_form(int bf16) { return step_form_name(pick_step(bf16 != 0
 
 int fa_rounds_wait(fa_rounds* r, int round, void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
-    if (!r->launched) return fail(FA_ERR_ARG, "fa_rounds_wait: the last rounds fold was not launched");
-    if (round < 0 || round >= r->rounds) return fail(FA_ERR_ARG, "fa_rounds_wait: round %d of %d", round, r->rounds);
     StreamDevice on_stream_device(stream);
-    hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, (hipStream_t)stream, r->sig + kSigFlag + round, r->epoch,
-                       r->sig + kSigTimeout, r->max_ticks);
-    return check_launch("k_wait_round");
+    return rounds_wait(*r, round, (hipStream_t)stream);
 }
 
 int fa_rounds_timeouts(fa_rounds* r) {

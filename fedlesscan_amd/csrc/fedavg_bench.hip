@@ -530,24 +530,11 @@ const char* fa_step_form_name(int form) { return step_form_name(form); }
 int fa_bench_rounds_create(void** r, int device) {
     if (!r) return fail(FA_ERR_ARG, "null handle");
     *r = nullptr;
-    int prev = 0;
-    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(FA_ERR_ARG, "no device %d", device);
-    }
     RoundsState* o = new RoundsState();
-    o->device = device;
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
-    o->max_ticks = (long long)khz * 1000LL * 10LL;
-    hipError_t e = hipMalloc((void**)&o->sig, kSigWords * sizeof(unsigned int));
-    if (e == hipSuccess) e = hipMemset(o->sig, 0, kSigWords * sizeof(unsigned int));
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    (void)hipSetDevice(prev);
-    if (e != hipSuccess) {
-        if (o->sig) (void)hipFree(o->sig);
+    const int rc = rounds_state_init(*o, device);
+    if (rc) {
         delete o;
-        return fail(FA_ERR_HIP, "rounds state: %s", hipGetErrorString(e));
+        return rc;
     }
     *r = o;
     return FA_OK;
@@ -556,12 +543,7 @@ int fa_bench_rounds_create(void** r, int device) {
 int fa_bench_rounds_destroy(void* r) {
     RoundsState* o = static_cast<RoundsState*>(r);
     if (!o) return FA_OK;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(o->device);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(o->sig);
-    (void)hipSetDevice(prev);
+    rounds_state_free(*o);
     delete o;
     return FA_OK;
 }
@@ -578,11 +560,9 @@ int fa_fedavg_rounds_form(void* r, int form, const void* X, int64_t N, int64_t l
 
 int fa_bench_rounds_wait(void* r, int round, void* stream) {
     RoundsState* o = static_cast<RoundsState*>(r);
-    if (!o || !o->launched || round < 0 || round >= o->rounds) return fail(FA_ERR_ARG, "bad rounds wait");
+    if (!o) return fail(FA_ERR_ARG, "null rounds state");
     StreamDevice on_stream_device(stream);
-    hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, (hipStream_t)stream, o->sig + kSigFlag + round, o->epoch,
-                       o->sig + kSigTimeout, o->max_ticks);
-    return check_launch("k_wait_round");
+    return rounds_wait(*o, round, (hipStream_t)stream);
 }
 
 int fa_num_bf16_forms(void) { return kNumBf16Forms; }

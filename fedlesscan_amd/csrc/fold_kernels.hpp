@@ -2384,6 +2384,9 @@ constexpr StepSpec kStepSpecs[] = {
     // outputs stored sc1 (no dirty L2 lines for the per-round release to write back)
     {"bf16_step_sd_u8c4w_p100_sc1", true, 8, 4, 8, 4, 100, 100},
     {"bf16_step_u8c4_sc1", true, 8, 4, 8, 4, -1, 100},
+    // every tile static (no pool): the one launch's cost without the dynamic part
+    {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0, 100},
+    {"bf16_step_static_u8c2", true, 8, 2, 8, 2, 0, 100},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2405,6 +2408,8 @@ struct RoundsState {
     int rounds = 0;               // of the last launch
     bool launched = false;        // the last launch was enqueued
     long long max_ticks = 0;      // a waiter's give-up time in wall-clock ticks
+    hipEvent_t start = nullptr;   // recorded on the launch's stream just before the launch: a waiter's
+                                  // stream waits for it, so its give-up clock starts with the fold
 };
 
 // The segments of one step launch over `rounds` slots at local columns
@@ -2457,6 +2462,51 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
     return FA_OK;
 }
 
+// Create / destroy a launch state on `device`; enqueue a waiter for round k.
+inline int rounds_state_init(RoundsState& o, int device) {
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FA_ERR_ARG, "rounds state: no device %d", device);
+    }
+    o.device = device;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    o.max_ticks = (long long)khz * 1000LL * 30LL;  // a waiter gives up 30 s after the fold reached its stream's head
+    hipError_t e = hipMalloc((void**)&o.sig, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipMemset(o.sig, 0, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&o.start, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        if (o.sig) (void)hipFree(o.sig);
+        if (o.start) (void)hipEventDestroy(o.start);
+        o.sig = nullptr;
+        o.start = nullptr;
+        return fail(FA_ERR_HIP, "rounds state: %s", hipGetErrorString(e));
+    }
+    return FA_OK;
+}
+inline void rounds_state_free(RoundsState& o) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(o.device);
+    (void)hipDeviceSynchronize();  // no launch or waiter may still use the words
+    if (o.sig) (void)hipFree(o.sig);
+    if (o.start) (void)hipEventDestroy(o.start);
+    o.sig = nullptr;
+    o.start = nullptr;
+    (void)hipSetDevice(prev);
+}
+inline int rounds_wait(RoundsState& o, int round, hipStream_t st) {
+    if (!o.launched) return fail(FA_ERR_ARG, "rounds wait: the last rounds fold was not launched");
+    if (round < 0 || round >= o.rounds) return fail(FA_ERR_ARG, "rounds wait: round %d of %d", round, o.rounds);
+    if (o.start && hipStreamWaitEvent(st, o.start, 0) != hipSuccess) return check_launch("rounds wait: event");
+    hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, st, o.sig + kSigFlag + round, o.epoch,
+                       o.sig + kSigTimeout, o.max_ticks);
+    return check_launch("k_wait_round");
+}
+
 // Enqueue one step launch of form f over `rounds` slots at local columns
 // [offsets[k], offsets[k+1]).
 inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int64_t N, int64_t ldx,
@@ -2482,6 +2532,7 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
+    if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
     const float* Xf = static_cast<const float*>(X);
 #define FA_STB(UB, CB, US, CS)                                                                                 \
@@ -2506,6 +2557,8 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         case 4: FA_STB(8, 2, 8, 2); break;
         case 7: case 8: case 9: case 15: case 16: FA_STF(8, 4, 16, 1); break;
         case 17: case 18: FA_STB1(8, 4, 8, 4); break;
+        case 19: FA_STB(8, 4, 8, 4); break;
+        case 20: FA_STB(8, 2, 8, 2); break;
         default: FA_STF(8, 4, 8, 4); break;
     }
 #undef FA_STB1

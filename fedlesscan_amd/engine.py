@@ -295,17 +295,18 @@ _rounds_states: dict = {}
 _rounds_lock = threading.Lock()
 
 
-def rounds_state(device: torch.device) -> ctypes.c_void_p:
-    """The library's one-launch-per-step state (fa_rounds) of a device: its
-    launches must be ordered, so callers issue them on one stream per device
-    (sharding.fold_stream)."""
+def rounds_state(device: torch.device, stream: Optional[int] = None) -> ctypes.c_void_p:
+    """The library's one-launch-per-step state (fa_rounds) for the launches
+    issued on one stream of a device (default: its current stream): launches
+    with one state must be ordered, and launches on one stream are."""
     dev = torch.device(device)
+    key = (dev, stream if stream is not None else stream_ptr(dev))
     with _rounds_lock:
-        h = _rounds_states.get(dev)
+        h = _rounds_states.get(key)
         if h is None:
             h = ctypes.c_void_p()
             _lib.call("fa_rounds_create", ctypes.byref(h), dev.index if dev.index is not None else 0)
-            _rounds_states[dev] = h
+            _rounds_states[key] = h
         return h
 
 

@@ -149,9 +149,12 @@ int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  *     [offsets[k], offsets[k+1]) of X (and writes the same columns of out);
  *     every round non-empty, 16-B aligned (offsets % 4, bf16 % 8), ldx too;
  *     1 <= rounds <= 8.  Not under graph capture (FA_ERR_ARG).
- *   fa_rounds_wait: round < the last launch's rounds; a waiter that sees no
- *     completion within ~10 s returns anyway and counts a timeout;
- *     fa_rounds_timeouts (synchronous) returns that count. */
+ *   fa_rounds_wait: round < the last launch's rounds; the stream first waits
+ *     for the launch to reach the head of its own stream (an event recorded
+ *     just before it), then a waiter that sees no completion within ~30 s
+ *     returns anyway and counts a timeout; fa_rounds_timeouts (synchronous)
+ *     returns that count.  One object per launching stream (engine.py keys
+ *     them by device and stream). */
 typedef struct fa_rounds fa_rounds;
 int fa_rounds_create(fa_rounds** r, int device);
 int fa_rounds_destroy(fa_rounds* r);

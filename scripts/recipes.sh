@@ -67,6 +67,12 @@ case "$recipe" in
   final)
     steps=("pytest_gpu:1100:$T -m gpu tests" "smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'"
            "bench_default:500:python3 bench.py" "prof_c3:900:scripts/profile_c3.sh $TAG $COMMIT") ;;
+  step_alone)  # the one launch's cost while it runs alone: fully static steps, one round
+    steps=("xi_alone4:300:$XI --config c4 --blocks '' --step-forms product,bf16_step_static_u8c4,bf16_step_static_u8c2"
+           "xi_alone4_forced:300:$XI --config c4 --blocks '' --forms bf16_bands4_u8c4,bf16_bands4_u8c2"
+           "xi_alone1:300:$XI --config c4 --rounds 1 --blocks '' --step-forms product,bf16_step_static_u8c4,bf16_step_static_u8c2") ;;
+  e2e_c2)  # C2 end to end over chunk sizes x slots, two alternating passes
+    steps=("e2e_c2_variants:900:for pass in 1 2; do for c in 32:3 64:3 64:4 16:4; do FEDAVG_STREAM_CHUNK_MB=\${c%:*} FEDAVG_STREAM_SLOTS=\${c#*:} python3 bench_e2e.py --clients 100 --params 1000000 --reps 15 --no-cpu --check-cols 100000; done; done") ;;
   none) steps=() ;;
   *) echo "unknown recipe '$recipe'" >&2; exit 2 ;;
 esac

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c3", "c4"])
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--blocks", default="16,32,64")
+    ap.add_argument("--rounds", type=int, default=4, help="exchange rounds per step (overlap_layout)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--host-src", action="store_true",
                     help="read the copied bytes from page-locked host memory (long-latency loads over PCIe, closer "
@@ -57,7 +58,7 @@ def main():
         P_total = P_rank * args.world
     else:
         N, P_total, dt, esz, out_esz = 256, 100_000_000, "bf16", 2, 2
-    lay = overlap_layout(P_total, args.world, dt)
+    lay = overlap_layout(P_total, args.world, dt, rounds=args.rounds)
     W = lay.local_width
     st0 = torch.cuda.current_stream(dev)
     X = torch.empty((N, W), dtype=torch.float32 if dt == "f32" else torch.bfloat16, device=dev)
