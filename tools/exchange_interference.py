@@ -213,16 +213,21 @@ def main():
         label = (fname or ("hint" if args.hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all"
                                                                   else "")
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
-            folds = []
+            folds, spans = [], []
             for _ in range(args.steps):
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(lay.rounds)]
                 step(blocks, ev)
                 torch.cuda.synchronize()
                 folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
+                spans.append(ev[0][0].elapsed_time(ev[-1][1]))
             folds.sort()
+            spans.sort()
+            # fold per step = the rounds' launches summed (gaps between them left out);
+            # span = first launch's start to last launch's end on the fold stream, the
+            # figure comparable with a one-launch step
             print(f"  {label:24s} copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
-                  f"(min {folds[0]:.4f})", flush=True)
+                  f"(min {folds[0]:.4f}), span median {spans[len(spans) // 2]:.4f} ms", flush=True)
 
 
 if __name__ == "__main__":
