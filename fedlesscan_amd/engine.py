@@ -315,7 +315,7 @@ def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], 
     """Every exchange round of a step in ONE launch (fa_fedavg_*_rounds): round
     k folds the columns [offsets[k], offsets[k+1]) of X (fp32 or bf16 rows)
     into the same columns of out (and of out_bf16, the RNE copy, for bf16 X),
-    on the current stream.  Returns the device's rounds state for
+    on the current stream.  Returns that stream's rounds state for
     `wait_round`: the exchange of round k may start, on another stream, as soon
     as round k is complete, while the launch goes on.  Same bits as
     fold_stacked on each round's columns."""
@@ -329,8 +329,8 @@ def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], 
     a, s = f.to(dev)
     rounds = len(offsets) - 1
     offs = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
-    r = rounds_state(dev)
     st = stream_ptr(dev)
+    r = rounds_state(dev, st)
     if X.dtype == torch.bfloat16:
         _lib.call("fa_fedavg_bf16_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
                   out.data_ptr(), _ptr(out_bf16), rounds, offs, st)
