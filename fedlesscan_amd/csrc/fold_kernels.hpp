@@ -1600,10 +1600,38 @@ struct StepTable {
     int64_t static_tiles;
     int32_t segs;
     int32_t rounds;
+    // pass barriers of the static tiles (bench forms): before static pass
+    // i * sync_passes (i = 1 .. bars) a block waits until `quorum` blocks have
+    // finished the pass before it, or sync_ticks of the wall clock went by
+    int32_t sync_passes, bars, quorum;
+    int64_t sync_ticks;
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
-// [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
-constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
+// [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out,
+// then kMaxBars pass-barrier counters
+constexpr int kMaxBars = 32;
+constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigBar = 3 + 2 * kMaxRounds,
+              kSigWords = kSigBar + kMaxBars;
+
+// Pass barrier i of a step launch: the block (all its waves done with the
+// pass before) counts itself, then, if `wait`, lane 0 polls until `quorum`
+// blocks have, or until the time limit (a barrier only shapes timing: a block
+// that gives up folds the same tiles).
+__device__ __forceinline__ void step_bar(const StepTable& T, unsigned int* sig, int i, bool wait) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&sig[kSigBar + i], 1u);
+        if (wait) {
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load(&sig[kSigBar + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   (unsigned int)T.quorum) {
+                if (wall_clock64() - t0 > T.sync_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    if (wait) __syncthreads();
+}
 
 template <class Tile>
 __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Tile tile) {
@@ -1613,7 +1641,9 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
     const int64_t G = gridDim.x;
     int p = 0;
     int64_t t = blockIdx.x;
+    const int S = T.sync_passes;
     if (t >= Ts) {  // no static tile for this block: its first tile from the counter
+        for (int i = 0; S && i < T.bars; ++i) step_bar(T, sig, i, false);
         if (threadIdx.x == 0) nxt[p] = atomicAdd(&sig[0], 1u);
         __syncthreads();
         t = Ts + nxt[p];
@@ -1635,6 +1665,15 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
             __syncthreads();
             tn = Ts + nxt[p];
             p ^= 1;
+        }
+        if (S && t < Ts) {  // pass barriers of the static tiles
+            const int64_t jt = t / G;
+            if (tn < Ts) {
+                const int64_t jn = tn / G;
+                if (jn % S == 0 && jn / S <= T.bars) step_bar(T, sig, (int)(jn / S) - 1, true);
+            } else {
+                for (int64_t i = jt / S + 1; i <= T.bars; ++i) step_bar(T, sig, (int)i - 1, false);
+            }
         }
         int gn = g;
         while (gn < T.segs && tn >= T.seg_end[gn]) ++gn;  // T.segs: no tile left
@@ -1664,7 +1703,8 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
         g = gn < T.segs ? gn : g;
     }
     if (threadIdx.x == 0) {
-        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {
+        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {  // every block has counted at every barrier
+            for (int i = 0; i < T.bars; ++i) atomicExch(&sig[kSigBar + i], 0u);
             atomicExch(&sig[0], 0u);
             atomicExch(&sig[1], 0u);
         }
@@ -2359,7 +2399,9 @@ struct StepSpec {
     const char* name;
     bool bf16;
     int ub, cb, us, cs, pool100;
-    int grid100;  // blocks per 100 CUs (100: one per CU)
+    int grid100;        // blocks per 100 CUs (100: one per CU)
+    int sync = 0;       // a pass barrier every `sync` static passes (0: none)
+    int quorum100 = 0;  // of the blocks, in percent, a barrier waits for
 };
 constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
@@ -2387,6 +2429,14 @@ constexpr StepSpec kStepSpecs[] = {
     // every tile static (no pool): the one launch's cost without the dynamic part
     {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0, 100},
     {"bf16_step_static_u8c2", true, 8, 2, 8, 2, 0, 100},
+    // pass barriers in the static tiles: do bands win because their launch
+    // boundaries put every block back in step?
+    {"bf16_step_static_u8c4_s3", true, 8, 4, 8, 4, 0, 100, 3, 100},
+    {"bf16_step_static_u8c4_s1", true, 8, 4, 8, 4, 0, 100, 1, 100},
+    {"bf16_step_static_u8c4_s3q90", true, 8, 4, 8, 4, 0, 100, 3, 90},
+    {"bf16_step_sd_u8c4w_p100_s3q90", true, 8, 4, 8, 4, 100, 100, 3, 90},
+    {"bf16_step_sd_u8c4w_p100_s2q75", true, 8, 4, 8, 4, 100, 100, 2, 75},
+    {"f32_step_sd_u8c4_p75_s3q90", false, 8, 4, 16, 1, 75, 100, 3, 90},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2531,6 +2581,15 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     if (rc) return rc;
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
+    if (sp.sync > 0 && T.static_tiles > 0) {
+        const int64_t passes = (T.static_tiles + grid - 1) / grid;
+        int64_t sync = sp.sync;
+        while ((passes - 1) / sync > kMaxBars) ++sync;
+        T.sync_passes = (int32_t)sync;
+        T.bars = (int32_t)((passes - 1) / sync);
+        T.quorum = (int32_t)((grid * sp.quorum100 + 99) / 100);
+        T.sync_ticks = R.max_ticks / 300000 > 0 ? R.max_ticks / 300000 : 1;  // 100 us
+    }
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
     if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
@@ -2557,8 +2616,9 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         case 4: FA_STB(8, 2, 8, 2); break;
         case 7: case 8: case 9: case 15: case 16: FA_STF(8, 4, 16, 1); break;
         case 17: case 18: FA_STB1(8, 4, 8, 4); break;
-        case 19: FA_STB(8, 4, 8, 4); break;
+        case 19: case 21: case 22: case 23: case 24: case 25: FA_STB(8, 4, 8, 4); break;
         case 20: FA_STB(8, 2, 8, 2); break;
+        case 26: FA_STF(8, 4, 16, 1); break;
         default: FA_STF(8, 4, 8, 4); break;
     }
 #undef FA_STB1
