@@ -101,9 +101,12 @@ def parse():
                     help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
                          "left exposed after the step's folds); 1 = equal rounds.  Default with several rounds: "
                          "the layout for the dtype (DEFAULT_TAIL)")
-    ap.add_argument("--per-round-launches", action="store_true",
-                    help="at N > 1: one fold launch per exchange round (round 3's step) instead of the whole step in "
-                         "one launch with each round's all-gather started behind its completion flag")
+    ap.add_argument("--step-mode", default="auto", choices=["auto", "one", "per-round"],
+                    help="with several rounds under a process group: 'one' = the whole step in one fold launch, "
+                         "each round's all-gather started behind its completion flag; 'per-round' = one fold "
+                         "launch per exchange round (round 3's step); 'auto' (default) = time both on this run's "
+                         "own ranks before the warm-up (max over ranks, best of two trials) and keep the faster")
+    ap.add_argument("--per-round-launches", action="store_true", help="same as --step-mode per-round")
     ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
                          "rounds: shares 1, 1, 0.5, 0.25)")
@@ -413,8 +416,12 @@ def main():
     # the first aggregation rounds of a deployment would
     L = _lib.load()
     tune_calls = 0
-    one_launch = dist_on and rounds > 1 and args.variant == 0 and not args.per_round_launches
-    if args.variant == 0 and L.fa_set_autotune(-1) == 1 and not one_launch:
+    step_mode = "per-round" if args.per_round_launches else args.step_mode
+    can_one = dist_on and rounds > 1 and args.variant == 0 and step_mode != "per-round"
+    probe_modes = can_one and step_mode == "auto"  # both step forms timed below, the faster kept
+    one_launch = can_one
+    per_round_possible = not can_one or probe_modes
+    if args.variant == 0 and L.fa_set_autotune(-1) == 1 and per_round_possible:
         for tune_calls in range(1, 201):
             for k in range(rounds):
                 wl.launch(0, k)
@@ -428,15 +435,16 @@ def main():
     forms_by_rank, forms_agree = None, None
     if dist_on and world > 1 and args.variant == 0:
         kind = 1 if wl.dtype == "f32" else 2
-        if one_launch:  # one fixed step form per dtype
-            mine = {"step": L.fa_rounds_form(1 if wl.dtype == "bf16" else 0).decode()}
-        else:
-            mine = {str(w): L.fa_fold_form(kind, wl.N, w, wl.ldx, 1 if wl.scored else 0, stream.cuda_stream).decode()
-                    for w in dict.fromkeys(lay.widths)}
+        mine = {}
+        if can_one:  # one fixed step form per dtype
+            mine["step"] = L.fa_rounds_form(1 if wl.dtype == "bf16" else 0).decode()
+        if per_round_possible:
+            mine.update({str(w): L.fa_fold_form(kind, wl.N, w, wl.ldx, 1 if wl.scored else 0,
+                                                stream.cuda_stream).decode() for w in dict.fromkeys(lay.widths)})
         forms_by_rank = [None] * world
         dist.all_gather_object(forms_by_rank, mine)
         forms_agree = all(f == forms_by_rank[0] for f in forms_by_rank)
-        if not one_launch:
+        if per_round_possible:
             text = [_lib.tune_export() if rank == 0 else None]
             dist.broadcast_object_list(text, src=0)
             if rank != 0:
@@ -474,7 +482,7 @@ def main():
     # the exchanged model: fp32 result for fp32 updates, the RNE bf16 result
     # for bf16 updates (2 B/param over xGMI: half the bytes of the fp32 result)
     send = wl.out if wl.dtype == "f32" else wl.out_bf16
-    if one_launch:
+    if can_one:
         from fedlesscan_amd import engine
         from fedlesscan_amd.sharding import gather_stream
         gs = gather_stream(dev)
@@ -502,9 +510,10 @@ def main():
         if ev is not None:
             ev[1].record(stream)
 
-    def step(ev=None):
-        """ev = (fold events per round, end event) for the timed steps."""
-        if one_launch:
+    def step(ev=None, mode=None):
+        """ev = (fold events per round, end event) for the timed steps; mode
+        "one" / "per-round" overrides the chosen step form (the probe)."""
+        if (one_launch if mode is None else mode == "one"):
             step_one_launch(ev)
             return
         works = []
@@ -525,6 +534,34 @@ def main():
             ev[1].record(stream)
 
     torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
+    mode_probe = None
+    if probe_modes:
+        # which step form is faster depends on how much the exchange kernels
+        # slow the fold, which only this run's own ranks and links can tell
+        # (DESIGN §8): time both, every rank in step, before the warm-up
+        modes = ("one", "per-round")
+        res = {m: [] for m in modes}
+        for m in modes:
+            step(mode=m)
+            step(mode=m)
+        for _trial in range(2):
+            for m in modes:
+                step(mode=m)
+                dist.barrier()
+                torch.cuda.synchronize()
+                tp = time.perf_counter()
+                for _ in range(5):
+                    step(mode=m)
+                torch.cuda.synchronize()
+                dist.barrier()
+                t = torch.tensor([time.perf_counter() - tp], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                res[m].append(float(t.item()) / 5 * 1e3)
+        best = {m: min(v) for m, v in res.items()}
+        one_launch = best["one"] <= best["per-round"]
+        mode_probe = {"one_launch_ms": round(best["one"], 4), "per_round_ms": round(best["per-round"], 4),
+                      "chosen": "one launch" if one_launch else "per round",
+                      "how": "wall time of 5 steps between barriers, max over ranks, best of 2 trials per form"}
     for _ in range(args.warmup):
         step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -588,7 +625,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
-    if one_launch:  # a round wait that gave up (never expected) would make the gather unordered
+    if can_one:  # a round wait that gave up (never expected) would make the gather unordered
         t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))],
                          dtype=torch.int64, device=dev)
         dist.all_reduce(t)
@@ -674,7 +711,9 @@ def main():
                                 "one launch per round" if dist_on else "one launch"),
                 "fold_form_by_rank_own_choice": forms_by_rank,
                 "fold_form_ranks_agreed": forms_agree,
-                "fold_form_rank0_broadcast": bool(dist_on and world > 1 and args.variant == 0 and not one_launch),
+                "fold_form_rank0_broadcast": bool(dist_on and world > 1 and args.variant == 0 and per_round_possible),
+                "step_mode": step_mode if dist_on and rounds > 1 else None,
+                "step_mode_probe": mode_probe,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
                 # the kernel form the product's fp32 auto fold takes for one launch of this rank

@@ -199,8 +199,11 @@ class ShardedAggregator:
     fed_avg_aggregator.py:31-35).
     """
 
+    # calls per step form the "auto" mode times before it keeps the faster
+    PROBE_CALLS = 2
+
     def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None,
-                 one_launch: bool = True):
+                 one_launch="auto"):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -211,8 +214,24 @@ class ShardedAggregator:
         self.fold = fold
         # aggregate_slots folds every round of a step in one launch
         # (engine.fold_rounds) and starts each round's exchange behind that
-        # round's completion flag; False: one fold launch per round
+        # round's completion flag (True), or one fold launch per round (False);
+        # "auto": the first calls of a shape alternate the two, each timed on
+        # the device and maxed over the group's ranks, then the faster is kept
+        # for the shape (which wins depends on how much the exchange kernels
+        # slow the fold on this machine)
+        if one_launch not in (True, False, "auto"):
+            raise ValueError(f"one_launch must be True, False or 'auto', not {one_launch!r}")
         self.one_launch = one_launch
+        self._probe: dict = {}  # shape key -> {"one": [ms], "per": [ms]} while probing, or the chosen bool
+
+    def step_form(self, X_local: torch.Tensor, layout: "SlotLayout") -> Optional[str]:
+        """The step form "auto" settled on for this shape ("one launch" /
+        "per round"), or None while it is still timing them."""
+        got = self._probe.get(self._shape_key(X_local, layout))
+        return None if got is None or isinstance(got, dict) else ("one launch" if got else "per round")
+
+    def _shape_key(self, X_local, layout):
+        return (X_local.shape[0], X_local.dtype, tuple(layout.widths), layout.world, layout.P)
 
     def bounds(self, P: int) -> Tuple[int, int]:
         return bucket_bounds(P, self.world)[self.rank]
@@ -272,31 +291,60 @@ class ShardedAggregator:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
         if not X_local.is_cuda or layout.rounds == 1:
             return self._aggregate_slots(X_local, weights, scores, layout, out, total)
-        if self._one_launch_ok(X_local, weights, scores, layout, total):
-            caller = torch.cuda.current_stream(X_local.device)
-            fs = fold_stream(X_local.device)
-            fs.wait_stream(caller)
-            with torch.cuda.stream(fs):
-                full = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
-            caller.wait_stream(fs)
-            full.record_stream(caller)
-            return full
+        one = self._one_launch_ok(X_local, weights, scores, layout, total)
+        probing = None
+        # the probe's schedule and its collective depend only on what every rank
+        # shares (the fold, the layout, the client count), never on this rank's
+        # own buffers: a rank that cannot take the one launch still times its
+        # per-round calls in step with the others
+        if self.one_launch == "auto" and self.default_fold and 1 < layout.rounds <= 8:
+            key = self._shape_key(X_local, layout)
+            got = self._probe.setdefault(key, {"one": [], "per": []})
+            if isinstance(got, dict):  # still timing: the form with fewer timed calls, one launch first
+                probing = (key, "one" if len(got["one"]) <= len(got["per"]) else "per")
+                one = one and probing[1] == "one"
+            else:
+                one = one and got
         # the rounds' folds on a high-priority stream of their own (fold_stream), ordered after
         # the caller's work and before the caller's later work
         caller = torch.cuda.current_stream(X_local.device)
         fs = fold_stream(X_local.device)
         fs.wait_stream(caller)
         with torch.cuda.stream(fs):
-            full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
+            if probing:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(fs)
+            if one:
+                full = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
+            else:
+                full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
+            if probing:
+                ev[1].record(fs)
         caller.wait_stream(fs)
         full.record_stream(caller)
+        if probing:
+            self._record_probe(probing, ev, X_local.device)
         return full
+
+    def _record_probe(self, probing, ev, device) -> None:
+        """One timed call of the "auto" mode: its device time (max over the
+        group's ranks, so every rank keeps the same form); after PROBE_CALLS
+        calls of each form the faster one (best call) is kept for the shape."""
+        key, form = probing
+        ev[1].synchronize()
+        t = torch.tensor([ev[0].elapsed_time(ev[1])], dtype=torch.float64, device=device)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        got = self._probe[key]
+        got[form].append(float(t.item()))
+        if len(got["one"]) >= self.PROBE_CALLS and len(got["per"]) >= self.PROBE_CALLS:
+            self._probe[key] = min(got["one"]) <= min(got["per"])
 
     def _one_launch_ok(self, X_local, weights, scores, layout, total) -> bool:
         import numpy as np
 
         from .engine import result_dtype
-        if not (self.one_launch and self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
+        if not (self.one_launch is not False and self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
             return False
         if X_local.dtype not in (torch.float32, torch.bfloat16) or X_local.stride(1) != 1:
             return False

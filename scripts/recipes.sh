@@ -41,9 +41,9 @@ case "$recipe" in
            "rehearse_c4_w8:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline"
            "rehearse_c4_w8_perround:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline --per-round-launches") ;;
   c4_rank)
-    steps=("c4_rank_one:300:python3 bench.py --rccl-world1 $C4R"
+    steps=("c4_rank_one:300:python3 bench.py --rccl-world1 $C4R --step-mode one"
            "c4_rank_perround:300:python3 bench.py --rccl-world1 $C4R --per-round-launches"
-           "c3_rank_one:300:python3 bench.py --rccl-world1 --config c3 --rounds 4 --steps 10 --no-cpu-baseline"
+           "c3_rank_one:300:python3 bench.py --rccl-world1 --config c3 --rounds 4 --steps 10 --no-cpu-baseline --step-mode one"
            "c3_rank_perround:300:python3 bench.py --rccl-world1 --config c3 --rounds 4 --steps 10 --no-cpu-baseline --per-round-launches") ;;
   exchange)
     steps=("xi_c4_host:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF"
@@ -62,7 +62,7 @@ case "$recipe" in
            "xi_c4_host_step:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF"
            "xi_c4_hbm_step:300:$XI --config c4 --step-forms $S_BF"
            "xi_c3_host_step:400:$XI --config c3 --host-src --scale 0.15 --step-forms $S_F32"
-           "c4_rank_one:300:python3 bench.py --rccl-world1 $C4R"
+           "c4_rank_one:300:python3 bench.py --rccl-world1 $C4R --step-mode one"
            "c4_rank_perround:300:python3 bench.py --rccl-world1 $C4R --per-round-launches") ;;
   final)
     steps=("pytest_gpu:1100:$T -m gpu tests" "smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'"
