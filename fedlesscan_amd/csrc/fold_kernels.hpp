@@ -2402,6 +2402,7 @@ struct StepSpec {
     int grid100;        // blocks per 100 CUs (100: one per CU)
     int sync = 0;       // a pass barrier every `sync` static passes (0: none)
     int quorum100 = 0;  // of the blocks, in percent, a barrier waits for
+    bool last_only = false;  // the pool never reaches past the last round's columns
 };
 constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
@@ -2437,6 +2438,12 @@ constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4w_p100_s3q90", true, 8, 4, 8, 4, 100, 100, 3, 90},
     {"bf16_step_sd_u8c4w_p100_s2q75", true, 8, 4, 8, 4, 100, 100, 2, 75},
     {"f32_step_sd_u8c4_p75_s3q90", false, 8, 4, 16, 1, 75, 100, 3, 90},
+    // the pool confined to the last round: a pool that reaches into round R-2
+    // holds that round's completion flag (and its exchange) until the launch's
+    // last tiles are done
+    {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, 100, 0, 0, true},
+    {"f32_step_sd_u8c4_p75_last", false, 8, 4, 16, 1, 75, 100, 0, 0, true},
+    {"f32_step_sd_u8c4w_p75_last", false, 8, 4, 8, 4, 75, 100, 0, 0, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2473,6 +2480,8 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
     T = StepTable{};
     T.rounds = rounds;
     int64_t pool = sp.pool100 < 0 ? INT64_MAX : (sp.pool100 * grid * wide_cols) / 100;  // columns
+    if (sp.last_only && sp.pool100 >= 0 && pool > offsets[rounds] - offsets[rounds - 1])
+        pool = offsets[rounds] - offsets[rounds - 1];
     int64_t split[kMaxRounds];  // round k: columns [0, split) wide-static, [split, width) narrow-dynamic
     for (int k = rounds - 1; k >= 0; --k) {
         const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
@@ -2618,7 +2627,8 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         case 17: case 18: FA_STB1(8, 4, 8, 4); break;
         case 19: case 21: case 22: case 23: case 24: case 25: FA_STB(8, 4, 8, 4); break;
         case 20: FA_STB(8, 2, 8, 2); break;
-        case 26: FA_STF(8, 4, 16, 1); break;
+        case 26: case 28: FA_STF(8, 4, 16, 1); break;
+        case 27: FA_STB(8, 4, 8, 4); break;
         default: FA_STF(8, 4, 8, 4); break;
     }
 #undef FA_STB1

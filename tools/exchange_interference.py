@@ -132,7 +132,7 @@ def main():
                                   outb.data_ptr() + off * 2, fs.cuda_stream)
         _lib.check(rc, "fold")
 
-    def step(blocks, ev):
+    def step(blocks, ev, end=None):
         for k in range(lay.rounds):
             ev[k][0].record(fs)
             fold(k)
@@ -143,6 +143,8 @@ def main():
                 _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
                            bench=True)
         fs.wait_stream(xs)
+        if end is not None:
+            end.record(fs)
 
     import ctypes as _ct
     offs = (_ct.c_int64 * (lay.rounds + 1))(*[lay.offset(k) for k in range(lay.rounds + 1)])
@@ -152,7 +154,7 @@ def main():
     rs_prod = _ct.c_void_p()
     _lib.check(L.fa_rounds_create(_ct.byref(rs_prod), 0), "rounds state")
 
-    def step_one_launch(sform, blocks, ev):
+    def step_one_launch(sform, blocks, ev, end=None):
         """The whole step in one launch; round k's copy behind a waiter for round k."""
         ev[0][0].record(fs)
         if sform == "product":
@@ -179,6 +181,8 @@ def main():
                 _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
                            bench=True)
         fs.wait_stream(xs)
+        if end is not None:
+            end.record(fs)
 
     for _ in range(3):  # the tuner's first calls, warm-up
         step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -192,15 +196,19 @@ def main():
             step_one_launch(sform, 0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))])
         torch.cuda.synchronize()
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
-            folds = []
+            folds, steps = [], []
             for _ in range(args.steps):
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-                step_one_launch(sform, blocks, ev)
+                end = torch.cuda.Event(enable_timing=True)
+                step_one_launch(sform, blocks, ev, end)
                 torch.cuda.synchronize()
                 folds.append(ev[0][0].elapsed_time(ev[0][1]))
+                steps.append(ev[0][0].elapsed_time(end))
             folds.sort()
+            steps.sort()
             print(f"  {'one launch ' + sform:24s} copy blocks {blocks:3d}: fold per step median "
-                  f"{folds[len(folds) // 2]:.4f} ms (min {folds[0]:.4f})", flush=True)
+                  f"{folds[len(folds) // 2]:.4f} ms (min {folds[0]:.4f}), step (copies included) median "
+                  f"{steps[len(steps) // 2]:.4f} ms", flush=True)
     tmo = L.fa_rounds_timeouts(rs_prod)
     if tmo:
         print(f"  WARNING: {tmo} round waits timed out", flush=True)
@@ -213,21 +221,25 @@ def main():
         label = (fname or ("hint" if args.hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all"
                                                                   else "")
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
-            folds, spans = [], []
+            folds, spans, steps = [], [], []
             for _ in range(args.steps):
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(lay.rounds)]
-                step(blocks, ev)
+                end = torch.cuda.Event(enable_timing=True)
+                step(blocks, ev, end)
                 torch.cuda.synchronize()
                 folds.append(sum(e0.elapsed_time(e1) for e0, e1 in ev))
                 spans.append(ev[0][0].elapsed_time(ev[-1][1]))
+                steps.append(ev[0][0].elapsed_time(end))
             folds.sort()
             spans.sort()
+            steps.sort()
             # fold per step = the rounds' launches summed (gaps between them left out);
             # span = first launch's start to last launch's end on the fold stream, the
             # figure comparable with a one-launch step
             print(f"  {label:24s} copy blocks {blocks:3d}: fold per step median {folds[len(folds) // 2]:.4f} ms "
-                  f"(min {folds[0]:.4f}), span median {spans[len(spans) // 2]:.4f} ms", flush=True)
+                  f"(min {folds[0]:.4f}), span median {spans[len(spans) // 2]:.4f} ms, step (copies included) "
+                  f"median {steps[len(steps) // 2]:.4f} ms", flush=True)
 
 
 if __name__ == "__main__":
