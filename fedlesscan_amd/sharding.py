@@ -73,11 +73,21 @@ def tail_shares(rounds: int, tail: float, steps: int = 1) -> List[float]:
 DEFAULT_TAIL = {"f32": (0.125, 1), "bf16": (0.343, 3)}
 
 
-def overlap_layout(P: int, world: int, dtype: str = "f32", rounds: int = 4, align: int = ALIGN) -> "SlotLayout":
+def overlap_layout(P: int, world: int, dtype: str = "f32", rounds: int = 4, align: int = ALIGN,
+                   quantum: int = 0) -> "SlotLayout":
     """The SlotLayout ShardedAggregator.aggregate_slots should get for a
-    `dtype` ("f32" / "bf16") model of P params over `world` ranks."""
+    `dtype` ("f32" / "bf16") model of P params over `world` ranks (quantum:
+    see SlotLayout, e.g. pass_quantum())."""
     tail, steps = DEFAULT_TAIL[dtype]
-    return SlotLayout(P, world, rounds, align=align, shares=tail_shares(rounds, tail, steps) if rounds > 1 else None)
+    return SlotLayout(P, world, rounds, align=align, shares=tail_shares(rounds, tail, steps) if rounds > 1 else None,
+                      quantum=quantum)
+
+
+def pass_quantum(cus: int, dtype: str = "f32") -> int:
+    """Columns one pass of the one-launch step's wide tiles covers (a block per
+    CU, 256 lanes x 4 quads / octets): a round that is a whole number of
+    passes completes with its last pass instead of a tile-time after it."""
+    return cus * 256 * 4 * (8 if dtype == "bf16" else 4)
 
 
 class SlotLayout:
@@ -97,7 +107,7 @@ class SlotLayout:
     """
 
     def __init__(self, P: int, world: int, rounds: int = 1, align: int = ALIGN,
-                 shares: Optional[Sequence[float]] = None):
+                 shares: Optional[Sequence[float]] = None, quantum: int = 0):
         if world < 1 or rounds < 1:
             raise ValueError("world and rounds must be >= 1")
         self.P, self.world, self.rounds = P, world, rounds
@@ -115,6 +125,19 @@ class SlotLayout:
             self.widths = [align * math.ceil(units * s / (world * tot)) if P else 0 for s in shares]
             while P and world * sum(self.widths) < align * units:  # float rounding slack
                 self.widths[0] += align
+        if quantum and rounds > 1 and P:
+            # every round but the last a whole number of `quantum` columns (the
+            # nearest, at least one), the last round the rest
+            if quantum % align:
+                raise ValueError(f"quantum {quantum} is not a multiple of align {align}")
+            total = sum(self.widths)
+            head = [max(quantum, quantum * round(w / quantum)) for w in self.widths[:-1]]
+            while sum(head) > total - align:  # the last round keeps at least one align unit
+                i = max(range(len(head)), key=lambda j: head[j])
+                if head[i] <= quantum:
+                    raise ValueError(f"{rounds} rounds of {quantum}-column quanta do not fit {total} columns")
+                head[i] -= quantum
+            self.widths = head + [total - sum(head)]
         self.sub = self.widths[0]  # the uniform layout's slot width (offset(k) = k*sub there)
         self._offs = [0]
         for w in self.widths:

@@ -65,6 +65,33 @@ def test_slot_layout_partitions_the_vector():
                     assert [lay.slot(r, 0) for r in range(world)] == bucket_bounds(P, world)
 
 
+def test_quantized_slot_layout():
+    """quantum: every round but the last a whole number of quanta (the nearest,
+    at least one), the last the rest; the rounds still partition [0, P)."""
+    from fedlesscan_amd.sharding import pass_quantum
+    assert pass_quantum(256, "bf16") == 2_097_152 and pass_quantum(256, "f32") == 1_048_576
+    lay = overlap_layout(100_000_000, 8, "bf16", quantum=pass_quantum(256, "bf16"))
+    assert lay.widths == [4_194_304, 4_194_304, 2_097_152, 2_014_400]
+    assert lay.local_width == overlap_layout(100_000_000, 8, "bf16").local_width
+    lay = overlap_layout(80_000_000, 8, quantum=pass_quantum(256, "f32"))
+    assert lay.widths == [3_145_728] * 3 + [562_816]
+    for P, world, rounds, q in ((10007, 2, 4, 128), (1_000_003, 3, 4, 4096), (64 * 8 * 5, 8, 4, 64),
+                                (300_000, 2, 3, 65536)):
+        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, 0.25), quantum=q)
+        assert all(w % q == 0 and w >= q for w in lay.widths[:-1]) and lay.widths[-1] >= 64
+        assert world * lay.local_width >= P
+        cover = sorted((lo, hi) for r in range(world) for lo, hi in lay.slots(r) if hi > lo)
+        pos = 0
+        for lo, hi in cover:
+            assert lo == pos
+            pos = hi
+        assert pos == P
+    with pytest.raises(ValueError):
+        SlotLayout(10007, 2, 4, quantum=100)  # not a multiple of the alignment
+    with pytest.raises(ValueError):
+        SlotLayout(1000, 2, 4, quantum=64 * 64)  # four rounds of quanta do not fit
+
+
 def test_tail_shares():
     assert tail_shares(4, 1.0) == [1.0] * 4
     assert tail_shares(4, 0.25) == [1.0, 1.0, 1.0, 0.25]
@@ -147,12 +174,12 @@ def test_sharded_fold_gloo_matches_oracle(world, P, scored):
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
 
 
-def _slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
+def _slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0, quantum=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         agg = ShardedAggregator(fold=_oracle_fold)
-        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, tail))
+        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, tail), quantum=quantum)
         X = torch.zeros((N, lay.local_width))
         for k, (lo, hi) in enumerate(lay.slots(rank)):
             if hi > lo:
@@ -165,16 +192,18 @@ def _slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,P,rounds,tail", [(2, 10007, 3, 1.0), (3, 5000, 2, 1.0), (2, 64, 4, 1.0),
-                                                 (2, 10007, 4, 0.25), (3, 20000, 3, 0.1)])
-def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds, tail):
-    """Equal rounds and a short last round (tail_shares) reassemble the same model."""
+@pytest.mark.parametrize("world,P,rounds,tail,quantum", [(2, 10007, 3, 1.0, 0), (3, 5000, 2, 1.0, 0),
+                                                         (2, 64, 4, 1.0, 0), (2, 10007, 4, 0.25, 0),
+                                                         (3, 20000, 3, 0.1, 0), (3, 20000, 4, 0.25, 1024)])
+def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds, tail, quantum):
+    """Equal rounds, a short last round (tail_shares) and rounds in whole
+    quanta reassemble the same model."""
     from oracle import fedavg_oracle as O
     N, seed = 7, 23
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, N, P, rounds, seed, q, tail))
+    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, N, P, rounds, seed, q, tail, quantum))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -21,7 +21,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedlesscan_amd import _lib, synth  # noqa: E402
 from fedlesscan_amd.engine import Factors  # noqa: E402
-from fedlesscan_amd.sharding import fold_stream, overlap_layout  # noqa: E402
+from fedlesscan_amd.sharding import fold_stream, overlap_layout, pass_quantum  # noqa: E402
 
 
 def main():
@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--step-forms", default="",
                     help="comma-separated step forms (fa_step_form_name; 'product' = fa_fedavg_*_rounds): the whole "
                          "step in ONE launch, each round's copy queued behind fa_*_rounds_wait on the copy stream")
+    ap.add_argument("--quantum", default="0",
+                    help="round slot widths in whole quanta of columns (SlotLayout quantum): a number, or 'pass' "
+                         "(sharding.pass_quantum: one pass of the one-launch step's wide tiles), or 'half'")
     ap.add_argument("--hint", action="store_true",
                     help="the product's shared-CU hint (fa_fedavg_*_ex, FA_HINT_SHARED) on the overlapped rounds")
     args = ap.parse_args()
@@ -58,7 +61,10 @@ def main():
         P_total = P_rank * args.world
     else:
         N, P_total, dt, esz, out_esz = 256, 100_000_000, "bf16", 2, 2
-    lay = overlap_layout(P_total, args.world, dt, rounds=args.rounds)
+    cus0 = torch.cuda.get_device_properties(dev).multi_processor_count
+    q = (pass_quantum(cus0, dt) if args.quantum == "pass" else pass_quantum(cus0, dt) // 2 if args.quantum == "half"
+         else int(args.quantum))
+    lay = overlap_layout(P_total, args.world, dt, rounds=args.rounds, quantum=q)
     W = lay.local_width
     st0 = torch.cuda.current_stream(dev)
     X = torch.empty((N, W), dtype=torch.float32 if dt == "f32" else torch.bfloat16, device=dev)
