@@ -107,6 +107,7 @@ def main():
     else:
         names = {B.fa_bf16_form_name(i).decode(): i for i in range(B.fa_num_bf16_forms())}
     form = [None]
+    hint_on = [False]  # the shared-CU hint on rounds 1.. (--hint: timed after the tuned forms)
 
     def fold(k):
         off, width = lay.offset(k), lay.width(k)
@@ -122,7 +123,7 @@ def main():
                                        outb.data_ptr() + off * 2, fs.cuda_stream, form[0])
             _lib.check(rc, "form", bench=True)
             return
-        if args.hint and k > 0:
+        if hint_on[0] and k > 0:
             if dt == "f32":
                 rc = L.fa_fedavg_f32_ex(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, 1,
                                         fs.cuda_stream)
@@ -218,14 +219,17 @@ def main():
     tmo = L.fa_rounds_timeouts(rs_prod)
     if tmo:
         print(f"  WARNING: {tmo} round waits timed out", flush=True)
-    for fname in [f for f in args.forms.split(",") if f] or [None]:
+    variants = [(f, False) for f in args.forms.split(",") if f] or [(None, False)]
+    if args.hint:
+        variants.append((None, True))
+    for fname, hint in variants:
         form[0] = None if fname is None else names[fname]
+        hint_on[0] = hint
         for _ in range(2):  # warm the forced form
             step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in range(lay.rounds)])
         torch.cuda.synchronize()
-        label = (fname or ("hint" if args.hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all"
-                                                                  else "")
+        label = (fname or ("hint" if hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all" else "")
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
             folds, spans, steps = [], [], []
             for _ in range(args.steps):
