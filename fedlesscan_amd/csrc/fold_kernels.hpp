@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(B) void k_fold_f32_dynp(
 //   launch acquire.  A waiter gives up after `max_ticks` of the device wall
 //   clock (never an endless spin), counting a timeout in the signal words.
 // ---------------------------------------------------------------------------
-constexpr int kMaxRounds = 8, kMaxSegs = 2 * kMaxRounds;
+constexpr int kMaxRounds = 8, kMaxSegs = 3 * kMaxRounds;
 // The launch's tiles, in column order: segment g covers local columns
 // [col0[g], col0[g] + width[g]) of round round[g] with wide tiles (small[g] = 0)
 // or narrow ones (1); its tiles are [seg_end[g-1], seg_end[g]) of the launch.
@@ -2403,6 +2403,7 @@ struct StepSpec {
     int sync = 0;       // a pass barrier every `sync` static passes (0: none)
     int quorum100 = 0;  // of the blocks, in percent, a barrier waits for
     bool last_only = false;  // the pool never reaches past the last round's columns
+    bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
 };
 constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
@@ -2444,17 +2445,45 @@ constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, 100, 0, 0, true},
     {"f32_step_sd_u8c4_p75_last", false, 8, 4, 16, 1, 75, 100, 0, 0, true},
     {"f32_step_sd_u8c4w_p75_last", false, 8, 4, 8, 4, 75, 100, 0, 0, true},
+    // a round's wide tiles past its last whole pass become narrow static tiles
+    // spread over the blocks, so the round completes closer to its share of
+    // the launch (its exchange starts earlier) than a partial pass of wide tiles
+    {"bf16_step_rt_u8c4n16c1_p100_last", true, 8, 4, 16, 1, 100, 100, 0, 0, true, true},
+    {"f32_step_rt_u8c4n16c1_p75_last", false, 8, 4, 16, 1, 75, 100, 0, 0, true, true},
+    {"bf16_step_rt_u8c4n8c2_p100_last", true, 8, 4, 8, 2, 100, 100, 0, 0, true, true},
+    {"bf16_step_rt_u8c4n8c2_p50_last", true, 8, 4, 8, 2, 50, 100, 0, 0, true, true},
+    {"bf16_step_rt_u8c4n16c2_p100_last", true, 8, 4, 16, 2, 100, 100, 0, 0, true, true},
+    {"f32_step_rt_u8c4n8c2_p75_last", false, 8, 4, 8, 2, 75, 100, 0, 0, true, true},
+    {"f32_step_rt_u8c4n8c2_p0", false, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
+    {"bf16_step_rt_u8c4n8c2_p0", true, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
-// The policy's step forms (profiles/r04_step/): for a C4 rank's bf16 slots,
-// wide 8 x 4-octet tiles dealt statically over the step with one pass of them
-// left to the counter (1.01-1.02 ms alone, 1.06-1.13 beside the proxy copy,
-// against 0.96 / 1.06-1.18 for per-round static launches); for a C3 rank's
-// fp32 slots, 8 x 4-quad static tiles and a pool of 0.75 passes in 16 x
-// 1-quad tiles (5.84-5.94 alone, 5.91-6.05 beside the copy, against 5.81-5.85
-// / 6.05-6.19).
-inline int pick_step(bool bf16) { return bf16 ? 2 : 7; }
+// The policy's step forms.  Measured on the whole step with the exchange
+// proxy's copies included (profiles/r04_step/round_tail/), not the fold
+// alone: a round's flag is what starts its exchange, so WHEN each round
+// completes counts as much as the fold's length.  bf16 (a C4 rank's slots):
+// whole passes of 8 x 4-octet wide tiles per round, the rest of each round in
+// 8 x 2-octet static tiles over all blocks (the round completes near its share
+// of the launch instead of a tile-time later), and the last round dynamic
+// (1.01 ms alone; 1.21-1.26 host / 1.20-2.00 HBM beside the copies against
+// 1.22-1.30 / 1.25-2.06 for per-round launches).  fp32 (a C3 rank): 8 x 4-quad
+// static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
+// 6.23-6.27 beside host copies, about even with per-round launches); the
+// round-tail forms lost there.  ShardedAggregator / bench.py pick between
+// this and per-round launches by measurement where they run ("auto").
+constexpr bool name_eq(const char* a, const char* b) { return *a == *b && (*a == 0 || name_eq(a + 1, b + 1)); }
+constexpr int step_form_index(const char* name) {
+    for (int i = 0; i < kNumStepForms; ++i)
+        if (name_eq(kStepSpecs[i].name, name)) return i;
+    return -1;
+}
+inline int pick_step(bool bf16) {
+    constexpr int kBf16 = step_form_index("bf16_step_rt_u8c4n8c2_p100_last");
+    constexpr int kF32 = step_form_index("f32_step_sd_u8c4_p75");
+    static_assert(kBf16 >= 0 && kF32 >= 0, "policy step forms");
+    return bf16 ? kBf16 : kF32;
+}
 
 // The per-launch state of fa_fedavg_*_rounds: the signal words in device
 // memory and the host epoch (fa_rounds in fedavg_hip.h).
@@ -2500,21 +2529,33 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
     // static segments first (all of them precede every dynamic one in column
     // order: only a suffix of the step is dynamic), then the dynamic ones
     const bool wide_dyn = sp.pool100 < 0;
+    auto add_seg = [&](int k, int64_t lo, int64_t hi, bool small, bool is_static) {
+        const int64_t c0 = offsets[k];
+        const int64_t per = small ? (int64_t)kBlock * sp.cs : (int64_t)kBlock * sp.cb;
+        const int g = T.segs++;
+        total += (units(hi - lo) + per - 1) / per;
+        T.seg_end[g] = total;
+        T.col0[g] = c0 + lo;
+        T.width[g] = hi - lo;
+        T.round[g] = k;
+        T.small[g] = small ? 1 : 0;
+        T.round_tiles[k] += (units(hi - lo) + per - 1) / per;
+        if (is_static) T.static_tiles = total;
+    };
     for (int pass = 0; pass < 2; ++pass)
         for (int k = 0; k < rounds; ++k) {
-            const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
+            const int64_t w = offsets[k + 1] - offsets[k];
             const int64_t lo = pass == 0 ? 0 : split[k], hi = pass == 0 ? split[k] : w;
             if (hi <= lo) continue;
-            const int64_t per = (pass == 0 || wide_dyn) ? (int64_t)kBlock * sp.cb : (int64_t)kBlock * sp.cs;
-            const int g = T.segs++;
-            total += (units(hi - lo) + per - 1) / per;
-            T.seg_end[g] = total;
-            T.col0[g] = c0 + lo;
-            T.width[g] = hi - lo;
-            T.round[g] = k;
-            T.small[g] = (pass == 1 && !wide_dyn) ? 1 : 0;
-            T.round_tiles[k] += (units(hi - lo) + per - 1) / per;
-            if (pass == 0) T.static_tiles = total;
+            if (pass == 0 && sp.round_tail && k + 1 < rounds) {
+                // whole passes of wide tiles, then the rest of the round's static columns narrow
+                const int64_t full = ((hi - lo) / wide_cols / grid) * grid;
+                const int64_t mid = lo + full * wide_cols;
+                if (mid > lo) add_seg(k, lo, mid, false, true);
+                if (hi > mid) add_seg(k, mid, hi, true, true);
+                continue;
+            }
+            add_seg(k, lo, hi, pass == 1 && !wide_dyn, pass == 0);
         }
     (void)narrow_cols;
     if (total > 0x7FFFFFFF) return fail(FA_ERR_ARG, "rounds fold: too many tiles");
@@ -2629,6 +2670,11 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         case 20: FA_STB(8, 2, 8, 2); break;
         case 26: case 28: FA_STF(8, 4, 16, 1); break;
         case 27: FA_STB(8, 4, 8, 4); break;
+        case 30: FA_STB(8, 4, 16, 1); break;
+        case 31: FA_STF(8, 4, 16, 1); break;
+        case 32: case 33: case 37: FA_STB(8, 4, 8, 2); break;
+        case 34: FA_STB(8, 4, 16, 2); break;
+        case 35: case 36: FA_STF(8, 4, 8, 2); break;
         default: FA_STF(8, 4, 8, 4); break;
     }
 #undef FA_STB1
