@@ -2404,6 +2404,7 @@ struct StepSpec {
     int quorum100 = 0;  // of the blocks, in percent, a barrier waits for
     bool last_only = false;  // the pool never reaches past the last round's columns
     bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
+    bool sc1 = false;         // outputs stored sc1 (bf16 forms)
 };
 constexpr StepSpec kStepSpecs[] = {
     {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
@@ -2426,8 +2427,8 @@ constexpr StepSpec kStepSpecs[] = {
     {"f32_step_sd_u8c4_p75_g80", false, 8, 4, 16, 1, 75, 80},
     {"f32_step_sd_u8c4_p75_g90", false, 8, 4, 16, 1, 75, 90},
     // outputs stored sc1 (no dirty L2 lines for the per-round release to write back)
-    {"bf16_step_sd_u8c4w_p100_sc1", true, 8, 4, 8, 4, 100, 100},
-    {"bf16_step_u8c4_sc1", true, 8, 4, 8, 4, -1, 100},
+    {"bf16_step_sd_u8c4w_p100_sc1", true, 8, 4, 8, 4, 100, 100, 0, 0, false, false, true},
+    {"bf16_step_u8c4_sc1", true, 8, 4, 8, 4, -1, 100, 0, 0, false, false, true},
     // every tile static (no pool): the one launch's cost without the dynamic part
     {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0, 100},
     {"bf16_step_static_u8c2", true, 8, 2, 8, 2, 0, 100},
@@ -2644,42 +2645,42 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
     const float* Xf = static_cast<const float*>(X);
-#define FA_STB(UB, CB, US, CS)                                                                                 \
-    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), \
-                              0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);                  \
-    else hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
-                            dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
-#define FA_STB1(UB, CB, US, CS)                                                                                \
-    if (s) hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, true>), dim3((unsigned)grid),   \
-                              dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
-    else hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, true>), dim3((unsigned)grid),    \
-                            dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch)
-#define FA_STF(UB, CB, US, CS)                                                                                \
-    if (s) hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid), dim3(kBlock), \
-                              0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);                       \
-    else hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),             \
-                            dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch)
-    switch (f) {
-        case 0: case 1: case 14: FA_STB(8, 4, 16, 1); break;
-        case 2: case 5: case 11: case 12: case 13: FA_STB(8, 4, 8, 4); break;
-        case 3: case 6: FA_STB(16, 2, 16, 2); break;
-        case 4: FA_STB(8, 2, 8, 2); break;
-        case 7: case 8: case 9: case 15: case 16: FA_STF(8, 4, 16, 1); break;
-        case 17: case 18: FA_STB1(8, 4, 8, 4); break;
-        case 19: case 21: case 22: case 23: case 24: case 25: FA_STB(8, 4, 8, 4); break;
-        case 20: FA_STB(8, 2, 8, 2); break;
-        case 26: case 28: FA_STF(8, 4, 16, 1); break;
-        case 27: FA_STB(8, 4, 8, 4); break;
-        case 30: FA_STB(8, 4, 16, 1); break;
-        case 31: FA_STF(8, 4, 16, 1); break;
-        case 32: case 33: case 37: FA_STB(8, 4, 8, 2); break;
-        case 34: FA_STB(8, 4, 16, 2); break;
-        case 35: case 36: FA_STF(8, 4, 8, 2); break;
-        default: FA_STF(8, 4, 8, 4); break;
+    // the kernel instantiation is found from the form's tile shapes (never by
+    // its index): a form whose shapes no instantiation below has is refused
+    bool launched = false;
+#define FA_STB(UB, CB, US, CS, SC1)                                                                                \
+    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.sc1 == SC1) {     \
+        launched = true;                                                                                         \
+        if (s)                                                                                                   \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, SC1>), dim3((unsigned)grid),    \
+                               dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, SC1>), dim3((unsigned)grid),   \
+                               dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
     }
-#undef FA_STB1
+#define FA_STF(UB, CB, US, CS)                                                                                    \
+    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && !sp.sc1) {          \
+        launched = true;                                                                                         \
+        if (s)                                                                                                   \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid),            \
+                               dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
+                               dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
+    }
+    FA_STB(8, 4, 16, 1, false)
+    FA_STB(8, 4, 8, 4, false)
+    FA_STB(16, 2, 16, 2, false)
+    FA_STB(8, 2, 8, 2, false)
+    FA_STB(8, 4, 8, 2, false)
+    FA_STB(8, 4, 16, 2, false)
+    FA_STB(8, 4, 8, 4, true)
+    FA_STF(8, 4, 16, 1)
+    FA_STF(8, 4, 8, 4)
+    FA_STF(8, 4, 8, 2)
 #undef FA_STB
 #undef FA_STF
+    if (!launched) return fail(FA_ERR_ARG, "step form %s: no kernel for its tile shapes", sp.name);
     rc = check_launch("rounds fold");
     if (rc) return rc;
     R.epoch = epoch;
