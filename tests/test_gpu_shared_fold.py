@@ -214,6 +214,40 @@ def test_f32_one_launch_steps_at_the_c3_rank_layout(dev, libs, scored):
             assert _same(o[c0:c0 + nc], exp), (name, c0)
 
 
+@pytest.mark.parametrize("bf16", [False, True])
+def test_one_launch_steps_many_small_rounds(dev, libs, bf16):
+    """Eight rounds, most narrower than one pass of wide tiles (the round-tail
+    forms then fold whole rounds in narrow static tiles, the segment table is
+    at its largest), an odd client count, stall-aware: every step form and the
+    product's rounds fold with its waits, every column."""
+    from fedlesscan_amd.sharding import SlotLayout, tail_shares
+    _lib, L, B = libs
+    N, seed = 37, 97
+    lay = SlotLayout(3_000_000, 1, 8, shares=tail_shares(8, 0.05, 5))
+    W = lay.local_width
+    st = torch.cuda.current_stream(dev).cuda_stream
+    X = torch.empty((N, W), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
+    gen = B.fa_synth_bf16 if bf16 else B.fa_synth_f32
+    _lib.check(gen(X.data_ptr(), N, W, W, seed, 0, 0, st), "synth", bench=True)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    s = torch.tensor(np.array(sc, np.float32), device=dev)
+    div = float(np.float32(sum(w)))
+    one = _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16=bf16)
+    an, sn = np.array(w, np.float32), np.array(sc, np.float32)
+    if bf16:
+        ef, eb = OL.fedavg_bf16(OL.synth_bf16(seed, N, W), an, np.float32(sum(w)), s=sn)
+        for name, (o, ob) in one.items():
+            if o is not None:
+                assert _same(o, ef), name
+            assert np.array_equal(ob, eb), name
+    else:
+        exp = OL.fedavg_f32(OL.synth_f32(seed, N, W), an, np.float32(sum(w)), s=sn)
+        for name, (o, _) in one.items():
+            assert _same(o, exp), name
+
+
 def test_rounds_entry_errors(dev, libs):
     """Argument errors are reported, never launched: empty or misaligned
     rounds, too many rounds, a wait before any launch or past the last
