@@ -254,7 +254,10 @@ class ShardedAggregator:
         return None if got is None or isinstance(got, dict) else ("one launch" if got else "per round")
 
     def _shape_key(self, X_local, layout):
-        return (X_local.shape[0], X_local.dtype, tuple(layout.widths), layout.world, layout.P)
+        # clients by power-of-two bucket (the count changes from round to round
+        # with stragglers; a form's advantage does not), the layout exactly
+        n = int(X_local.shape[0])
+        return (1 << max(0, n - 1).bit_length(), X_local.dtype, tuple(layout.widths), layout.world, layout.P)
 
     def bounds(self, P: int) -> Tuple[int, int]:
         return bucket_bounds(P, self.world)[self.rank]
@@ -322,6 +325,8 @@ class ShardedAggregator:
         # per-round calls in step with the others
         if self.one_launch == "auto" and self.default_fold and 1 < layout.rounds <= 8:
             key = self._shape_key(X_local, layout)
+            if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
+                self._probe.pop(next(iter(self._probe)))
             got = self._probe.setdefault(key, {"one": [], "per": []})
             if isinstance(got, dict):  # still timing: the form with fewer timed calls, one launch first
                 probing = (key, "one" if len(got["one"]) <= len(got["per"]) else "per")
