@@ -73,6 +73,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-s", type=float, default=0.0,
+                    help="after the W warm-up steps, more untimed steps until about this many seconds of warm-up "
+                         "have run (the same count on every rank); 0 (default) = exactly W.  Measured A/B on one "
+                         "box: C3 unchanged (7060-7068 GB/s either way), C2 slower after 10,000 extra launches "
+                         "(5.7-6.2 TB/s against 6.7-6.8; profiles/r04_warmup_ab.log)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr table)")
@@ -562,8 +567,22 @@ def main():
         mode_probe = {"one_launch_ms": round(best["one"], 4), "per_round_ms": round(best["per-round"], 4),
                       "chosen": "one launch" if one_launch else "per round",
                       "how": "wall time of 5 steps between barriers, max over ranks, best of 2 trials per form"}
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize()
+    warm_extra = 0
+    if args.warmup_s > 0:
+        spent = time.perf_counter() - tw
+        per = spent / max(1, args.warmup)
+        warm_extra = max(0, min(10_000, int((args.warmup_s - spent) / max(per, 1e-6)) + 1)) if spent < args.warmup_s \
+            else 0
+        if dist_on:  # every rank runs the same number of steps (each has collectives)
+            t = torch.tensor([warm_extra], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            warm_extra = int(t.item())
+        for _ in range(warm_extra):
+            step()
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(rounds)], torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist_on:
@@ -687,6 +706,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_steps": warm_extra,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": wl.scaling,
