@@ -2457,6 +2457,9 @@ constexpr StepSpec kStepSpecs[] = {
     {"f32_step_rt_u8c4n8c2_p75_last", false, 8, 4, 8, 2, 75, 100, 0, 0, true, true},
     {"f32_step_rt_u8c4n8c2_p0", false, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
     {"bf16_step_rt_u8c4n8c2_p0", true, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
+    {"bf16_step_rt_u8c4n8c2_p100_last_s3q90", true, 8, 4, 8, 2, 100, 100, 3, 90, true, true},
+    {"bf16_step_rt_u8c4n8c2_p100_last_s2q90", true, 8, 4, 8, 2, 100, 100, 2, 90, true, true},
+    {"bf16_step_rt_u8c4n8c2_p100_last_g90", true, 8, 4, 8, 2, 100, 90, 0, 0, true, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
