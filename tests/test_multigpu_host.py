@@ -149,3 +149,20 @@ def test_bench_default_slot_layouts():
             covered = sorted(sl for r in range(world) for sl in lay.slots(r) if sl[1] > sl[0])
             assert covered[0][0] == 0 and covered[-1][1] == P_total
             assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+
+
+def test_bench_step_mode_flags(monkeypatch):
+    """--step-mode auto (default) / one / per-round; --per-round-launches is
+    per-round; --warmup-s defaults to exactly W warm-up steps."""
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert a.step_mode == "auto" and not a.per_round_launches and a.warmup_s == 0.0
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--step-mode", "one", "--warmup-s", "1.5"])
+    a = bench.parse()
+    assert a.step_mode == "one" and a.warmup_s == 1.5
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--per-round-launches"])
+    assert bench.parse().per_round_launches
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--step-mode", "sometimes"])
+    with pytest.raises(SystemExit):
+        bench.parse()
