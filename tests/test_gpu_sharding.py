@@ -108,6 +108,35 @@ def test_auto_step_form_settles_and_stays_exact(bf16):
         ShardedAggregator(one_launch="sometimes")
 
 
+@pytest.mark.parametrize("one_launch", [True, False])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_quantised_layout_world1(one_launch, bf16):
+    """Rounds in whole quanta (SlotLayout quantum), both step forms, bit-exact."""
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout, tail_shares
+    from oracle import fedavg_oracle as O
+    dev = torch.device("cuda", 0)
+    N, P, seed = 45, 300_001, 14
+    lay = SlotLayout(P, 1, 4, shares=tail_shares(4, 0.25), quantum=4096)
+    assert all(w % 4096 == 0 for w in lay.widths[:-1])
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N)
+    if bf16:
+        X = torch.zeros((N, lay.local_width), dtype=torch.int16, device=dev)
+        Xb = synth.clients_bf16(seed, N, 0, P)
+        src = Xb.view(np.int16)
+        _, exp = O.fedavg_stacked_bf16(Xb, w, sc)
+    else:
+        X = torch.zeros((N, lay.local_width), dtype=torch.float32, device=dev)
+        src = synth.clients_f32(seed, N, 0, P)
+        exp = O.fedavg_stacked(src, w, sc).view(np.uint32)
+    for k, (lo, hi) in enumerate(lay.slots(0)):
+        if hi > lo:
+            X[:, lay.offset(k):lay.offset(k) + hi - lo] = torch.from_numpy(src[:, lo:hi]).to(dev)
+    full = ShardedAggregator(one_launch=one_launch).aggregate_slots(X.view(torch.bfloat16) if bf16 else X, w, sc, lay)
+    got = full.view(torch.int16).cpu().numpy().view(np.uint16) if bf16 else full.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, exp)
+
+
 def test_aggregate_layers_world1_matches_reference_goldens():
     """The reference's own fixture shapes through the sharded per-layer entry."""
     from fedlesscan_amd.sharding import ShardedAggregator
