@@ -106,11 +106,13 @@ def parse():
                     help="last exchange round's slot as a fraction of the others' (its all-gather is the one "
                          "left exposed after the step's folds); 1 = equal rounds.  Default with several rounds: "
                          "the layout for the dtype (DEFAULT_TAIL)")
-    ap.add_argument("--step-mode", default="auto", choices=["auto", "one", "per-round"],
+    ap.add_argument("--step-mode", default="auto", choices=["auto", "probe", "one", "per-round"],
                     help="with several rounds under a process group: 'one' = the whole step in one fold launch, "
                          "each round's all-gather started behind its completion flag; 'per-round' = one fold "
-                         "launch per exchange round (round 3's step); 'auto' (default) = time both on this run's "
-                         "own ranks before the warm-up (max over ranks, best of two trials) and keep the faster")
+                         "launch per exchange round (round 3's step); 'probe' = time both on this run's own "
+                         "ranks before the warm-up (max over ranks, best of two trials), keep the faster and "
+                         "record it in the tuner's cache file (fa_step_record); 'auto' (default) = the form "
+                         "recorded for this machine and shape (rank 0's record), or 'probe' when none is")
     ap.add_argument("--per-round-launches", action="store_true", help="same as --step-mode per-round")
     ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
@@ -423,8 +425,18 @@ def main():
     tune_calls = 0
     step_mode = "per-round" if args.per_round_launches else args.step_mode
     can_one = dist_on and rounds > 1 and args.variant == 0 and step_mode != "per-round"
-    probe_modes = can_one and step_mode == "auto"  # both step forms timed below, the faster kept
-    one_launch = can_one
+    # "auto": the step form recorded for this machine and shape (the product's
+    # ShardedAggregator reads the same record), or, with none, both forms timed
+    # below and the faster recorded; "probe": time them whatever is recorded
+    from fedlesscan_amd.sharding import device_ident, step_key as make_step_key
+    skey = make_step_key(device_ident(dev), wl.dtype == "bf16", wl.N, lay) if can_one else None
+    recorded = L.fa_step_lookup(skey.encode()) if (can_one and step_mode == "auto") else -1
+    if can_one and world > 1:  # every rank runs rank 0's record (ranks may share no cache file)
+        t = torch.tensor([recorded], dtype=torch.int64, device=dev)
+        dist.broadcast(t, src=0)
+        recorded = int(t.item())
+    probe_modes = can_one and step_mode in ("auto", "probe") and recorded < 0
+    one_launch = can_one and (recorded != 0)
     per_round_possible = not can_one or probe_modes
     if args.variant == 0 and L.fa_set_autotune(-1) == 1 and per_round_possible:
         for tune_calls in range(1, 201):
@@ -564,9 +576,14 @@ def main():
                 res[m].append(float(t.item()) / 5 * 1e3)
         best = {m: min(v) for m, v in res.items()}
         one_launch = best["one"] <= best["per-round"]
+        _lib.call("fa_step_record", skey.encode(), 1 if one_launch else 0)  # for the product and later runs
         mode_probe = {"one_launch_ms": round(best["one"], 4), "per_round_ms": round(best["per-round"], 4),
                       "chosen": "one launch" if one_launch else "per round",
-                      "how": "wall time of 5 steps between barriers, max over ranks, best of 2 trials per form"}
+                      "how": "wall time of 5 steps between barriers, max over ranks, best of 2 trials per form",
+                      "recorded": skey}
+    elif can_one and recorded >= 0:
+        mode_probe = {"chosen": "one launch" if one_launch else "per round", "restored": skey,
+                      "how": "recorded by an earlier probe (fa_step_lookup): no timing run"}
     tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
@@ -644,7 +661,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
-    if can_one:  # a round wait that gave up (never expected) would make the gather unordered
+    if can_one:  # a round wait that gave up (never expected) let an exchange read an unfinished round
         t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))],
                          dtype=torch.int64, device=dev)
         dist.all_reduce(t)
@@ -781,6 +798,11 @@ def main():
                                       * (world - 1) // world) if dist_on else 0,
         }
         print(json.dumps(line), file=out, flush=True)
+        if timeouts:
+            # an exchange behind a timed-out round wait read an unfinished round: the
+            # line above is reported, the run fails (ShardedAggregator raises the same)
+            from fedlesscan_amd.aggregator.exceptions import AggregationError
+            raise AggregationError(f"{timeouts} round wait(s) timed out during the run")
     if dist_on:
         dist.destroy_process_group()
 

@@ -27,10 +27,9 @@ BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
 HOSTFAST_PATH = os.path.join(PKG, "_native", "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FA_OK, FA_ERR_ARG, FA_ERR_NO_CLIENTS, FA_ERR_SHAPE, FA_ERR_HIP = range(5)
-FA_HINT_SHARED = 1  # fa_fedavg_*_ex: other kernels share the GPU during the fold
 
 _i64 = ctypes.c_int64
 _vp = ctypes.c_void_p
@@ -53,13 +52,12 @@ _PROTOS = {
     "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),
     "fa_finalize_f32": (_int, [_vp, _f32, _vp, _i64, _vp]),
     "fa_fedavg_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
-    "fa_fedavg_f32_ex": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp]),
-    "fa_fedavg_bf16_ex": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp]),
     "fa_rounds_create": (_int, [_vp, _int]),
     "fa_rounds_destroy": (_int, [_vp]),
     "fa_fedavg_f32_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
     "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
     "fa_rounds_wait": (_int, [_vp, _int, _vp]),
+    "fa_rounds_check": (_int, [_vp]),
     "fa_rounds_timeouts": (_int, [_vp]),
     "fa_rounds_form": (ctypes.c_char_p, [_int]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
@@ -81,6 +79,8 @@ _PROTOS = {
     "fa_tune_cache_path": (_int, [ctypes.c_char_p]),
     "fa_tune_export": (_i64, [_vp, _i64]),
     "fa_tune_import": (_int, [ctypes.c_char_p]),
+    "fa_step_lookup": (_int, [ctypes.c_char_p]),
+    "fa_step_record": (_int, [ctypes.c_char_p, _int]),
     "fa_ingest_create": (_int, [_vp, _i64, _i64, _int, _int]),
     "fa_ingest_rows_per_chunk": (_int, [_vp]),
     "fa_ingest_begin": (_int, [_vp, _vp, _vp, _i64]),

@@ -213,18 +213,6 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const f
     return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
 }
 
-int fa_fedavg_f32_ex(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                     float divisor, float* out, int hints, void* stream) {
-    if (hints & ~FA_HINT_SHARED) return fail(FA_ERR_ARG, "unknown fold hints 0x%x", hints);
-    return fold_f32_auto(X, N, P, ldx, a, s, nullptr, divisor, 1, out, stream, hints);
-}
-
-int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                      float divisor, float* out_f32, uint16_t* out_bf16, int hints, void* stream) {
-    if (hints & ~FA_HINT_SHARED) return fail(FA_ERR_ARG, "unknown fold hints 0x%x", hints);
-    return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream, hints);
-}
-
 // ---- one launch per exchange step -------------------------------------------
 struct fa_rounds : RoundsState {};
 
@@ -274,6 +262,11 @@ int fa_rounds_wait(fa_rounds* r, int round, void* stream) {
     return rounds_wait(*r, round, (hipStream_t)stream);
 }
 
+int fa_rounds_check(fa_rounds* r) {
+    if (!r) return -fail(FA_ERR_ARG, "null fa_rounds");
+    return rounds_check(*r);
+}
+
 int fa_rounds_timeouts(fa_rounds* r) {
     if (!r) return -fail(FA_ERR_ARG, "null fa_rounds");
     int prev = 0;
@@ -284,6 +277,18 @@ int fa_rounds_timeouts(fa_rounds* r) {
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return -fail(FA_ERR_HIP, "fa_rounds_timeouts: %s", hipGetErrorString(e));
     return (int)v;
+}
+
+int fa_step_lookup(const char* key) {
+    if (!key) return -2;
+    return g_tuner.step_lookup(std::string(key));
+}
+
+int fa_step_record(const char* key, int one_launch) {
+    if (!key || !g_tuner.step_record(std::string(key), one_launch != 0))
+        return fail(FA_ERR_ARG, "fa_step_record: malformed key '%s'", key ? key : "(null)");
+    g_err[0] = 0;
+    return FA_OK;
 }
 
 int fa_set_autotune(int mode) { return g_tuner.set_mode(mode); }

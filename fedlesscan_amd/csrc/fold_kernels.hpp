@@ -222,37 +222,6 @@ __global__ __launch_bounds__(B) void k_fold_f32_gs(
         fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
 }
 
-// Grid-stride fold with tiles handed out dynamically (k_fold_f32_dyn, round
-// 3): ~one block per CU, each fetching its next tile from a device counter.
-// When other kernels share some CUs -- an all-gather overlapping the next
-// round's fold -- the blocks there run slower, and a static tile assignment
-// makes every other block of the launch wait for them at its end
-// (tools/exchange_interference.py); with dynamic tiles the slowed blocks just
-// fold fewer of them.  ctr = {next tile, blocks done}: the last block to
-// finish zeroes both for the next launch that uses the slot.
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
-__global__ __launch_bounds__(B) void k_fold_f32_dyn(
-    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
-    const float* __restrict__ a, const float* __restrict__ s,
-    const float* acc_in, float divisor, float* out, int64_t ntiles, unsigned int* ctr) {
-    __shared__ unsigned int next;
-    for (;;) {
-        if (threadIdx.x == 0) next = atomicAdd(&ctr[0], 1u);
-        __syncthreads();
-        const int64_t bid = next;
-        __syncthreads();  // every thread has the tile before thread 0 fetches the next
-        if (bid >= ntiles) break;
-        fold_tile<U, C, NT, SCORED, ACC, FIN, NTS, B>(bid, X, N, P, ldx, a, s, acc_in, divisor, out);
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
-            atomicExch(&ctr[0], 0u);
-            atomicExch(&ctr[1], 0u);
-        }
-    }
-}
-
 // One block per tile (few clients: more blocks in flight than the grid-stride
 // form, each with a short row run).
 template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS>
@@ -1363,21 +1332,10 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
     odd = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
 }
 
-// A 16-byte output store: non-temporal, or (SC1) two 8-byte agent-scope
-// stores, which leave no dirty line in the XCD's L2 (the one-launch step's
-// per-round release then writes back nothing; MI355X_MICROARCH.md, stores)
-template <bool SC1>
-__device__ __forceinline__ void st16(void* p, u32x4 v) {
-    if constexpr (SC1) {
-        unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-        __hip_atomic_store(q, ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    }
-}
+// A 16-byte non-temporal output store
+__device__ __forceinline__ void st16(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
-template <int U, int C, bool SCORED, int B = kBlock, bool SC1 = false>
+template <int U, int C, bool SCORED, int B = kBlock>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -1429,22 +1387,22 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
         const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
         const int64_t oc = o0 + (int64_t)c * B;
         f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
-        st16<SC1>(o4, __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y}));
-        st16<SC1>(o4 + 1, __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w}));
+        st16(o4, __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y}));
+        st16(o4 + 1, __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w}));
         if (outb) {
             u32x4 b;
             b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
             b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
             b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
             b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
-            st16<SC1>(reinterpret_cast<u32x4*>(outb) + oc, b);
+            st16(reinterpret_cast<u32x4*>(outb) + oc, b);
         }
     }
 }
 
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
-template <int U, int C, bool SCORED, int B = kBlock, bool SC1 = false>
+template <int U, int C, bool SCORED, int B = kBlock>
 __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
@@ -1453,13 +1411,13 @@ __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restric
     const int64_t o0 = bid * (B * C) + threadIdx.x;
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
     if (o0 + (int64_t)(C - 1) * B < no) {
-        fold_octets<U, C, SCORED, B, SC1>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+        fold_octets<U, C, SCORED, B>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int64_t o = o0 + (int64_t)c * B;
-        if (o < no) fold_octets<U, 1, SCORED, B, SC1>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+        if (o < no) fold_octets<U, 1, SCORED, B>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
     const int64_t tb = no / (B * C), tl = (no % (B * C)) % B;
     if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
@@ -1490,69 +1448,6 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_gs(
     float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles) {
     for (int64_t bid = blockIdx.x; bid < ntiles; bid += gridDim.x)
         bf16_tile<U, C, SCORED>(bid, X, N, P, ldx, a, s, divisor, out, outb);
-}
-
-// ---------------------------------------------------------------------------
-// Dynamic tiles with the next tile fetched a whole tile ahead (round 4).
-// When another kernel shares some CUs -- at N > 1 the all-gather of round k
-// runs beside the fold of round k+1 -- the fold blocks on those CUs run
-// slower, and a static tile assignment (the balanced grid-stride / band forms)
-// makes the whole launch wait for them: one rank's C4 step went from 0.96 to
-// 1.11-1.17 ms beside a copy kernel on 16-64 blocks
-// (profiles/r03_exchange_proxy/).  Here ~one block per CU takes tiles from a
-// device counter, so a slowed block folds fewer of them.  What that leaves is
-// up to one tile of tail per launch, and a tile's time is (rows / U) x the
-// load latency, independent of its width at a fixed number of bytes in flight
-// per CU: deep row pipelines (U = 16-32 rows ahead) over narrow tiles (one
-// octet or quad per lane, 64-256 lanes) keep it at ~10-40 us for 256 rows.
-// The fetch is issued by lane 0 of the block before the tile's loads and
-// its result is read only after the tile's fold (its latency hides under the
-// tile); the shared index slot alternates between two words, so a write can
-// never race the previous tile's reads.  The first tile is blockIdx.x, and the
-// counter hands out the tiles from gridDim.x on.  ctr = {next, blocks done}:
-// the last block to finish zeroes both for the next launch on the slot.  Every
-// tile runs the same in-order per-lane fold as the static forms: same bits.
-// ---------------------------------------------------------------------------
-template <class Tile>
-__device__ __forceinline__ void dyn_tiles(int64_t ntiles, unsigned int* ctr, Tile tile) {
-    __shared__ unsigned int nxt[2];
-    int64_t bid = blockIdx.x;
-    int p = 0;
-    while (bid < ntiles) {
-        unsigned int nx = 0;
-        if (threadIdx.x == 0) nx = atomicAdd(&ctr[0], 1u);
-        tile(bid);
-        if (threadIdx.x == 0) nxt[p] = nx;
-        __syncthreads();
-        bid = (int64_t)nxt[p] + gridDim.x;
-        p ^= 1;
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) {
-            atomicExch(&ctr[0], 0u);
-            atomicExch(&ctr[1], 0u);
-        }
-    }
-}
-
-template <int U, int C, bool SCORED, int B>
-__global__ __launch_bounds__(B) void k_fedavg_bf16_dyn(
-    const uint16_t* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
-    const float* __restrict__ a, const float* __restrict__ s, float divisor,
-    float* __restrict__ out, uint16_t* __restrict__ outb, int64_t ntiles, unsigned int* ctr) {
-    dyn_tiles(ntiles, ctr, [&](int64_t bid) { bf16_tile<U, C, SCORED, B>(bid, X, N, P, ldx, a, s, divisor, out, outb); });
-}
-
-// fp32 one-shot fold (no accumulator in, divide at the end) on the same schedule
-template <int U, int C, bool SCORED, int B>
-__global__ __launch_bounds__(B) void k_fold_f32_dynp(
-    const float* __restrict__ X, int64_t N, int64_t P, int64_t ldx,
-    const float* __restrict__ a, const float* __restrict__ s, float divisor,
-    float* __restrict__ out, int64_t ntiles, unsigned int* ctr) {
-    dyn_tiles(ntiles, ctr, [&](int64_t bid) {
-        fold_tile<U, C, true, SCORED, false, true, true, B>(bid, X, N, P, ldx, a, s, nullptr, divisor, out);
-    });
 }
 
 // ---------------------------------------------------------------------------
@@ -1600,38 +1495,10 @@ struct StepTable {
     int64_t static_tiles;
     int32_t segs;
     int32_t rounds;
-    // pass barriers of the static tiles (bench forms): before static pass
-    // i * sync_passes (i = 1 .. bars) a block waits until `quorum` blocks have
-    // finished the pass before it, or sync_ticks of the wall clock went by
-    int32_t sync_passes, bars, quorum;
-    int64_t sync_ticks;
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
-// [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out,
-// then kMaxBars pass-barrier counters
-constexpr int kMaxBars = 32;
-constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigBar = 3 + 2 * kMaxRounds,
-              kSigWords = kSigBar + kMaxBars;
-
-// Pass barrier i of a step launch: the block (all its waves done with the
-// pass before) counts itself, then, if `wait`, lane 0 polls until `quorum`
-// blocks have, or until the time limit (a barrier only shapes timing: a block
-// that gives up folds the same tiles).
-__device__ __forceinline__ void step_bar(const StepTable& T, unsigned int* sig, int i, bool wait) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicAdd(&sig[kSigBar + i], 1u);
-        if (wait) {
-            const long long t0 = wall_clock64();
-            while (__hip_atomic_load(&sig[kSigBar + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                   (unsigned int)T.quorum) {
-                if (wall_clock64() - t0 > T.sync_ticks) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-    }
-    if (wait) __syncthreads();
-}
+// [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
+constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
 
 template <class Tile>
 __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Tile tile) {
@@ -1641,9 +1508,7 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
     const int64_t G = gridDim.x;
     int p = 0;
     int64_t t = blockIdx.x;
-    const int S = T.sync_passes;
     if (t >= Ts) {  // no static tile for this block: its first tile from the counter
-        for (int i = 0; S && i < T.bars; ++i) step_bar(T, sig, i, false);
         if (threadIdx.x == 0) nxt[p] = atomicAdd(&sig[0], 1u);
         __syncthreads();
         t = Ts + nxt[p];
@@ -1666,15 +1531,6 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
             tn = Ts + nxt[p];
             p ^= 1;
         }
-        if (S && t < Ts) {  // pass barriers of the static tiles
-            const int64_t jt = t / G;
-            if (tn < Ts) {
-                const int64_t jn = tn / G;
-                if (jn % S == 0 && jn / S <= T.bars) step_bar(T, sig, (int)(jn / S) - 1, true);
-            } else {
-                for (int64_t i = jt / S + 1; i <= T.bars; ++i) step_bar(T, sig, (int)i - 1, false);
-            }
-        }
         int gn = g;
         while (gn < T.segs && tn >= T.seg_end[gn]) ++gn;  // T.segs: no tile left
         const int kn = gn < T.segs ? T.round[gn] : kMaxRounds;
@@ -1684,16 +1540,20 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
             // form): every storing wave waits for its stores, a barrier, then
             // one lane writes the XCD's L2 back (agent release) and, after
             // waiting for that, counts the tiles with an agent-scope add.  The
-            // add that completes the round raises its flag.
+            // add that completes the round is acq_rel (it acquires what every
+            // other block released before its own add) and raises the round's
+            // flag with a release store, so whoever acquires the flag sees the
+            // whole round -- not only on this hardware's write-back ordering.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const unsigned int nk = (unsigned int)T.round_tiles[k];
-                if (atomicAdd(&sig[kSigDone + k], cnt) + cnt == nk) {  // the round's last tiles
-                    atomicExch(&sig[kSigDone + k], 0u);
-                    atomicExch(&sig[kSigFlag + k], epoch);
+                if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) +
+                        cnt == nk) {  // the round's last tiles
+                    __hip_atomic_store(&sig[kSigDone + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             cnt = 0;
@@ -1703,8 +1563,7 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
         g = gn < T.segs ? gn : g;
     }
     if (threadIdx.x == 0) {
-        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {  // every block has counted at every barrier
-            for (int i = 0; i < T.bars; ++i) atomicExch(&sig[kSigBar + i], 0u);
+        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {  // the last block out resets the tile counters
             atomicExch(&sig[0], 0u);
             atomicExch(&sig[1], 0u);
         }
@@ -1712,7 +1571,7 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
 }
 
 // wide tiles: UB rows ahead x CB octets (quads) per lane; narrow: US x CS
-template <int UB, int CB, int US, int CS, bool SCORED, int B, bool SC1 = false>
+template <int UB, int CB, int US, int CS, bool SCORED, int B>
 __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
     const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
@@ -1721,9 +1580,9 @@ __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
         const int64_t c0 = T.col0[g];
         uint16_t* ob = outb ? outb + c0 : nullptr;
         if (T.small[g])
-            bf16_tile<US, CS, SCORED, B, SC1>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
+            bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
         else
-            bf16_tile<UB, CB, SCORED, B, SC1>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
+            bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
     });
 }
 
@@ -1744,8 +1603,14 @@ __global__ __launch_bounds__(B) void k_fold_f32_step(
 
 // Poll round flag `flag` until it reaches `epoch` (wrapping compare), then
 // return: the kernel a stream runs before an exchange that needs the round.
+// A waiter that sees no completion within max_ticks of the device wall clock
+// returns anyway (no launch can hang a stream), counts the timeout in device
+// memory and stores the launch's epoch into `status`, a word of page-locked
+// host memory mapped into the device: the host reads it without a HIP call
+// once the wait has run, and the caller raises instead of handing on an
+// exchange that read an unfinished round (ShardedAggregator, fa_rounds_check).
 __global__ __launch_bounds__(64) void k_wait_round(const unsigned int* flag, unsigned int epoch, unsigned int* timeouts,
-                                                   long long max_ticks) {
+                                                   unsigned int* status, long long max_ticks) {
     if (threadIdx.x != 0) return;
     const long long t0 = wall_clock64();
     // relaxed agent-scope (L2-served) polls: the exchange kernels that follow
@@ -1753,6 +1618,7 @@ __global__ __launch_bounds__(64) void k_wait_round(const unsigned int* flag, uns
     while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0) {
         if (wall_clock64() - t0 > max_ticks) {
             atomicAdd(timeouts, 1u);
+            if (status) __hip_atomic_store(status, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         __builtin_amdgcn_s_sleep(4);
@@ -1912,47 +1778,6 @@ int cu_count() {
     return cus;
 }
 
-// Counter slots of the dynamic-tile folds (k_fold_f32_dyn), per device:
-// kDynSlots pairs of unsigned ints, zeroed when first allocated; a launch takes
-// the next pair (fewer than kDynSlots such launches may be in flight on one
-// device at once) and leaves it zeroed.  nullptr (the caller then launches the
-// static schedule): no device memory, or a stream under graph capture (no
-// allocation there, and a captured slot would be replayed).
-constexpr unsigned kDynSlots = 4096;
-struct DynCounters {
-    std::mutex mu;
-    unsigned int* base = nullptr;
-    std::atomic<unsigned> next{0};
-};
-DynCounters g_dyn[16];
-inline unsigned int* dyn_slot(hipStream_t st) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    DynCounters& D = g_dyn[dev];
-    {
-        std::lock_guard<std::mutex> lk(D.mu);
-        if (!D.base) {
-            void* p = nullptr;
-            if (hipMalloc(&p, 2 * sizeof(unsigned int) * kDynSlots) != hipSuccess ||
-                hipMemset(p, 0, 2 * sizeof(unsigned int) * kDynSlots) != hipSuccess) {
-                (void)hipGetLastError();
-                if (p) (void)hipFree(p);
-                return nullptr;
-            }
-            D.base = static_cast<unsigned int*>(p);
-        }
-    }
-    return D.base + 2 * (D.next.fetch_add(1) % kDynSlots);
-}
-
 // The "auto" fp32 fold, from variant sweeps (interleaved, shuffled order) over
 // model sizes x client counts on MI355X (profiles/r01_sweep_shapes.log,
 // profiles/r01_sweep_balanced.log).  tiles4 = 16 KiB column tiles (4 quads per lane):
@@ -1976,10 +1801,8 @@ inline unsigned int* dyn_slot(hipStream_t st) {
 enum class F32Pick { kLdsW2T16, kLdsW2T16D4, kLdsW2T16D2, kLdsW2T32, kLdsW4T24, kLdsW4T40, kLdsW8, kColumn, kTileC1, kTileC4,
                      kTileC4Plain, kGsBalC2, kGsBalC4,
                      // forms only the tuner (below) chooses: plain one-shot folds (no accumulator in, divide)
-                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32, kDynC4, kDynC2,
-                     // dynamic tiles fetched a tile ahead (round 4): the forms for folds that share the CUs
-                     kDynpU32C1B128, kDynpU16C1B256, kDynpU32C1B64, kDynpU16C2B256, kDynpU32C1B256 };
-constexpr int kNumF32Picks = (int)F32Pick::kDynpU32C1B256 + 1;
+                     kGsBands6, kGs1C4, kTileU8C2, kEvenU4C4, kLdsQfW4T32 };
+constexpr int kNumF32Picks = (int)F32Pick::kLdsQfW4T32 + 1;
 inline bool f32_tuning_only(F32Pick p) { return (int)p >= (int)F32Pick::kGsBands6; }
 inline const char* f32_pick_name(F32Pick p) {
     switch (p) {
@@ -2001,23 +1824,13 @@ inline const char* f32_pick_name(F32Pick p) {
         case F32Pick::kTileU8C2: return "tile_8k";
         case F32Pick::kEvenU4C4: return "even_u4c4";
         case F32Pick::kLdsQfW4T32: return "lds_qf_w4_t32";
-        case F32Pick::kDynC4: return "dyn_16k";
-        case F32Pick::kDynC2: return "dyn_8k";
-        case F32Pick::kDynpU32C1B128: return "dynp_u32c1b128";
-        case F32Pick::kDynpU16C1B256: return "dynp_u16c1b256";
-        case F32Pick::kDynpU32C1B64: return "dynp_u32c1b64";
-        case F32Pick::kDynpU16C2B256: return "dynp_u16c2b256";
-        case F32Pick::kDynpU32C1B256: return "dynp_u32c1b256";
     }
     return "";
 }
 // bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
 enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
-                      kBandsU16C2, kGsBalU8C2, kGs1U8C4,
-                      // dynamic tiles fetched a tile ahead (round 4): folds that share the CUs
-                      kDynU32C1B128, kDynU16C1B256, kDynU32C1B64, kDynU16C2B128, kDynU8C2B256, kDynU32C1B256 };
-constexpr int kNumBf16Forms = (int)Bf16Form::kDynU32C1B256 + 1;
-inline bool bf16_dyn_form(Bf16Form f) { return (int)f >= (int)Bf16Form::kDynU32C1B128; }
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
 inline const char* bf16_form_name(Bf16Form f) {
     switch (f) {
         case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
@@ -2031,12 +1844,6 @@ inline const char* bf16_form_name(Bf16Form f) {
         case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
         case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
         case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
-        case Bf16Form::kDynU32C1B128: return "bf16_dyn_u32c1b128";
-        case Bf16Form::kDynU16C1B256: return "bf16_dyn_u16c1b256";
-        case Bf16Form::kDynU32C1B64: return "bf16_dyn_u32c1b64";
-        case Bf16Form::kDynU16C2B128: return "bf16_dyn_u16c2b128";
-        case Bf16Form::kDynU8C2B256: return "bf16_dyn_u8c2b256";
-        case Bf16Form::kDynU32C1B256: return "bf16_dyn_u32c1b256";
     }
     return "";
 }
@@ -2178,35 +1985,6 @@ void launch_gs_flags(hipStream_t st, int per_cu, bool sc, bool acc, bool fin, co
 #undef FA_G
 }
 
-// Dynamic tiles (k_fold_f32_dyn) on ~one block per CU; the static balanced
-// grid-stride launch when no counter slot is available.
-template <int U, int C, bool NTS, bool ALLF = false>
-void launch_dyn_flags(hipStream_t st, bool sc, bool acc, bool fin, const float* X, int64_t N, int64_t P,
-                      int64_t ldx, const float* a, const float* s, const float* acc_in, float d, float* out) {
-    const int64_t per_block = (int64_t)kBlock * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
-    const int64_t tiles = (units + per_block - 1) / per_block;
-    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
-    if (!ctr) {
-        launch_gs_flags<U, C, NTS, kBlock, ALLF>(st, -1, sc, acc, fin, X, N, P, ldx, a, s, acc_in, d, out);
-        return;
-    }
-    int64_t grid = cu_count();
-    if (grid > tiles) grid = tiles;
-#define FA_D(SC, ACC, FIN)                                                                                  \
-    hipLaunchKernelGGL((k_fold_f32_dyn<U, C, true, SC, ACC, FIN, NTS>), dim3((unsigned)grid), dim3(kBlock), 0, st, \
-                       X, N, P, ldx, a, s, acc_in, d, out, tiles, ctr)
-    if constexpr (!ALLF) {
-        if (sc) FA_D(true, false, true); else FA_D(false, false, true);
-    } else if (sc) {
-        if (acc) { if (fin) FA_D(true, true, true); else FA_D(true, true, false); }
-        else     { if (fin) FA_D(true, false, true); else FA_D(true, false, false); }
-    } else {
-        if (acc) { if (fin) FA_D(false, true, true); else FA_D(false, true, false); }
-        else     { if (fin) FA_D(false, false, true); else FA_D(false, false, false); }
-    }
-#undef FA_D
-}
-
 // Column bands: the fold as several back-to-back balanced grid-stride
 // launches over contiguous column bands of about `passes` x CUs tiles each.
 // Columns are independent, so this is the same arithmetic; the kernel
@@ -2346,136 +2124,44 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
     }
 }
 
-// Dynamic tiles fetched a tile ahead (k_fedavg_bf16_dyn / k_fold_f32_dynp):
-// per_cu blocks per CU, B threads, C octets (quads) per lane, U rows ahead.
-// Without a counter slot (graph capture, no device memory) the static
-// balanced band form runs instead: same bits.
-template <int U, int C, int B>
-void launch_bf16_dyn(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
-                     const float* a, const float* s, float d, float* out, uint16_t* outb) {
-    const int64_t per_block = (int64_t)B * C, units = (P >> 3) + ((P & 7) ? 1 : 0);
-    const int64_t tiles = (units + per_block - 1) / per_block;
-    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
-    if (!ctr) {
-        launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, d, out, outb);
-        return;
-    }
-    int64_t g = (int64_t)per_cu * cu_count();
-    if (g > tiles) g = tiles;
-    if (s)
-        hipLaunchKernelGGL((k_fedavg_bf16_dyn<U, C, true, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a, s,
-                           d, out, outb, tiles, ctr);
-    else
-        hipLaunchKernelGGL((k_fedavg_bf16_dyn<U, C, false, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a,
-                           s, d, out, outb, tiles, ctr);
-}
-
-template <int U, int C, int B>
-void launch_f32_dynp(hipStream_t st, int per_cu, bool sc, const float* X, int64_t N, int64_t P, int64_t ldx,
-                     const float* a, const float* s, float d, float* out) {
-    const int64_t per_block = (int64_t)B * C, units = (P >> 2) + ((P & 3) ? 1 : 0);
-    const int64_t tiles = (units + per_block - 1) / per_block;
-    unsigned int* ctr = tiles > 0x7FFFFFFF ? nullptr : dyn_slot(st);
-    if (!ctr) {
-        launch_gs_bands<8, 4, true>(st, 3, sc, false, true, X, N, P, ldx, a, s, nullptr, d, out);
-        return;
-    }
-    int64_t g = (int64_t)per_cu * cu_count();
-    if (g > tiles) g = tiles;
-    if (sc)
-        hipLaunchKernelGGL((k_fold_f32_dynp<U, C, true, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a, s,
-                           d, out, tiles, ctr);
-    else
-        hipLaunchKernelGGL((k_fold_f32_dynp<U, C, false, B>), dim3((unsigned)g), dim3(B), 0, st, X, N, P, ldx, a,
-                           s, d, out, tiles, ctr);
-}
-
 // ---- one launch per exchange step (k_*_step, fa_fedavg_*_rounds) ---------
 // A step form: wide tiles (UB rows ahead x CB octets / quads per lane) dealt
 // statically, and a dynamic pool of narrow tiles (US x CS) over the step's
 // last columns, sized in passes of the grid over wide tiles (pool100 = 100:
-// one pass; -1: every tile dynamic, wide).  256-thread blocks, one per CU.
+// one pass; 0: every tile static).  256-thread blocks, one per CU.
 struct StepSpec {
     const char* name;
     bool bf16;
     int ub, cb, us, cs, pool100;
-    int grid100;        // blocks per 100 CUs (100: one per CU)
-    int sync = 0;       // a pass barrier every `sync` static passes (0: none)
-    int quorum100 = 0;  // of the blocks, in percent, a barrier waits for
-    bool last_only = false;  // the pool never reaches past the last round's columns
+    bool last_only = false;   // the pool never reaches past the last round's columns
     bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
-    bool sc1 = false;         // outputs stored sc1 (bf16 forms)
 };
+// The policy's two forms and two bf16 comparison forms (the bench library
+// and the GPU tests run every one).  Round 4 measured 41 forms on the whole
+// step with the exchange proxy's copies included (DESIGN_HISTORY.md R4;
+// profiles/r04_step/): pool sizes, reduced grids, sc1 stores, pass barriers,
+// all-dynamic tiles.  What is left:
+//   bf16_step_rt_u8c4n8c2_p100_last  the bf16 policy (a C4 rank's slots): whole
+//     passes of 8 x 4-octet wide tiles per round, the rest of each round in
+//     8 x 2-octet static tiles over all blocks (the round completes near its
+//     share of the launch instead of a tile-time later), the last round's
+//     columns a one-pass dynamic pool (1.01 ms alone; 1.21-1.26 host / 1.20-2.00
+//     HBM beside the proxy's copies against 1.22-1.30 / 1.25-2.06 per round)
+//   f32_step_sd_u8c4_p75             the fp32 policy (a C3 rank): 8 x 4-quad
+//     static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
+//     6.23-6.27 beside host copies, even with per-round launches)
+//   bf16_step_sd_u8c4w_p100_last     comparison: round 4's first bf16 policy
+//     (no round tails: rounds complete a tile-time after their share)
+//   bf16_step_static_u8c4            comparison: every tile static (the one
+//     launch without its dynamic part)
 constexpr StepSpec kStepSpecs[] = {
-    {"bf16_step_sd_u8c4_p150", true, 8, 4, 16, 1, 150, 100},
-    {"bf16_step_sd_u8c4_p75", true, 8, 4, 16, 1, 75, 100},
-    {"bf16_step_sd_u8c4w_p100", true, 8, 4, 8, 4, 100, 100},
-    {"bf16_step_sd_u16c2_p150", true, 16, 2, 16, 2, 150, 100},
-    {"bf16_step_sd_u8c2w_p150", true, 8, 2, 8, 2, 150, 100},
-    {"bf16_step_u8c4", true, 8, 4, 8, 4, -1, 100},
-    {"bf16_step_u16c2", true, 16, 2, 16, 2, -1, 100},
-    {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75, 100},
-    {"f32_step_sd_u8c4_p150", false, 8, 4, 16, 1, 150, 100},
-    {"f32_step_sd_u8c4_p300", false, 8, 4, 16, 1, 300, 100},
-    {"f32_step_u8c4", false, 8, 4, 8, 4, -1, 100},
-    // fewer blocks than CUs: the band forms' balanced launches run C4's slots on
-    // ~200 blocks and were faster there than a block on every CU
-    {"bf16_step_sd_u8c4w_p100_g80", true, 8, 4, 8, 4, 100, 80},
-    {"bf16_step_sd_u8c4w_p100_g90", true, 8, 4, 8, 4, 100, 90},
-    {"bf16_step_u8c4_g80", true, 8, 4, 8, 4, -1, 80},
-    {"bf16_step_sd_u8c4_p150_g80", true, 8, 4, 16, 1, 150, 80},
-    {"f32_step_sd_u8c4_p75_g80", false, 8, 4, 16, 1, 75, 80},
-    {"f32_step_sd_u8c4_p75_g90", false, 8, 4, 16, 1, 75, 90},
-    // outputs stored sc1 (no dirty L2 lines for the per-round release to write back)
-    {"bf16_step_sd_u8c4w_p100_sc1", true, 8, 4, 8, 4, 100, 100, 0, 0, false, false, true},
-    {"bf16_step_u8c4_sc1", true, 8, 4, 8, 4, -1, 100, 0, 0, false, false, true},
-    // every tile static (no pool): the one launch's cost without the dynamic part
-    {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0, 100},
-    {"bf16_step_static_u8c2", true, 8, 2, 8, 2, 0, 100},
-    // pass barriers in the static tiles: do bands win because their launch
-    // boundaries put every block back in step?
-    {"bf16_step_static_u8c4_s3", true, 8, 4, 8, 4, 0, 100, 3, 100},
-    {"bf16_step_static_u8c4_s1", true, 8, 4, 8, 4, 0, 100, 1, 100},
-    {"bf16_step_static_u8c4_s3q90", true, 8, 4, 8, 4, 0, 100, 3, 90},
-    {"bf16_step_sd_u8c4w_p100_s3q90", true, 8, 4, 8, 4, 100, 100, 3, 90},
-    {"bf16_step_sd_u8c4w_p100_s2q75", true, 8, 4, 8, 4, 100, 100, 2, 75},
-    {"f32_step_sd_u8c4_p75_s3q90", false, 8, 4, 16, 1, 75, 100, 3, 90},
-    // the pool confined to the last round: a pool that reaches into round R-2
-    // holds that round's completion flag (and its exchange) until the launch's
-    // last tiles are done
-    {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, 100, 0, 0, true},
-    {"f32_step_sd_u8c4_p75_last", false, 8, 4, 16, 1, 75, 100, 0, 0, true},
-    {"f32_step_sd_u8c4w_p75_last", false, 8, 4, 8, 4, 75, 100, 0, 0, true},
-    // a round's wide tiles past its last whole pass become narrow static tiles
-    // spread over the blocks, so the round completes closer to its share of
-    // the launch (its exchange starts earlier) than a partial pass of wide tiles
-    {"bf16_step_rt_u8c4n16c1_p100_last", true, 8, 4, 16, 1, 100, 100, 0, 0, true, true},
-    {"f32_step_rt_u8c4n16c1_p75_last", false, 8, 4, 16, 1, 75, 100, 0, 0, true, true},
-    {"bf16_step_rt_u8c4n8c2_p100_last", true, 8, 4, 8, 2, 100, 100, 0, 0, true, true},
-    {"bf16_step_rt_u8c4n8c2_p50_last", true, 8, 4, 8, 2, 50, 100, 0, 0, true, true},
-    {"bf16_step_rt_u8c4n16c2_p100_last", true, 8, 4, 16, 2, 100, 100, 0, 0, true, true},
-    {"f32_step_rt_u8c4n8c2_p75_last", false, 8, 4, 8, 2, 75, 100, 0, 0, true, true},
-    {"f32_step_rt_u8c4n8c2_p0", false, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
-    {"bf16_step_rt_u8c4n8c2_p0", true, 8, 4, 8, 2, 0, 100, 0, 0, false, true},
-    {"bf16_step_rt_u8c4n8c2_p100_last_s3q90", true, 8, 4, 8, 2, 100, 100, 3, 90, true, true},
-    {"bf16_step_rt_u8c4n8c2_p100_last_s2q90", true, 8, 4, 8, 2, 100, 100, 2, 90, true, true},
-    {"bf16_step_rt_u8c4n8c2_p100_last_g90", true, 8, 4, 8, 2, 100, 90, 0, 0, true, true},
+    {"bf16_step_rt_u8c4n8c2_p100_last", true, 8, 4, 8, 2, 100, true, true},
+    {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75},
+    {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, true},
+    {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
-// The policy's step forms.  Measured on the whole step with the exchange
-// proxy's copies included (profiles/r04_step/round_tail/), not the fold
-// alone: a round's flag is what starts its exchange, so WHEN each round
-// completes counts as much as the fold's length.  bf16 (a C4 rank's slots):
-// whole passes of 8 x 4-octet wide tiles per round, the rest of each round in
-// 8 x 2-octet static tiles over all blocks (the round completes near its share
-// of the launch instead of a tile-time later), and the last round dynamic
-// (1.01 ms alone; 1.21-1.26 host / 1.20-2.00 HBM beside the copies against
-// 1.22-1.30 / 1.25-2.06 for per-round launches).  fp32 (a C3 rank): 8 x 4-quad
-// static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
-// 6.23-6.27 beside host copies, about even with per-round launches); the
-// round-tail forms lost there.  ShardedAggregator / bench.py pick between
-// this and per-round launches by measurement where they run ("auto").
 constexpr bool name_eq(const char* a, const char* b) { return *a == *b && (*a == 0 || name_eq(a + 1, b + 1)); }
 constexpr int step_form_index(const char* name) {
     for (int i = 0; i < kNumStepForms; ++i)
@@ -2490,16 +2176,23 @@ inline int pick_step(bool bf16) {
 }
 
 // The per-launch state of fa_fedavg_*_rounds: the signal words in device
-// memory and the host epoch (fa_rounds in fedavg_hip.h).
+// memory, the waiters' timeout record in mapped host memory and the host
+// epoch (fa_rounds in fedavg_hip.h).
 struct RoundsState {
     int device = 0;
-    unsigned int* sig = nullptr;  // kSigWords, zeroed at creation
-    unsigned int epoch = 0;       // of the last launch (0: none yet)
-    int rounds = 0;               // of the last launch
-    bool launched = false;        // the last launch was enqueued
-    long long max_ticks = 0;      // a waiter's give-up time in wall-clock ticks
-    hipEvent_t start = nullptr;   // recorded on the launch's stream just before the launch: a waiter's
-                                  // stream waits for it, so its give-up clock starts with the fold
+    unsigned int* sig = nullptr;          // kSigWords, zeroed at creation
+    unsigned int* status_host = nullptr;  // [kMaxRounds] page-locked, mapped: the epoch whose round-k wait timed out
+    unsigned int* status_dev = nullptr;   // the same words as the device addresses them
+    unsigned int epoch = 0;               // of the last launch (0: none yet)
+    unsigned int checked = 0;             // epochs up to this one were reported by rounds_check
+    int rounds = 0;                       // of the last launch
+    bool launched = false;                // the last launch was enqueued
+    long long max_ticks = 0;              // a waiter's give-up time in wall-clock ticks
+    hipEvent_t start = nullptr;           // recorded on the launch's stream just before the launch: a waiter's
+                                          // stream waits for it, so its give-up clock starts with the fold
+    hipEvent_t done = nullptr;            // recorded just after the launch: the next launch with this state
+                                          // waits for it, whatever stream it is on (a stream handle reused
+                                          // after its stream was destroyed cannot overlap two launches)
 };
 
 // The segments of one step launch over `rounds` slots at local columns
@@ -2509,12 +2202,11 @@ struct RoundsState {
 inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offsets, int64_t ldx, int64_t grid,
                             StepTable& T) {
     const int64_t ucols = sp.bf16 ? 8 : 4;  // columns per octet / quad
-    const int64_t wide_cols = (int64_t)kBlock * sp.cb * ucols, narrow_cols = (int64_t)kBlock * sp.cs * ucols;
+    const int64_t wide_cols = (int64_t)kBlock * sp.cb * ucols;
     T = StepTable{};
     T.rounds = rounds;
-    int64_t pool = sp.pool100 < 0 ? INT64_MAX : (sp.pool100 * grid * wide_cols) / 100;  // columns
-    if (sp.last_only && sp.pool100 >= 0 && pool > offsets[rounds] - offsets[rounds - 1])
-        pool = offsets[rounds] - offsets[rounds - 1];
+    int64_t pool = (sp.pool100 * grid * wide_cols) / 100;  // columns
+    if (sp.last_only && pool > offsets[rounds] - offsets[rounds - 1]) pool = offsets[rounds] - offsets[rounds - 1];
     int64_t split[kMaxRounds];  // round k: columns [0, split) wide-static, [split, width) narrow-dynamic
     for (int k = rounds - 1; k >= 0; --k) {
         const int64_t c0 = offsets[k], w = offsets[k + 1] - offsets[k];
@@ -2526,13 +2218,10 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
         split[k] = ((w - pool) / wide_cols) * wide_cols;  // the static part ends on a wide-tile boundary
         pool = 0;
     }
-    if (sp.pool100 < 0)
-        for (int k = 0; k < rounds; ++k) split[k] = 0;
     auto units = [&](int64_t w) { return sp.bf16 ? (w >> 3) + ((w & 7) ? 1 : 0) : (w >> 2) + ((w & 3) ? 1 : 0); };
     int64_t total = 0;
     // static segments first (all of them precede every dynamic one in column
     // order: only a suffix of the step is dynamic), then the dynamic ones
-    const bool wide_dyn = sp.pool100 < 0;
     auto add_seg = [&](int k, int64_t lo, int64_t hi, bool small, bool is_static) {
         const int64_t c0 = offsets[k];
         const int64_t per = small ? (int64_t)kBlock * sp.cs : (int64_t)kBlock * sp.cb;
@@ -2559,11 +2248,24 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
                 if (hi > mid) add_seg(k, mid, hi, true, true);
                 continue;
             }
-            add_seg(k, lo, hi, pass == 1 && !wide_dyn, pass == 0);
+            add_seg(k, lo, hi, pass == 1, pass == 0);
         }
-    (void)narrow_cols;
     if (total > 0x7FFFFFFF) return fail(FA_ERR_ARG, "rounds fold: too many tiles");
     return FA_OK;
+}
+
+// A waiter's give-up time: 30 s after the fold reached the head of its
+// stream, or FEDAVG_ROUND_WAIT_US microseconds (tests force the timeout path
+// with a limit far below one fold).
+inline long long round_wait_ticks(int khz) {
+    long long us = 30LL * 1000 * 1000;
+    const char* e = getenv("FEDAVG_ROUND_WAIT_US");
+    if (e && e[0]) {
+        char* end = nullptr;
+        const long long v = strtoll(e, &end, 10);
+        if (end && *end == 0 && v >= 0) us = v;
+    }
+    return (long long)khz * us / 1000;
 }
 
 // Create / destroy a launch state on `device`; enqueue a waiter for round k.
@@ -2576,17 +2278,28 @@ inline int rounds_state_init(RoundsState& o, int device) {
     o.device = device;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
-    o.max_ticks = (long long)khz * 1000LL * 30LL;  // a waiter gives up 30 s after the fold reached its stream's head
+    o.max_ticks = round_wait_ticks(khz);
     hipError_t e = hipMalloc((void**)&o.sig, kSigWords * sizeof(unsigned int));
     if (e == hipSuccess) e = hipMemset(o.sig, 0, kSigWords * sizeof(unsigned int));
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&o.status_host, kMaxRounds * sizeof(unsigned int),
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        memset(o.status_host, 0, kMaxRounds * sizeof(unsigned int));
+        e = hipHostGetDevicePointer((void**)&o.status_dev, o.status_host, 0);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&o.start, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&o.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         if (o.sig) (void)hipFree(o.sig);
+        if (o.status_host) (void)hipHostFree(o.status_host);
         if (o.start) (void)hipEventDestroy(o.start);
+        if (o.done) (void)hipEventDestroy(o.done);
         o.sig = nullptr;
-        o.start = nullptr;
+        o.status_host = o.status_dev = nullptr;
+        o.start = o.done = nullptr;
         return fail(FA_ERR_HIP, "rounds state: %s", hipGetErrorString(e));
     }
     return FA_OK;
@@ -2597,9 +2310,12 @@ inline void rounds_state_free(RoundsState& o) {
     (void)hipSetDevice(o.device);
     (void)hipDeviceSynchronize();  // no launch or waiter may still use the words
     if (o.sig) (void)hipFree(o.sig);
+    if (o.status_host) (void)hipHostFree(o.status_host);
     if (o.start) (void)hipEventDestroy(o.start);
+    if (o.done) (void)hipEventDestroy(o.done);
     o.sig = nullptr;
-    o.start = nullptr;
+    o.status_host = o.status_dev = nullptr;
+    o.start = o.done = nullptr;
     (void)hipSetDevice(prev);
 }
 inline int rounds_wait(RoundsState& o, int round, hipStream_t st) {
@@ -2607,8 +2323,20 @@ inline int rounds_wait(RoundsState& o, int round, hipStream_t st) {
     if (round < 0 || round >= o.rounds) return fail(FA_ERR_ARG, "rounds wait: round %d of %d", round, o.rounds);
     if (o.start && hipStreamWaitEvent(st, o.start, 0) != hipSuccess) return check_launch("rounds wait: event");
     hipLaunchKernelGGL(k_wait_round, dim3(1), dim3(64), 0, st, o.sig + kSigFlag + round, o.epoch,
-                       o.sig + kSigTimeout, o.max_ticks);
+                       o.sig + kSigTimeout, o.status_dev ? o.status_dev + round : nullptr, o.max_ticks);
     return check_launch("k_wait_round");
+}
+// Rounds whose wait timed out in the launches since the last check (host
+// memory only, no HIP call): valid for the waits that have already run.
+inline int rounds_check(RoundsState& o) {
+    if (!o.status_host) return 0;
+    int n = 0;
+    for (int k = 0; k < kMaxRounds; ++k) {
+        const unsigned int v = __atomic_load_n(&o.status_host[k], __ATOMIC_ACQUIRE);
+        if (v != 0 && (int)(v - o.checked) > 0 && (int)(v - o.epoch) <= 0) ++n;
+    }
+    o.checked = o.epoch;
+    return n;
 }
 
 // Enqueue one step launch of form f over `rounds` slots at local columns
@@ -2629,40 +2357,34 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
         (void)hipGetLastError();
         return fail(FA_ERR_ARG, "rounds fold cannot be captured (its epochs would replay)");
     }
-    int64_t grid = (cu_count() * sp.grid100 + 99) / 100;
+    int64_t grid = cu_count();
     StepTable T;
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
-    if (sp.sync > 0 && T.static_tiles > 0) {
-        const int64_t passes = (T.static_tiles + grid - 1) / grid;
-        int64_t sync = sp.sync;
-        while ((passes - 1) / sync > kMaxBars) ++sync;
-        T.sync_passes = (int32_t)sync;
-        T.bars = (int32_t)((passes - 1) / sync);
-        T.quorum = (int32_t)((grid * sp.quorum100 + 99) / 100);
-        T.sync_ticks = R.max_ticks / 300000 > 0 ? R.max_ticks / 300000 : 1;  // 100 us
-    }
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
+    // after the previous launch with this state, on whatever stream it ran
+    if (R.epoch != 0 && R.done && hipStreamWaitEvent(st, R.done, 0) != hipSuccess)
+        return check_launch("rounds fold: previous launch");
     if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
     const float* Xf = static_cast<const float*>(X);
     // the kernel instantiation is found from the form's tile shapes (never by
     // its index): a form whose shapes no instantiation below has is refused
     bool launched = false;
-#define FA_STB(UB, CB, US, CS, SC1)                                                                                \
-    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.sc1 == SC1) {     \
+#define FA_STB(UB, CB, US, CS)                                                                                   \
+    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS) {                      \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, SC1>), dim3((unsigned)grid),    \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid),         \
                                dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, SC1>), dim3((unsigned)grid),   \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),        \
                                dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
     }
 #define FA_STF(UB, CB, US, CS)                                                                                    \
-    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && !sp.sc1) {          \
+    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS) {                     \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
             hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid),            \
@@ -2671,21 +2393,15 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
             hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
                                dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
     }
-    FA_STB(8, 4, 16, 1, false)
-    FA_STB(8, 4, 8, 4, false)
-    FA_STB(16, 2, 16, 2, false)
-    FA_STB(8, 2, 8, 2, false)
-    FA_STB(8, 4, 8, 2, false)
-    FA_STB(8, 4, 16, 2, false)
-    FA_STB(8, 4, 8, 4, true)
+    FA_STB(8, 4, 8, 2)
+    FA_STB(8, 4, 8, 4)
     FA_STF(8, 4, 16, 1)
-    FA_STF(8, 4, 8, 4)
-    FA_STF(8, 4, 8, 2)
 #undef FA_STB
 #undef FA_STF
     if (!launched) return fail(FA_ERR_ARG, "step form %s: no kernel for its tile shapes", sp.name);
     rc = check_launch("rounds fold");
     if (rc) return rc;
+    if (R.done && hipEventRecord(R.done, st) != hipSuccess) return check_launch("rounds fold: done event");
     R.epoch = epoch;
     R.rounds = rounds;
     R.launched = true;
@@ -2938,57 +2654,15 @@ inline int launch_f32_pick(F32Pick pick, hipStream_t st, bool sc, bool acc, bool
             rc = launch_lds_flags<4, 16, 32, 2, false, false, false>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in,
                                                                       divisor, out);
             break;
-        case F32Pick::kDynC4:  // dynamic 16 KiB tiles on ~one block per CU
-            launch_dyn_flags<8, 4, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kDynC2:  // dynamic 8 KiB tiles (twice the tiles: finer balance)
-            launch_dyn_flags<8, 2, true>(st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-            break;
-        case F32Pick::kDynpU32C1B128:
-            launch_f32_dynp<32, 1, 128>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
-        case F32Pick::kDynpU16C1B256:
-            launch_f32_dynp<16, 1, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
-        case F32Pick::kDynpU32C1B64:
-            launch_f32_dynp<32, 1, 64>(st, 2, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
-        case F32Pick::kDynpU16C2B256:
-            launch_f32_dynp<16, 2, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
-        case F32Pick::kDynpU32C1B256:
-            launch_f32_dynp<32, 1, 256>(st, 1, sc, X, N, P, ldx, a, s, divisor, out);
-            break;
     }
     return rc;
-}
-
-// Forms for a fold that shares the GPU with other kernels (FA_HINT_SHARED:
-// the overlapped rounds of the multi-GPU exchange): dynamic tiles fetched a
-// tile ahead, deep row pipelines over narrow tiles (tools/exchange_interference.py,
-// DESIGN.md 8).  Only where the static policy runs a grid-stride / band launch
-// over many tiles (large models); narrower shapes keep their policy form.
-inline bool shared_applies_f32(F32Pick p) { return p == F32Pick::kGsBalC4 || p == F32Pick::kGsBalC2; }
-inline F32Pick pick_f32_shared(int64_t N, int64_t P) {
-    (void)N;
-    (void)P;
-    return F32Pick::kDynpU32C1B128;
-}
-inline bool shared_applies_bf16(Bf16Form f) {
-    return f == Bf16Form::kBandsU8C4 || f == Bf16Form::kBandsU8C2 || f == Bf16Form::kBandsU2C8;
-}
-inline Bf16Form pick_bf16_shared(int64_t N, int64_t P) {
-    (void)N;
-    (void)P;
-    return Bf16Form::kDynU32C1B128;
 }
 
 // The product fp32 fold: checks, then the scalar fallback for unaligned input
 // or the shape-picked vector fold (pick_f32).  acc_in continues a fold
 // (fa_fold_f32); with acc_in and N == 0 it only finalises.
 inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                         const float* acc_in, float divisor, int finalize, float* out, void* stream,
-                         int hints = 0) {
+                         const float* acc_in, float divisor, int finalize, float* out, void* stream) {
     if (!(acc_in && N == 0)) {
         int rc = check_common(N, P, ldx, X, a, out);
         if (rc) return rc;
@@ -3030,13 +2704,6 @@ inline int fold_f32_auto(const float* X, int64_t N, int64_t P, int64_t ldx, cons
         return check_launch("k_fold_f32_scalar");
     }
     const F32Pick policy = pick_f32(N, P);
-    if ((hints & FA_HINT_SHARED) && !acc && fin && shared_applies_f32(policy)) {
-        // one launch: each tile's block reads every row of its columns before
-        // it writes them, so an in-place fold is fine here too
-        int rc = launch_f32_pick(pick_f32_shared(N, P), st, sc, acc, fin, X, N, P, ldx, a, s, acc_in, divisor, out);
-        if (rc) return rc;
-        return check_launch("fold_f32 (shared)");
-    }
     // a plain one-shot fold (no accumulator in, with the divide) takes the
     // form the tuner measured fastest on this device.  Not when `out` overlaps
     // the rows: the measuring call runs several launches, and a later one
@@ -3131,31 +2798,13 @@ inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int6
             break;
         case Bf16Form::kGsBalU8C2: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case Bf16Form::kGs1U8C4: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
-        case Bf16Form::kDynU32C1B128:
-            launch_bf16_dyn<32, 1, 128>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
-        case Bf16Form::kDynU16C1B256:
-            launch_bf16_dyn<16, 1, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
-        case Bf16Form::kDynU32C1B64:
-            launch_bf16_dyn<32, 1, 64>(st, 2, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
-        case Bf16Form::kDynU16C2B128:
-            launch_bf16_dyn<16, 2, 128>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
-        case Bf16Form::kDynU8C2B256:
-            launch_bf16_dyn<8, 2, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
-        case Bf16Form::kDynU32C1B256:
-            launch_bf16_dyn<32, 1, 256>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-            break;
     }
 #undef FA_BF
 }
 
 // The product bf16 fold (exact upcast, fp32 fold in order, optional RNE bf16 copy).
 inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
-                     float divisor, float* out_f32, uint16_t* out_bf16, void* stream, int hints = 0) {
+                     float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
     int rc = check_common(N, P, ldx, X, a, out_f32);
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
@@ -3172,10 +2821,6 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
         return check_launch("k_fedavg_bf16_scalar");
     }
     const Bf16Form policy = pick_bf16(N, P);
-    if ((hints & FA_HINT_SHARED) && shared_applies_bf16(policy)) {  // one launch (in place is fine)
-        launch_bf16_form(pick_bf16_shared(N, P), st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);
-        return check_launch("fedavg_bf16 (shared)");
-    }
     const size_t xbytes = ((size_t)(N - 1) * ldx + P) * 2;
     if (overlaps(out_f32, (size_t)P * 4, X, xbytes) || (out_bf16 && overlaps(out_bf16, (size_t)P * 2, X, xbytes))) {
         launch_bf16_form(policy, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);  // in place: one launch

@@ -69,6 +69,20 @@ constexpr int kTuneOk = 0;  // FA_OK: launch() returns an FA status
 // The same lines move decisions between processes (fa_tune_export /
 // fa_tune_import: a multi-GPU job runs rank 0's forms on every rank).
 //
+// Step-form decisions (round 5): at N > 1 ShardedAggregator runs an exchange
+// step either as one fold launch per step or one launch per round; "auto"
+// keeps the choice a probe measured on this machine.  Those choices live in
+// the same file as "fedavg-step" lines (key: device identity, dtype, world
+// size, client bucket, P, the layout's slot widths), so a cold process -- one
+// FaaS invocation -- runs the measured step form without probing, and
+// export/import carry them with the kernel forms.
+//
+// File I/O never runs under the tuner's mutex: a decision queues its line,
+// and the call that made it merges the queue into the file after releasing
+// the mutex, taking the file lock with LOCK_NB and a bounded retry (a file
+// held elsewhere or a slow filesystem delays the write to a later call, never
+// a fold).
+//
 // FEDAVG_AUTOTUNE=0 (or fa_set_autotune(0)) keeps the policy pick;
 // FEDAVG_AUTOTUNE_LOG=1 prints every decision with each candidate's time.
 // ---------------------------------------------------------------------------
@@ -76,6 +90,7 @@ constexpr float kTuneMargin = 0.97f;
 constexpr double kTuneBatchMs = 0.3;  // timed span per candidate
 constexpr int kTuneMaxBatch = 32;
 constexpr const char* kCacheMagic = "fedavg-tune";
+constexpr const char* kStepMagic = "fedavg-step";
 constexpr int kCacheFormat = 1;
 constexpr size_t kCacheMaxLines = 4096;
 
@@ -96,6 +111,9 @@ class Tuner {
     explicit Tuner(FormName name = nullptr, FormFromName from_name = nullptr, DeviceIdent ident = nullptr,
                    int abi = 0)
         : name_(name), from_name_(from_name), ident_(ident), abi_(abi) {}
+    ~Tuner() { flush_persist(); }  // best effort, bounded (flush_persist)
+    Tuner(const Tuner&) = delete;
+    Tuner& operator=(const Tuner&) = delete;
     static int env_mode() {
         const char* e = getenv("FEDAVG_AUTOTUNE");
         return (e && e[0] == '0') ? 0 : 1;
@@ -112,6 +130,7 @@ class Tuner {
         path_ = p;
         path_set_ = true;
         loaded_.clear();
+        steps_loaded_ = false;
     }
     std::string cache_path() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -126,6 +145,7 @@ class Tuner {
     int run(int kind, int64_t N, int64_t P, int64_t ldx, bool scored, int policy, double bytes, hipStream_t st,
             Cands cands, Launch launch) {
         if (!mode_.load()) return launch(policy);
+        Flush flush_after{this};  // destroyed after every lock_guard below: merges queued lines unlocked
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) {
             (void)hipGetLastError();
@@ -209,6 +229,7 @@ class Tuner {
         return rc;
     }
     int pending() {
+        Flush flush_after{this};
         std::lock_guard<std::mutex> lk(mu_);
         int n = 0;
         for (auto& kv : map_) {
@@ -220,6 +241,7 @@ class Tuner {
     }
     // chosen form (>= 0), -1 while the shape is being measured, -2 unknown shape
     int chosen(int dev, int kind, int64_t N, int policy, int64_t P, int64_t ldx, bool scored) {
+        Flush flush_after{this};
         std::lock_guard<std::mutex> lk(mu_);
         auto it = map_.find(Key{dev, kind, n_bucket(N), policy, P, ldx, scored ? 1 : 0});
         if (it == map_.end()) return -2;
@@ -235,6 +257,7 @@ class Tuner {
             const std::string id = ident_of(std::get<0>(kv.first));
             if (!id.empty()) out += line_of(id, kv.first, kv.second.chosen);
         }
+        for (auto& kv : steps_) out += step_line(kv.first, kv.second);
         return out;
     }
     // Apply decisions given as cache-file lines (every device whose identity
@@ -249,7 +272,12 @@ class Tuner {
             if (nl == std::string::npos) nl = text.size();
             DiskKey dk;
             int form = -1;
-            if (parse_line(text.substr(pos, nl - pos), dk, form)) {
+            std::string sk;
+            int one = -1;
+            if (parse_step_line(text.substr(pos, nl - pos), sk, one)) {
+                steps_[sk] = one;
+                ++applied;
+            } else if (parse_line(text.substr(pos, nl - pos), dk, form)) {
                 preset_[dk] = form;
                 for (auto& kv : map_) {
                     if (disk_key(kv.first) != dk) continue;
@@ -265,7 +293,40 @@ class Tuner {
         return applied;
     }
 
+    // ---- step-form decisions ------------------------------------------------
+    // key: "<ident> <dtype> <world> <client bucket> <P> <w0,w1,...>" (the
+    // caller's device identity, "f32" or "bf16", the slot widths of its
+    // layout).  lookup: 1 one launch, 0 per-round launches, -1 no decision
+    // (the file is read on the first lookup; -2: a malformed key).
+    int step_lookup(const std::string& key) {
+        std::string k;
+        if (!canon_step_key(key, k)) return -2;
+        std::lock_guard<std::mutex> lk(mu_);
+        load_steps_locked();
+        auto it = steps_.find(k);
+        return it == steps_.end() ? -1 : it->second;
+    }
+    // Record a decision (this process, and queued for the file).  false: a
+    // malformed key.
+    bool step_record(const std::string& key, bool one_launch) {
+        std::string k;
+        if (!canon_step_key(key, k)) return false;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            load_steps_locked();
+            steps_[k] = one_launch ? 1 : 0;
+            queue_.push_back(step_line(k, one_launch ? 1 : 0));
+            queued_.store(true);
+        }
+        flush_persist();
+        return true;
+    }
+
   private:
+    struct Flush {
+        Tuner* t;
+        ~Flush() { t->flush_persist(); }
+    };
     // (dev, kind, client bucket, policy form, P, ldx, scored)
     typedef std::tuple<int, int, int64_t, int, int64_t, int64_t, int> Key;
     // (device identity, kind, client bucket, policy NAME, P, ldx, scored)
@@ -371,49 +432,177 @@ class Tuner {
         for (size_t i = 1; i < p.size(); ++i)
             if (p[i] == '/') (void)mkdir(p.substr(0, i).c_str(), 0755);
     }
-    // Under mu_: merge one new decision into the file (never fails the caller).
-    void persist_locked(const Entry& e) {
+    // ---- step lines --------------------------------------------------------
+    // "<ident> <dtype> <world> <bucket> <P> <widths>" -> the same fields
+    // re-printed (canonical), or false
+    static bool canon_step_key(const std::string& key, std::string& out) {
+        char id[128], dt[8], widths[400];
+        long long world = 0, nb = 0, P = 0;
+        char tail = 0;
+        if (key.size() > 500) return false;
+        if (sscanf(key.c_str(), "%127s %7s %lld %lld %lld %399s %c", id, dt, &world, &nb, &P, widths, &tail) != 6)
+            return false;
+        if ((strcmp(dt, "f32") != 0 && strcmp(dt, "bf16") != 0) || world < 1 || world > 4096 || nb < 1 ||
+            (nb & (nb - 1)) || P < 1)
+            return false;
+        // widths: 1..8 positive integers separated by commas
+        int n = 0;
+        const char* q = widths;
+        while (*q) {
+            if (*q < '0' || *q > '9') return false;
+            char* end = nullptr;
+            const long long w = strtoll(q, &end, 10);
+            if (w < 1 || ++n > 8) return false;
+            q = end;
+            if (*q == ',') {
+                ++q;
+                if (!*q) return false;
+            } else if (*q) {
+                return false;
+            }
+        }
+        if (n < 1) return false;
+        char buf[600];
+        snprintf(buf, sizeof(buf), "%s %s %lld %lld %lld %s", id, dt, world, nb, P, widths);
+        out = buf;
+        return true;
+    }
+    std::string step_line(const std::string& k, int one) const {
+        char buf[700];
+        snprintf(buf, sizeof(buf), "%s %d %d %s %s\n", kStepMagic, kCacheFormat, abi_, k.c_str(),
+                 one ? "one" : "per");
+        return buf;
+    }
+    // "fedavg-step <format> <abi> <key...> one|per" -> canonical key + choice
+    bool parse_step_line(const std::string& line, std::string& key, int& one) const {
+        char magic[32], rest[600], choice[8];
+        int fmt = 0, abi = 0, used = 0;
+        if (line.size() > 600) return false;
+        if (sscanf(line.c_str(), "%31s %d %d %n", magic, &fmt, &abi, &used) != 3 || strcmp(magic, kStepMagic) != 0 ||
+            fmt != kCacheFormat || abi != abi_)
+            return false;
+        std::string body = line.substr((size_t)used);
+        while (!body.empty() && (body.back() == ' ' || body.back() == '\r')) body.pop_back();
+        const size_t sp = body.rfind(' ');
+        if (sp == std::string::npos) return false;
+        snprintf(choice, sizeof(choice), "%s", body.substr(sp + 1).c_str());
+        if (strcmp(choice, "one") == 0) one = 1;
+        else if (strcmp(choice, "per") == 0) one = 0;
+        else return false;
+        snprintf(rest, sizeof(rest), "%s", body.substr(0, sp).c_str());
+        return canon_step_key(rest, key);
+    }
+    // Under mu_: read the file's step lines once (every identity: the key holds it).
+    void load_steps_locked() {
+        if (steps_loaded_) return;
+        steps_loaded_ = true;
+        const std::string p = path_locked();
+        if (p.empty()) return;
+        const std::string text = read_file(p);
+        size_t pos = 0;
+        while (pos < text.size()) {
+            size_t nl = text.find('\n', pos);
+            if (nl == std::string::npos) nl = text.size();
+            std::string k;
+            int one = -1;
+            if (parse_step_line(text.substr(pos, nl - pos), k, one) && !steps_.count(k)) steps_[k] = one;
+            pos = nl + 1;
+        }
+    }
+    // Under mu_: queue one new kernel-form decision for the file.
+    void queue_locked(const Entry& e) {
         const std::string p = path_locked();
         const std::string id = ident_of(std::get<0>(e.key));
         if (p.empty() || id.empty() || e.chosen < 0) return;
-        const std::string mine = line_of(id, e.key, e.chosen);
+        queue_.push_back(line_of(id, e.key, e.chosen));
+        queued_.store(true);
+    }
+    // The key a cache line replaces: kernel lines by DiskKey, step lines by
+    // their step key; "" for a line that does not parse (dropped on rewrite).
+    std::string line_key(const std::string& ln) const {
         DiskKey dk;
         int form = -1;
-        if (!parse_line(mine.substr(0, mine.size() - 1), dk, form)) return;
+        std::string sk;
+        int one = -1;
+        if (parse_step_line(ln, sk, one)) return "S " + sk;
+        if (!parse_line(ln, dk, form)) return std::string();
+        char buf[512];
+        snprintf(buf, sizeof(buf), "K %s %d %lld %s %lld %lld %d", std::get<0>(dk).c_str(), std::get<1>(dk),
+                 (long long)std::get<2>(dk), std::get<3>(dk).c_str(), (long long)std::get<4>(dk),
+                 (long long)std::get<5>(dk), std::get<6>(dk));
+        return buf;
+    }
+    // Merge the queued lines into the file, outside mu_ (never fails the
+    // caller, never blocks on the file lock for long): one thread of the
+    // process at a time; flock(LOCK_NB) retried for at most ~50 ms, after
+    // which the lines go back to the queue for a later call.
+    void flush_persist() {
+        if (!queued_.load()) return;
+        std::unique_lock<std::mutex> io(io_mu_, std::try_to_lock);
+        if (!io.owns_lock()) return;  // another thread is writing; it or a later call takes the queue
+        std::vector<std::string> lines;
+        std::string p;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            lines.swap(queue_);
+            queued_.store(false);
+            p = path_locked();
+        }
+        if (lines.empty() || p.empty()) return;
+        bool written = false;
         make_dirs(p);
         const int lk = open((p + ".lock").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
-        if (lk < 0) return;
-        if (flock(lk, LOCK_EX) == 0) {
-            // keep every other line that parses (other shapes, devices,
-            // processes); lines of another ABI or format and corrupt lines go
-            std::string out;
-            size_t kept = 0;
-            const std::string text = read_file(p);
-            size_t pos = 0;
-            while (pos < text.size()) {
-                size_t nl = text.find('\n', pos);
-                if (nl == std::string::npos) nl = text.size();
-                const std::string ln = text.substr(pos, nl - pos);
-                DiskKey k2;
-                int f2 = -1;
-                if (parse_line(ln, k2, f2) && k2 != dk && kept + 1 < kCacheMaxLines) {
-                    out += ln + "\n";
-                    ++kept;
+        if (lk >= 0) {
+            bool locked = false;
+            for (int attempt = 0; attempt < 25 && !(locked = flock(lk, LOCK_EX | LOCK_NB) == 0); ++attempt)
+                usleep(2000);
+            if (locked) {
+                // the new lines replace any line of the same key; every other line
+                // that parses stays (other shapes, devices, processes); lines of
+                // another ABI or format and corrupt lines go
+                std::map<std::string, size_t> mine;
+                for (size_t i = 0; i < lines.size(); ++i) {
+                    std::string ln = lines[i];
+                    if (!ln.empty() && ln.back() == '\n') ln.pop_back();
+                    const std::string k = line_key(ln);
+                    if (!k.empty()) mine[k] = i;  // the last decision of a key wins
                 }
-                pos = nl + 1;
+                std::string out;
+                size_t kept = 0;
+                const std::string text = read_file(p);
+                size_t pos = 0;
+                while (pos < text.size()) {
+                    size_t nl = text.find('\n', pos);
+                    if (nl == std::string::npos) nl = text.size();
+                    const std::string ln = text.substr(pos, nl - pos);
+                    const std::string k = line_key(ln);
+                    if (!k.empty() && !mine.count(k) && kept + mine.size() < kCacheMaxLines) {
+                        out += ln + "\n";
+                        ++kept;
+                    }
+                    pos = nl + 1;
+                }
+                for (auto& kv : mine) out += lines[kv.second];
+                char tmp_suffix[64];
+                snprintf(tmp_suffix, sizeof(tmp_suffix), ".tmp.%ld", (long)getpid());
+                const std::string tmp = p + tmp_suffix;
+                FILE* f = fopen(tmp.c_str(), "wb");
+                bool ok = f && fwrite(out.data(), 1, out.size(), f) == out.size();
+                if (f) ok = (fclose(f) == 0) && ok;
+                if (ok) ok = rename(tmp.c_str(), p.c_str()) == 0;
+                if (!ok) (void)unlink(tmp.c_str());
+                (void)flock(lk, LOCK_UN);
+                written = true;  // a failed write is not retried (a read-only cache directory)
             }
-            out += mine;
-            char tmp_suffix[64];
-            snprintf(tmp_suffix, sizeof(tmp_suffix), ".tmp.%ld", (long)getpid());
-            const std::string tmp = p + tmp_suffix;
-            FILE* f = fopen(tmp.c_str(), "wb");
-            bool ok = f && fwrite(out.data(), 1, out.size(), f) == out.size();
-            if (f) ok = (fclose(f) == 0) && ok;
-            if (ok) ok = rename(tmp.c_str(), p.c_str()) == 0;
-            if (!ok) (void)unlink(tmp.c_str());
-            (void)flock(lk, LOCK_UN);
+            close(lk);
+        } else {
+            written = true;  // no lock file possible: the cache is unusable, drop the lines
         }
-        close(lk);
+        if (!written) {
+            std::lock_guard<std::mutex> g(mu_);
+            queue_.insert(queue_.begin(), lines.begin(), lines.end());
+            queued_.store(true);
+        }
     }
     // Decide once the last candidate's end event has completed (the events
     // complete in stream order).  Under mu_.
@@ -454,7 +643,7 @@ class Tuner {
             fprintf(stderr, "%s ms\n", line);
         }
         release(e);
-        persist_locked(e);
+        queue_locked(e);
     }
     const char* form_name(int kind, int form) const { return name_ ? name_(kind, form) : "?"; }
     FormName name_;
@@ -466,6 +655,11 @@ class Tuner {
     std::map<DiskKey, int> preset_;         // decisions from the file / other processes
     std::map<std::string, bool> loaded_;    // device identities whose file lines are in preset_
     std::map<int, std::string> ident_cache_;
+    std::map<std::string, int> steps_;      // step-form decisions: canonical key -> 1 one launch / 0 per round
+    bool steps_loaded_ = false;
+    std::vector<std::string> queue_;        // cache lines waiting for flush_persist
+    std::atomic<bool> queued_{false};
+    std::mutex io_mu_;                      // one file merge at a time in this process
     std::string path_;
     bool path_set_ = false;
     std::atomic<int> mode_{env_mode()};

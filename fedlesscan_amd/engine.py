@@ -297,8 +297,12 @@ _rounds_lock = threading.Lock()
 
 def rounds_state(device: torch.device, stream: Optional[int] = None) -> ctypes.c_void_p:
     """The library's one-launch-per-step state (fa_rounds) for the launches
-    issued on one stream of a device (default: its current stream): launches
-    with one state must be ordered, and launches on one stream are."""
+    issued on one stream of a device (default: its current stream), kept for
+    the life of the process (torch's streams come from fixed pools, so the
+    handles a process sees are few).  Launches with one state must not
+    overlap: the library orders each launch after the previous launch of its
+    state (an event), so even a stream handle reused after its stream was
+    destroyed cannot run two launches of one state at once."""
     dev = torch.device(device)
     key = (dev, stream if stream is not None else stream_ptr(dev))
     with _rounds_lock:

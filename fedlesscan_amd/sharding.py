@@ -211,6 +211,24 @@ def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
     return dist.all_gather_into_tensor(full, piece, group=group, async_op=async_op)
 
 
+def device_ident(device) -> str:
+    """The identity a step-form decision is keyed by: gfx arch and CU count of
+    `device` ("gfx950:256"), as the tuner's cache file keys kernel forms."""
+    p = torch.cuda.get_device_properties(torch.device(device))
+    arch = getattr(p, "gcnArchName", "") or p.name
+    return f"{arch}:{p.multi_processor_count}".replace(" ", "_")
+
+
+def step_key(ident: str, bf16: bool, n_clients: int, layout: "SlotLayout") -> str:
+    """The key of a step-form decision (fa_step_lookup / fa_step_record):
+    device identity, dtype, world size, client-count bucket (the count moves
+    from round to round with stragglers; a form's advantage does not), P and
+    the layout's slot widths."""
+    bucket = 1 << max(0, int(n_clients) - 1).bit_length()
+    return (f"{ident} {'bf16' if bf16 else 'f32'} {layout.world} {bucket} {layout.P} "
+            f"{','.join(str(w) for w in layout.widths)}")
+
+
 class ShardedAggregator:
     """Fold this rank's parameter bucket, then all-gather the global model.
 
@@ -220,13 +238,41 @@ class ShardedAggregator:
     oracle instead.  `total` is the divisor sum over EVERY weight (the
     reference divides by sum(weights) even where zip() truncated the rows,
     fed_avg_aggregator.py:31-35).
+
+    one_launch -- how aggregate_slots runs an exchange step's folds:
+      True      one launch for every round (engine.fold_rounds), each round's
+                exchange started behind that round's completion flag;
+      False     one fold launch per round;
+      "auto"    the form recorded for this machine and shape (the tuner's
+                cache file, fa_step_lookup: a decision a probe made in an
+                earlier process or another rank's, imported), per-round
+                launches when none is recorded -- never a timing run, a
+                synchronisation or a collective of its own, so a one-call
+                process (one FaaS invocation, aggregation.py:71-75) runs the
+                recorded form from its first call;
+      "probe"   as "auto", but a shape with no recorded form is timed: its
+                first 2 x PROBE_CALLS calls alternate the two forms on the
+                device (max over the group's ranks), then the faster is kept
+                and recorded (fa_step_record) for later processes.
+    check -- what a one-launch step does about a round wait that timed out (a
+      waiter gives up after 30 s, and the exchange behind it then reads an
+      unfinished round):
+      "sync"      (default) every call waits for its step's waits, reads the
+                  timeout record (fa_rounds_check) and, over an all-reduce
+                  (MAX) so that every rank agrees, raises AggregationError
+                  (exceptions.py:1) instead of returning the model;
+      "deferred"  the call returns at once (pipelined steps); check_timeouts()
+                  does the same check for every step since the last one and
+                  must be called before the results are used.
+    device_ident -- the identity decisions are keyed by (default: the GPU's
+      arch and CU count, device_ident()).
     """
 
-    # calls per step form the "auto" mode times before it keeps the faster
+    # calls per step form the "probe" mode times before it keeps the faster
     PROBE_CALLS = 2
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None,
-                 one_launch="auto"):
+                 one_launch="auto", check: str = "sync", device_ident: Optional[str] = None):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -235,29 +281,56 @@ class ShardedAggregator:
         if fold is None:
             fold = engine.fold_stacked
         self.fold = fold
-        # aggregate_slots folds every round of a step in one launch
-        # (engine.fold_rounds) and starts each round's exchange behind that
-        # round's completion flag (True), or one fold launch per round (False);
-        # "auto": the first calls of a shape alternate the two, each timed on
-        # the device and maxed over the group's ranks, then the faster is kept
-        # for the shape (which wins depends on how much the exchange kernels
-        # slow the fold on this machine)
-        if one_launch not in (True, False, "auto"):
-            raise ValueError(f"one_launch must be True, False or 'auto', not {one_launch!r}")
+        if one_launch not in (True, False, "auto", "probe"):
+            raise ValueError(f"one_launch must be True, False, 'auto' or 'probe', not {one_launch!r}")
+        if check not in ("sync", "deferred"):
+            raise ValueError(f"check must be 'sync' or 'deferred', not {check!r}")
         self.one_launch = one_launch
-        self._probe: dict = {}  # shape key -> {"one": [ms], "per": [ms]} while probing, or the chosen bool
+        self.check = check
+        self.ident = device_ident
+        self._probe: dict = {}  # step key -> {"one": [ms], "per": [ms]} while probing
+        self._steps: dict = {}  # step key -> True (one launch) / False (per round): decided or restored
+        self._pending: list = []  # "deferred": (event after the waits, rounds state) per unchecked step
+
+    def step_key(self, X_local: torch.Tensor, layout: "SlotLayout") -> Optional[str]:
+        """This call's step-form key (module step_key); None without an
+        identity (a CPU tensor and no device_ident given)."""
+        ident = self.ident
+        if ident is None:
+            if not X_local.is_cuda:
+                return None
+            ident = self.ident = device_ident(X_local.device)
+        return step_key(ident, X_local.dtype == torch.bfloat16, int(X_local.shape[0]), layout)
 
     def step_form(self, X_local: torch.Tensor, layout: "SlotLayout") -> Optional[str]:
-        """The step form "auto" settled on for this shape ("one launch" /
-        "per round"), or None while it is still timing them."""
-        got = self._probe.get(self._shape_key(X_local, layout))
-        return None if got is None or isinstance(got, dict) else ("one launch" if got else "per round")
+        """The recorded step form for this shape ("one launch" / "per round"),
+        or None (nothing recorded, or a probe still timing)."""
+        key = self.step_key(X_local, layout)
+        got = self._lookup(key)
+        return None if got is None else ("one launch" if got else "per round")
 
-    def _shape_key(self, X_local, layout):
-        # clients by power-of-two bucket (the count changes from round to round
-        # with stragglers; a form's advantage does not), the layout exactly
-        n = int(X_local.shape[0])
-        return (1 << max(0, n - 1).bit_length(), X_local.dtype, tuple(layout.widths), layout.world, layout.P)
+    def record_step_form(self, X_local: torch.Tensor, layout: "SlotLayout", one_launch: bool) -> None:
+        """Record a step form for this shape: in this process and, merged into
+        the tuner's cache file, for later ones (fa_step_record)."""
+        key = self.step_key(X_local, layout)
+        if key is None:
+            raise ValueError("no device identity for a CPU tensor: pass device_ident=")
+        from . import _lib
+        _lib.call("fa_step_record", key.encode(), 1 if one_launch else 0)
+        self._steps[key] = bool(one_launch)
+
+    def _lookup(self, key: Optional[str]) -> Optional[bool]:
+        if key is None:
+            return None
+        got = self._steps.get(key)
+        if got is None:
+            from . import _lib
+            v = _lib.load().fa_step_lookup(key.encode())
+            if v == -2:
+                raise ValueError(f"malformed step key {key!r}")
+            if v >= 0:
+                got = self._steps[key] = bool(v)
+        return got
 
     def bounds(self, P: int) -> Tuple[int, int]:
         return bucket_bounds(P, self.world)[self.rank]
@@ -312,114 +385,115 @@ class ShardedAggregator:
         float32 for fp32 updates; for bf16 updates the RNE bf16 model (the fold
         still accumulates in fp32), so the exchange moves 2 bytes per parameter,
         half the xGMI bytes of the fp32 result.  `fold` must accept out= (and
-        want_bf16= for bf16 input), as engine.fold_stacked does."""
+        want_bf16= for bf16 input), as engine.fold_stacked does.  Raises
+        AggregationError (every rank) when a one-launch step's round wait timed
+        out (check="sync"; "deferred": at check_timeouts())."""
         if X_local.shape[1] != layout.local_width:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
+        multi = 1 < layout.rounds <= 8
+        # which step form: fixed, or the recorded decision (a lookup only: no
+        # timing, synchronisation or collective unless "probe" has to measure)
+        if self.one_launch in (True, False) or not multi:
+            one, probing = self.one_launch is True, None
+        else:
+            key = self.step_key(X_local, layout)
+            got = self._lookup(key)
+            one, probing = bool(got), None
+            if got is None and self.one_launch == "probe" and X_local.is_cuda and self.default_fold:
+                if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
+                    self._probe.pop(next(iter(self._probe)))
+                t = self._probe.setdefault(key, {"one": [], "per": []})
+                # the form with fewer timed calls, one launch first; the schedule
+                # depends only on what every rank shares (layout, client count),
+                # so a rank whose buffers cannot take the one launch still times
+                # its per-round calls in step with the others
+                probing = (key, "one" if len(t["one"]) <= len(t["per"]) else "per")
+                one = probing[1] == "one"
         if not X_local.is_cuda or layout.rounds == 1:
             return self._aggregate_slots(X_local, weights, scores, layout, out, total)
-        one = self._one_launch_ok(X_local, weights, scores, layout, total)
-        probing = None
-        # the probe's schedule and its collective depend only on what every rank
-        # shares (the fold, the layout, the client count), never on this rank's
-        # own buffers: a rank that cannot take the one launch still times its
-        # per-round calls in step with the others
-        if self.one_launch == "auto" and self.default_fold and 1 < layout.rounds <= 8:
-            key = self._shape_key(X_local, layout)
-            if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
-                self._probe.pop(next(iter(self._probe)))
-            got = self._probe.setdefault(key, {"one": [], "per": []})
-            if isinstance(got, dict):  # still timing: the form with fewer timed calls, one launch first
-                probing = (key, "one" if len(got["one"]) <= len(got["per"]) else "per")
-                one = one and probing[1] == "one"
-            else:
-                one = one and got
+        if torch.cuda.is_current_stream_capturing():
+            # a HIP graph capture: the per-round launches (the one launch
+            # refuses capture: its epochs would replay), nothing timed
+            return self._aggregate_slots(X_local, weights, scores, layout, out, total)
+        one = one and self._one_launch_ok(X_local, weights, scores, layout, total)
         # the rounds' folds on a high-priority stream of their own (fold_stream), ordered after
         # the caller's work and before the caller's later work
         caller = torch.cuda.current_stream(X_local.device)
         fs = fold_stream(X_local.device)
         fs.wait_stream(caller)
+        waited = None
         with torch.cuda.stream(fs):
             if probing:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(fs)
             if one:
-                full = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
+                full, waited = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
             else:
                 full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
             if probing:
                 ev[1].record(fs)
         caller.wait_stream(fs)
         full.record_stream(caller)
+        if waited is not None:
+            if self.check == "sync":
+                waited[0].synchronize()
+                self._raise_on_timeouts(self._timed_out([waited[1]]))
+            else:
+                self._pending.append(waited)
         if probing:
-            self._record_probe(probing, ev, X_local.device)
+            self._record_probe(probing, ev, X_local, layout)
         return full
 
-    def _record_probe(self, probing, ev, device) -> None:
-        """One timed call of the "auto" mode: its device time (max over the
+    def _timed_out(self, states) -> int:
+        from . import _lib
+        L = _lib.load()
+        n = 0
+        for st in {id(x): x for x in states}.values():
+            v = L.fa_rounds_check(st)
+            if v < 0:
+                _lib.check(-v, "fa_rounds_check")
+            n += v
+        return n
+
+    def _raise_on_timeouts(self, n: int) -> None:
+        """Every rank learns whether any rank's round wait timed out (MAX over
+        the group) and, if one did, raises: an exchange behind that wait read
+        an unfinished round, so no rank may use the gathered model."""
+        if self.world > 1:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+            t = torch.tensor([n], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            n = int(t.item())
+        if n:
+            from .aggregator.exceptions import AggregationError
+            raise AggregationError(
+                f"round wait timed out ({n} round(s) on the worst rank): the exchange read an unfinished round; "
+                "the aggregated model is not valid")
+
+    def check_timeouts(self) -> None:
+        """check="deferred": wait for every unchecked step's round waits, then
+        raise AggregationError on every rank if any of them timed out.  A
+        collective over the group: every rank calls it at the same point."""
+        pending, self._pending = self._pending, []
+        if pending:
+            pending[-1][0].synchronize()  # the waits complete in stream order
+        self._raise_on_timeouts(self._timed_out([p[1] for p in pending]))
+
+    def _record_probe(self, probing, ev, X_local, layout) -> None:
+        """One timed call of the "probe" mode: its device time (max over the
         group's ranks, so every rank keeps the same form); after PROBE_CALLS
-        calls of each form the faster one (best call) is kept for the shape."""
+        calls of each form the faster one (best call) is recorded for the
+        shape (record_step_form: this process and the cache file)."""
         key, form = probing
         ev[1].synchronize()
-        t = torch.tensor([ev[0].elapsed_time(ev[1])], dtype=torch.float64, device=device)
+        t = torch.tensor([ev[0].elapsed_time(ev[1])], dtype=torch.float64, device=X_local.device)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         got = self._probe[key]
         got[form].append(float(t.item()))
         if len(got["one"]) >= self.PROBE_CALLS and len(got["per"]) >= self.PROBE_CALLS:
-            self._probe[key] = min(got["one"]) <= min(got["per"])
-
-    def _one_launch_ok(self, X_local, weights, scores, layout, total) -> bool:
-        import numpy as np
-
-        from .engine import result_dtype
-        if not (self.one_launch is not False and self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
-            return False
-        if X_local.dtype not in (torch.float32, torch.bfloat16) or X_local.stride(1) != 1:
-            return False
-        if X_local.shape[0] < 1 or min(layout.widths) < 1:
-            return False
-        align = 8 if X_local.dtype == torch.bfloat16 else 4
-        if any(layout.offset(k) % align for k in range(layout.rounds)) or X_local.stride(0) % align:
-            return False
-        if X_local.data_ptr() % 16:
-            return False
-        return result_dtype(np.dtype(np.float32), list(weights), scores, total) == np.float32
-
-    def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total):
-        """Every round's fold in ONE launch on the current (fold) stream; round
-        k's exchange issued on the gather stream behind a wait for round k, so
-        it runs while the launch folds the later rounds."""
-        from . import engine
-        dev = X_local.device
-        bf16 = X_local.dtype == torch.bfloat16
-        odt = torch.bfloat16 if bf16 else torch.float32
-        full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
-        if full.dtype != odt or full.numel() < layout.padded_total:
-            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
-        local = torch.empty(layout.local_width, dtype=torch.float32, device=dev)
-        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=dev) if bf16 else None
-        offs = [layout.offset(k) for k in range(layout.rounds + 1)]
-        r = engine.fold_rounds(X_local, weights, scores, offs, out=local, out_bf16=local_b, total=total)
-        fs = torch.cuda.current_stream(dev)
-        gs = gather_stream(dev)
-        send_all = local_b if bf16 else local
-        send_all.record_stream(gs)
-        works = []
-        for k in range(layout.rounds):
-            engine.wait_round(r, k, gs)
-            lo, hi = layout.round_range(k)
-            send = send_all[layout.offset(k):layout.offset(k + 1)]
-            with torch.cuda.stream(gs):
-                if self.world == 1:
-                    full[lo:hi].copy_(send)
-                    continue
-                w = gather_into(full[lo:hi], send, self.group, async_op=True)
-            if w is not None:
-                works.append(w)
-        for w in works:
-            w.wait()  # the fold stream waits for the collectives
-        fs.wait_stream(gs)
-        return full[: layout.P]
+            del self._probe[key]
+            self.record_step_form(X_local, layout, min(got["one"]) <= min(got["per"]))
 
     def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
         bf16 = X_local.dtype == torch.bfloat16

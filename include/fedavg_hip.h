@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 3
+#define FA_ABI_VERSION 4
 
 enum fa_status {
     FA_OK = 0,
@@ -111,23 +111,6 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                    const float* a, const float* s, float divisor,
                    float* out_f32, uint16_t* out_bf16, void* stream);
 
-/* The same folds with hints (ABI 3).  FA_HINT_SHARED: other kernels run on
- * the GPU beside this fold -- at N > 1 the all-gather of exchange round k
- * overlaps the fold of round k+1 (fedlesscan_amd/sharding.py).  A static tile
- * schedule waits at its end for the blocks that share a CU with them; with
- * the hint a large fold takes its column tiles from a device counter, fetched
- * a tile ahead, with deep row pipelines over narrow tiles, so the slowed
- * blocks fold fewer tiles.  Narrow models keep their usual
- * form.  Same bits with or without hints; hints = 0 is exactly fa_fedavg_f32
- * / fa_fedavg_bf16.  Unknown hint bits are FA_ERR_ARG. */
-#define FA_HINT_SHARED 1
-int fa_fedavg_f32_ex(const float* X, int64_t N, int64_t P, int64_t ldx,
-                     const float* a, const float* s, float divisor,
-                     float* out, int hints, void* stream);
-int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
-                      const float* a, const float* s, float divisor,
-                      float* out_f32, uint16_t* out_bf16, int hints, void* stream);
-
 /* ---- one launch per exchange step (ABI 3) -----------------------------------
  * At N > 1 a rank folds its columns in `rounds` slots and all-gathers each
  * slot while the next one folds (fedlesscan_amd/sharding.py).  Folding each
@@ -151,10 +134,19 @@ int fa_fedavg_bf16_ex(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  *     1 <= rounds <= 8.  Not under graph capture (FA_ERR_ARG).
  *   fa_rounds_wait: round < the last launch's rounds; the stream first waits
  *     for the launch to reach the head of its own stream (an event recorded
- *     just before it), then a waiter that sees no completion within ~30 s
- *     returns anyway and counts a timeout; fa_rounds_timeouts (synchronous)
- *     returns that count.  One object per launching stream (engine.py keys
- *     them by device and stream). */
+ *     just before it), then a waiter that sees no completion within 30 s
+ *     (FEDAVG_ROUND_WAIT_US at fa_rounds_create: another limit, for tests)
+ *     returns anyway: whatever is queued behind it would read an unfinished
+ *     round.  The waiter records that in page-locked host memory.
+ *   fa_rounds_check (ABI 4): [host, no HIP call, no synchronisation] the
+ *     number of rounds whose wait timed out in the launches since the last
+ *     check (or creation), as far as the waits that have already run show --
+ *     call it once the waits are known complete (an event recorded behind
+ *     them); nonzero means an exchange behind a wait read an unfinished round
+ *     and its result must not be used (fedlesscan_amd/sharding.py raises
+ *     AggregationError on every rank).
+ *   fa_rounds_timeouts: (synchronous) every timed-out wait since creation.
+ *   One object per launching stream (engine.py keeps one per stream object). */
 typedef struct fa_rounds fa_rounds;
 int fa_rounds_create(fa_rounds** r, int device);
 int fa_rounds_destroy(fa_rounds* r);
@@ -166,6 +158,7 @@ int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ld
                           float* out_f32, uint16_t* out_bf16,
                           int rounds, const int64_t* offsets, void* stream);
 int fa_rounds_wait(fa_rounds* r, int round, void* stream);
+int fa_rounds_check(fa_rounds* r);
 int fa_rounds_timeouts(fa_rounds* r);
 /* [host] the kernel form fa_fedavg_bf16_rounds (bf16 != 0) / _f32_rounds runs */
 const char* fa_rounds_form(int bf16);
@@ -241,6 +234,20 @@ const char* fa_fold_form(int kind, int64_t N, int64_t P, int64_t ldx, int scored
 int fa_tune_cache_path(const char* path);
 int64_t fa_tune_export(char* buf, int64_t cap);
 int fa_tune_import(const char* text);
+/* Step-form decisions (ABI 4).  A multi-GPU exchange step runs as one
+ * fa_fedavg_*_rounds launch or as one fold launch per round; which is faster
+ * depends on how much the exchange's kernels slow the fold on the machine,
+ * so ShardedAggregator measures it once (an opt-in probe) and keeps the
+ * answer in the tuner's cache file as a "fedavg-step" line, exported and
+ * imported with the kernel forms.  key = "<device identity> <f32|bf16>
+ * <world size> <client-count bucket (a power of two)> <P> <w0,w1,...>" (the
+ * layout's 1-8 slot widths).  A cold process then runs the recorded form with
+ * no probe (aggregation.py:71-75 builds a fresh strategy per invocation).
+ *   fa_step_lookup: 1 one launch per step, 0 per-round launches, -1 no
+ *                   decision, -2 malformed key (the file is read once)
+ *   fa_step_record: record (and merge into the file) a decision */
+int fa_step_lookup(const char* key);
+int fa_step_record(const char* key, int one_launch);
 
 /* float64 updates (the reference unit-test fixture is float64,
  * test/test_aggregation.py:23-38). */

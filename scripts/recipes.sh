@@ -14,15 +14,17 @@
 #                 is `python bench.py --gpus 8` and `python bench.py --gpus 8 --config c4`)
 #   c4_rank       one 8-GPU C4 rank on one GPU under nccl at world 1: one launch per step vs per round
 #   exchange      the exchange-interference proxy (tools/exchange_interference.py), C4 and C3 ranks
+#   exchange_sdma the same proxy with copy-engine copies (hipMemcpyAsync, no CUs) beside the fold
+#   changed       the GPU tests of round 5's changes (step forms, sharding, RCCL world 1, tuner, host)
 #   e2e           end-to-end from host NPZ blobs: config-1 shapes, C2, 1024 x 1M, and C3 (1024 x 10M)
 #   tuner         the tuner's first-call cost, cold and with a warm cache file; varying client counts
 #   final         gpu_suite + bench + prof_c3 (the end-of-round evidence)
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 XI="python3 tools/exchange_interference.py"
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 COMMIT=${COMMIT:-unknown}
-S_BF="product,bf16_step_sd_u8c4w_p100_sc1,bf16_step_u8c4,bf16_step_u8c4_sc1"
+S_BF="product,bf16_step_sd_u8c4w_p100_last,bf16_step_static_u8c4"
 S_F32="product"
 C4R="--config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5 --no-cpu-baseline"
 recipe=${1:-}
@@ -49,6 +51,13 @@ case "$recipe" in
     steps=("xi_c4_host:300:$XI --config c4 --host-src --scale 0.15 --step-forms $S_BF"
            "xi_c4_hbm:300:$XI --config c4 --step-forms $S_BF"
            "xi_c3_host:400:$XI --config c3 --host-src --scale 0.15 --step-forms $S_F32") ;;
+  exchange_sdma)  # round 5: the fold beside copy-engine traffic
+    steps=("xsd_c4_full:300:$XI --config c4 --copy sdma --blocks 1 --step-forms product"
+           "xsd_c4_015:300:$XI --config c4 --copy sdma --scale 0.15 --blocks 1 --step-forms product"
+           "xsd_c3_full:400:$XI --config c3 --copy sdma --blocks 1 --step-forms product"
+           "xk_c4_host:300:$XI --config c4 --host-src --scale 0.15 --step-forms product") ;;
+  changed)
+    steps=("pytest_changed:900:$T tests/test_gpu_shared_fold.py tests/test_gpu_sharding.py tests/test_gpu_rccl.py tests/test_gpu_tuner.py tests/test_host.py") ;;
   e2e)
     steps=("e2e_small:600:python3 bench_e2e.py --clients 10 --params 582026 --reps 20 && python3 bench_e2e.py --clients 100 --params 1000000 --reps 15 && python3 bench_e2e.py --clients 1024 --params 1000000 --reps 5"
            "e2e_c3:900:python3 bench_e2e.py --clients 1024 --params 10000000 --reps 3 --no-cpu --check-cols 1000000") ;;
@@ -68,9 +77,9 @@ case "$recipe" in
     steps=("pytest_gpu:1100:$T -m gpu tests" "smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'"
            "bench_default:500:python3 bench.py" "prof_c3:900:scripts/profile_c3.sh $TAG $COMMIT") ;;
   step_alone)  # the one launch's cost while it runs alone: fully static steps, one round
-    steps=("xi_alone4:300:$XI --config c4 --blocks '' --step-forms product,bf16_step_static_u8c4,bf16_step_static_u8c2"
+    steps=("xi_alone4:300:$XI --config c4 --blocks '' --step-forms product,bf16_step_static_u8c4"
            "xi_alone4_forced:300:$XI --config c4 --blocks '' --forms bf16_bands4_u8c4,bf16_bands4_u8c2"
-           "xi_alone1:300:$XI --config c4 --rounds 1 --blocks '' --step-forms product,bf16_step_static_u8c4,bf16_step_static_u8c2") ;;
+           "xi_alone1:300:$XI --config c4 --rounds 1 --blocks '' --step-forms product,bf16_step_static_u8c4") ;;
   e2e_c2)  # C2 end to end over chunk sizes x slots, two alternating passes
     steps=("e2e_c2_variants:900:for pass in 1 2; do for c in 32:3 64:3 64:4 16:4; do FEDAVG_STREAM_CHUNK_MB=\${c%:*} FEDAVG_STREAM_SLOTS=\${c#*:} python3 bench_e2e.py --clients 100 --params 1000000 --reps 15 --no-cpu --check-cols 100000; done; done") ;;
   none) steps=() ;;

@@ -64,14 +64,19 @@ def _rccl_worker(port, q):
                     agg = ShardedAggregator(one_launch=one)
                     full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
                     out[(dt, P, tail, scored, one)] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
-                # "auto" (the default): both forms timed over the first calls, then the faster kept
-                agg = ShardedAggregator()
+                # "probe": both forms timed over the first calls, then the faster kept and recorded
+                agg = ShardedAggregator(one_launch="probe")
                 runs = set()
                 for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
                     full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
                     runs.add(full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes())
                 assert len(runs) == 1 and agg.step_form(X.view(T.bfloat16) if bf16 else X, lay) is not None
-                out[(dt, P, tail, scored, "auto")] = runs.pop()
+                out[(dt, P, tail, scored, "probe")] = runs.pop()
+                # "auto" (the default) in a fresh aggregator: the recorded form, no probe
+                agg = ShardedAggregator()
+                assert agg.step_form(X.view(T.bfloat16) if bf16 else X, lay) is not None
+                full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
+                out[(dt, P, tail, scored, "auto")] = full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes()
         m = G.manifest()["f32_small"]
         layers = ShardedAggregator().aggregate_layers(G.parameters("f32_small"), m["weights"])
         out["layers"] = [np.array(a) for a in layers]
@@ -96,7 +101,7 @@ def test_rccl_world1_slots_and_layers_bit_exact():
     for dt, P, _, tail in CASES:
         for scored in (False, True):
             s = sc if scored else None
-            for one in (True, False, "auto"):
+            for one in (True, False, "probe", "auto"):
                 key = (dt, P, tail, scored, one)
                 if dt == "bf16":
                     _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(SEED, N, 0, P), w, s)

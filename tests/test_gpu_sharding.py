@@ -68,44 +68,139 @@ def test_slots_world1_bf16_exchange(P, rounds, one_launch):
     assert np.array_equal(full.view(torch.int16).cpu().numpy().view(np.uint16), expb)
 
 
-@pytest.mark.parametrize("bf16", [False, True])
-def test_auto_step_form_settles_and_stays_exact(bf16):
-    """one_launch="auto": the first 2 x PROBE_CALLS calls of a shape alternate
-    the one launch and per-round launches (each timed), later calls keep the
-    faster; every call's result is bit-exact, and a new shape probes anew."""
-    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+def _slots_input(bf16, N, P, seed, lay, dev):
+    """X [N, lay.local_width] on the GPU holding rank 0's slots, and the
+    oracle's expected bits (fp32 as uint32, bf16 as the RNE uint16 model)."""
     from oracle import fedavg_oracle as O
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N)
+    if bf16:
+        X = torch.zeros((N, lay.local_width), dtype=torch.int16, device=dev)
+        Xb = synth.clients_bf16(seed, N, 0, P)
+        src = Xb.view(np.int16)
+        _, exp = O.fedavg_stacked_bf16(Xb, w, sc)
+    else:
+        X = torch.zeros((N, lay.local_width), dtype=torch.float32, device=dev)
+        src = synth.clients_f32(seed, N, 0, P)
+        exp = O.fedavg_stacked(src, w, sc).view(np.uint32)
+    for k, (lo, hi) in enumerate(lay.slots(0)):
+        if hi > lo:
+            X[:, lay.offset(k):lay.offset(k) + hi - lo] = torch.from_numpy(src[:, lo:hi]).to(dev)
+    return (X.view(torch.bfloat16) if bf16 else X), w, sc, exp
+
+
+def _bits(full, bf16):
+    return full.view(torch.int16).cpu().numpy().view(np.uint16) if bf16 else full.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_probe_step_form_settles_records_and_stays_exact(bf16, monkeypatch):
+    """one_launch="probe": the first 2 x PROBE_CALLS calls of a shape alternate
+    the one launch and per-round launches (each timed), later calls keep the
+    faster, and the choice is recorded: a fresh "auto" aggregator (a later
+    process's) runs it without probing.  Every call bit-exact; a new shape
+    probes anew."""
+    from fedlesscan_amd import engine
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
     dev = torch.device("cuda", 0)
-    agg = ShardedAggregator()
-    assert agg.one_launch == "auto"
+    agg = ShardedAggregator(one_launch="probe")
+    assert ShardedAggregator().one_launch == "auto"
     for P, rounds in ((300_001, 4), (65_536, 3)):
         N, seed = 33, 9
         lay = SlotLayout(P, 1, rounds)
-        w = synth.cardinalities(seed, N)
-        sc = _scores(seed, N)
-        if bf16:
-            X = torch.zeros((N, lay.local_width), dtype=torch.int16, device=dev)
-            Xb = synth.clients_bf16(seed, N, 0, P)
-            src = Xb.view(np.int16)
-            _, exp = O.fedavg_stacked_bf16(Xb, w, sc)
-        else:
-            X = torch.zeros((N, lay.local_width), dtype=torch.float32, device=dev)
-            src = synth.clients_f32(seed, N, 0, P)
-            exp = O.fedavg_stacked(src, w, sc).view(np.uint32)
-        for k, (lo, hi) in enumerate(lay.slots(0)):
-            if hi > lo:
-                X[:, k * lay.sub:k * lay.sub + hi - lo] = torch.from_numpy(src[:, lo:hi]).to(dev)
-        Xin = X.view(torch.bfloat16) if bf16 else X
+        Xin, w, sc, exp = _slots_input(bf16, N, P, seed, lay, dev)
         for call in range(2 * ShardedAggregator.PROBE_CALLS + 2):
             settled = agg.step_form(Xin, lay)
             assert (settled is None) == (call < 2 * ShardedAggregator.PROBE_CALLS), (call, settled)
-            full = agg.aggregate_slots(Xin, w, sc, lay)
-            got = full.view(torch.int16).cpu().numpy().view(np.uint16) if bf16 else \
-                full.cpu().numpy().view(np.uint32)
-            assert np.array_equal(got, exp), (P, call)
-        assert agg.step_form(Xin, lay) in ("one launch", "per round")
+            assert np.array_equal(_bits(agg.aggregate_slots(Xin, w, sc, lay), bf16), exp), (P, call)
+        form = agg.step_form(Xin, lay)
+        assert form in ("one launch", "per round")
+        # a fresh aggregator finds the record and times nothing
+        fresh = ShardedAggregator()
+        assert fresh.step_form(Xin, lay) == form
+        calls = []
+        real = engine.fold_rounds
+        monkeypatch.setattr(engine, "fold_rounds", lambda *a, **k: calls.append(1) or real(*a, **k))
+        monkeypatch.setattr(torch.cuda.Event, "elapsed_time", lambda *a: pytest.fail("a probe timed a call"))
+        assert np.array_equal(_bits(fresh.aggregate_slots(Xin, w, sc, lay), bf16), exp)
+        assert len(calls) == (1 if form == "one launch" else 0)
+        monkeypatch.undo()
     with pytest.raises(ValueError):
         ShardedAggregator(one_launch="sometimes")
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("recorded", ["one", "per", None])
+def test_step_form_restored_from_the_cache_file(bf16, recorded, monkeypatch):
+    """A "fedavg-step" line another process wrote to the tuner's cache file:
+    a fresh process (the cache re-read) with one_launch="auto" runs that form
+    from its first call -- no probe, no timing -- and is bit-exact; with no
+    line it runs per-round launches."""
+    from fedlesscan_amd import _lib, engine
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    dev = torch.device("cuda", 0)
+    N, P, seed = 70, 200_003 + (8 if bf16 else 0), 31 + (recorded == "one")
+    lay = SlotLayout(P, 1, 4)
+    Xin, w, sc, exp = _slots_input(bf16, N, P, seed, lay, dev)
+    agg = ShardedAggregator()
+    key = agg.step_key(Xin, lay)
+    path = os.environ["FEDAVG_TUNE_CACHE"]
+    if recorded:
+        with open(path, "a") as f:
+            f.write(f"fedavg-step 1 {_lib.ABI_VERSION} {key} {recorded}\n")
+    _lib.call("fa_tune_cache_path", path.encode())  # as a new process: the file is read on the next lookup
+    calls = []
+    real = engine.fold_rounds
+    monkeypatch.setattr(engine, "fold_rounds", lambda *a, **k: calls.append(1) or real(*a, **k))
+    monkeypatch.setattr(torch.cuda.Event, "elapsed_time", lambda *a: pytest.fail("a probe timed a call"))
+    assert np.array_equal(_bits(agg.aggregate_slots(Xin, w, sc, lay), bf16), exp)
+    assert len(calls) == (1 if recorded == "one" else 0)
+    assert agg.step_form(Xin, lay) == {"one": "one launch", "per": "per round", None: None}[recorded]
+
+
+def test_round_wait_timeout_raises_on_every_path(monkeypatch):
+    """A round wait that gives up (a tick limit far below one C4-slot fold,
+    FEDAVG_ROUND_WAIT_US) lets the exchange behind it read an unfinished
+    round: aggregate_slots raises AggregationError instead of returning the
+    model (check="sync"), or check_timeouts() does (check="deferred").  At the
+    default limit the same step is bit-exact against the oracle, every column."""
+    from fedlesscan_amd import engine
+    from fedlesscan_amd.aggregator.exceptions import AggregationError
+    from fedlesscan_amd.sharding import ShardedAggregator, overlap_layout
+    from oracle import oracle_lib as OL
+    dev = torch.device("cuda", 0)
+    B = __import__("fedlesscan_amd._lib", fromlist=["x"]).load_bench()
+    N, seed = 256, 52
+    lay = overlap_layout(100_000_000 // 8, 1, "bf16")  # a C4 rank's share as 4 rounds: ~1 ms of fold
+    W = lay.local_width
+    X = torch.empty((N, W), dtype=torch.bfloat16, device=dev)
+    assert B.fa_synth_bf16(X.data_ptr(), N, W, W, seed, 0, 0, torch.cuda.current_stream(dev).cuda_stream) == 0
+    w = synth.cardinalities(seed, N)
+    sc = _scores(seed, N)
+    monkeypatch.setattr(engine, "_rounds_states", {})  # fresh states read the limit
+    monkeypatch.setenv("FEDAVG_ROUND_WAIT_US", "1")
+    with pytest.raises(AggregationError, match="timed out"):
+        ShardedAggregator(one_launch=True).aggregate_slots(X, w, sc, lay)
+    deferred = ShardedAggregator(one_launch=True, check="deferred")
+    out = deferred.aggregate_slots(X, w, sc, lay)
+    assert out.dtype == torch.bfloat16
+    with pytest.raises(AggregationError, match="timed out"):
+        deferred.check_timeouts()
+    deferred.check_timeouts()  # nothing left unchecked
+    torch.cuda.synchronize()
+    monkeypatch.setattr(engine, "_rounds_states", {})
+    monkeypatch.delenv("FEDAVG_ROUND_WAIT_US")
+    agg = ShardedAggregator(one_launch=True)
+    got = _bits(agg.aggregate_slots(X, w, sc, lay), True)
+    del X, out
+    torch.cuda.empty_cache()
+    an, sn = np.array(w, np.float32), np.array(sc, np.float32)
+    P = lay.P  # world 1: global column p is local column p
+    expb = np.empty(P, np.uint16)
+    for c0 in range(0, P, 1 << 21):
+        nc = min(1 << 21, P - c0)
+        _, expb[c0:c0 + nc] = OL.fedavg_bf16(OL.synth_bf16(seed, N, nc, col0=c0), an, np.float32(sum(w)), s=sn)
+    assert np.array_equal(got, expb)
 
 
 @pytest.mark.parametrize("one_launch", [True, False])
@@ -177,7 +272,7 @@ def _rank(rank, world, port, N, P, rounds, seed, bf16, q):
                 X[:, k * lay.sub:k * lay.sub + hi - lo] = T.from_numpy(part).to(dev)
         w = synth.cardinalities(seed, N)
         sc = _scores(seed, N)
-        agg = ShardedAggregator()  # one_launch="auto": the probe's all-reduce runs over the group
+        agg = ShardedAggregator(one_launch="probe")  # the probe's all-reduce runs over the group
         outs = []
         for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
             full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc, lay)

@@ -1,14 +1,13 @@
-"""Folds that share the GPU (round 4): the dynamic-tile forms the overlapped
-exchange rounds run (FA_HINT_SHARED, fa_fedavg_*_ex; csrc/fold_kernels.hpp
-dyn_tiles), bit for bit against the C oracle of fed_avg_aggregator.py:24-42 /
-stall_aware_aggregation.py:42-67 (bf16: exact upcast + that fold).
+"""The one-launch exchange step (fa_fedavg_*_rounds, csrc/fold_kernels.hpp
+step_tiles): every step form of the library and the product entry with its
+per-round waits, bit for bit against the C oracle of fed_avg_aggregator.py:24-42
+/ stall_aware_aggregation.py:42-67 (bf16: exact upcast + that fold).
 
-Covered: every dynamic form at the slot widths an 8-GPU C4 rank folds
-(sharding.overlap_layout(100M, 8, "bf16"): 256 clients, every column checked),
-the fp32 forms at a C3 rank's slot width with a P % 4 tail, the product entry
-with the hint on wide and narrow shapes, stall-aware, in place, a graph capture
-(no counter slot there: the static form runs) and back-to-back launches that
-reuse counter slots while others are in flight.
+Covered: the slot widths an 8-GPU C4 rank folds (sharding.overlap_layout(100M,
+8, "bf16"): 256 clients, every column checked), a C3 rank's layout, eight
+small rounds with an odd client count, stall-aware, each round's result
+copied behind its wait on another stream the moment it is flagged, four
+launches back to back on one state, and the argument checks.
 """
 import numpy as np
 import pytest
@@ -35,12 +34,6 @@ def libs():
 
 def _same(a, b):
     return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
-
-
-def _dyn_forms(B, kind):
-    if kind == "bf16":
-        return [f for f in range(B.fa_num_bf16_forms()) if "_dyn_" in B.fa_bf16_form_name(f).decode()]
-    return [f for f in range(B.fa_num_f32_forms()) if B.fa_f32_form_name(f).decode().startswith("dyn")]
 
 
 def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
@@ -96,14 +89,16 @@ def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
         res[f"product rounds rep {rep}"] = (o.cpu().numpy(), ob.cpu().numpy().view(np.uint16) if bf16 else None)
         g = got.cpu().numpy()
         res[f"copied behind the waits rep {rep}"] = ((None, g.view(np.uint16)) if bf16 else (g.view(np.float32), None))
-    assert L.fa_rounds_timeouts(r) == 0
+    assert L.fa_rounds_timeouts(r) == 0 and L.fa_rounds_check(r) == 0
     _lib.check(L.fa_rounds_destroy(r), "destroy")
     return res
 
 
-def test_bf16_dynamic_forms_at_the_c4_rank_slots(dev, libs):
+def test_bf16_one_launch_steps_at_the_c4_rank_slots(dev, libs):
     """One 8-GPU C4 rank: 256 clients x its four slots side by side (12.5M
-    bf16 columns), every dynamic form on every slot, every column checked."""
+    bf16 columns), stall-aware: every bf16 step form and the product entry
+    with each round's result copied behind fa_rounds_wait on another stream,
+    every column checked."""
     _lib, L, B = libs
     N, seed = 256, 44
     lay = overlap_layout(100_000_000, 8, "bf16")
@@ -116,73 +111,18 @@ def test_bf16_dynamic_forms_at_the_c4_rank_slots(dev, libs):
     a = torch.tensor(np.array(w, np.float32), device=dev)
     s = torch.tensor(np.array(sc, np.float32), device=dev)
     div = float(np.float32(sum(w)))
-    forms = _dyn_forms(B, "bf16")
-    assert len(forms) >= 4
-    outs = {}
-    for f in forms:
-        o = torch.full((W,), float("nan"), dtype=torch.float32, device=dev)
-        ob = torch.zeros((W,), dtype=torch.int16, device=dev)
-        for k in range(lay.rounds):  # stall-aware on the odd rounds
-            off, wd = lay.offset(k), lay.width(k)
-            _lib.check(B.fa_fedavg_bf16_form(X.data_ptr() + off * 2, N, wd, W, a.data_ptr(),
-                                             s.data_ptr() if k % 2 else None, div, o.data_ptr() + off * 4,
-                                             ob.data_ptr() + off * 2, st, f), "bf16 form", bench=True)
-        outs[B.fa_bf16_form_name(f).decode()] = (o.cpu().numpy(), ob.cpu().numpy().view(np.uint16))
-    # the whole step in one launch (stall-aware on every round): every bf16
-    # step form, and the product entry with each round's result copied behind
-    # fa_rounds_wait on another stream
     one = _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16=True)
+    assert len(one) >= 10
     del X
     torch.cuda.empty_cache()
     an, sn = np.array(w, np.float32), np.array(sc, np.float32)
-    for k in range(lay.rounds):
-        off, wd = lay.offset(k), lay.width(k)
-        for c0 in range(0, wd, 1 << 20):
-            nc = min(1 << 20, wd - c0)
-            xb = OL.synth_bf16(seed, N, nc, col0=off + c0)
-            es = OL.fedavg_bf16(xb, an, np.float32(sum(w)), s=sn)
-            ep = es if k % 2 else OL.fedavg_bf16(xb, an, np.float32(sum(w)))
-            for group, (ef, eb) in ((outs, ep), (one, es)):
-                for name, (o, ob) in group.items():
-                    if o is not None:
-                        assert _same(o[off + c0:off + c0 + nc], ef), (name, k, c0)
-                    assert np.array_equal(ob[off + c0:off + c0 + nc], eb), (name, k, c0)
-
-
-@pytest.mark.parametrize("scored", [False, True])
-def test_f32_dynamic_forms_at_a_c3_rank_slot(dev, libs, scored):
-    """A C3 rank's overlapped-round slot width (3.2M at 8 GPUs) plus a P % 4
-    tail, 300 clients, every fp32 dynamic form, every column."""
-    _lib, L, B = libs
-    N, P, seed = 300, 3_200_003, 61
-    ldx = (P + 63) // 64 * 64
-    st = torch.cuda.current_stream(dev).cuda_stream
-    X = torch.empty((N, ldx), dtype=torch.float32, device=dev)
-    _lib.check(B.fa_synth_f32(X.data_ptr(), N, P, ldx, seed, 0, 0, st), "synth", bench=True)
-    w = synth.cardinalities(seed, N)
-    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
-    a = torch.tensor(np.array(w, np.float32), device=dev)
-    s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
-    div = float(np.float32(sum(w)))
-    outs = {}
-    for f in _dyn_forms(B, "f32"):
-        o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-        _lib.check(B.fa_fedavg_f32_form(X.data_ptr(), N, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(),
-                                        div, o.data_ptr(), st, f), "f32 form", bench=True)
-        outs[f] = o.cpu().numpy()
-    o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)  # the product entry with the hint
-    _lib.check(L.fa_fedavg_f32_ex(X.data_ptr(), N, P, ldx, a.data_ptr(), None if s is None else s.data_ptr(), div,
-                                  o.data_ptr(), _lib.FA_HINT_SHARED, st), "f32_ex")
-    outs[-1] = o.cpu().numpy()
-    del X
-    torch.cuda.empty_cache()
-    an = np.array(w, np.float32)
-    sn = None if sc is None else np.array(sc, np.float32)
-    for c0 in range(0, P, 1 << 20):
-        nc = min(1 << 20, P - c0)
-        exp = OL.fedavg_f32(OL.synth_f32(seed, N, nc, col0=c0), an, np.float32(sum(w)), s=sn)
-        for f, got in outs.items():
-            assert _same(got[c0:c0 + nc], exp), (f, c0)
+    for c0 in range(0, W, 1 << 20):
+        nc = min(1 << 20, W - c0)
+        ef, eb = OL.fedavg_bf16(OL.synth_bf16(seed, N, nc, col0=c0), an, np.float32(sum(w)), s=sn)
+        for name, (o, ob) in one.items():
+            if o is not None:
+                assert _same(o[c0:c0 + nc], ef), (name, c0)
+            assert np.array_equal(ob[c0:c0 + nc], eb), (name, c0)
 
 
 @pytest.mark.parametrize("scored", [False, True])
@@ -203,7 +143,7 @@ def test_f32_one_launch_steps_at_the_c3_rank_layout(dev, libs, scored):
     s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
     div = float(np.float32(sum(w)))
     one = _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16=False)
-    assert len(one) >= 8
+    assert len(one) >= 9
     del X
     torch.cuda.empty_cache()
     an, sn = np.array(w, np.float32), None if sc is None else np.array(sc, np.float32)
@@ -285,81 +225,5 @@ def test_rounds_entry_errors(dev, libs):
             rc = L.fa_fedavg_f32_rounds(r, X.data_ptr(), 4, 1024, a.data_ptr(), None, 4.0, o.data_ptr(), 2, offs,
                                         side.cuda_stream)
     assert rc == _lib.FA_ERR_ARG
-    assert L.fa_rounds_timeouts(r) == 0
+    assert L.fa_rounds_timeouts(r) == 0 and L.fa_rounds_check(r) == 0
     _lib.check(L.fa_rounds_destroy(r), "destroy")
-
-
-@pytest.mark.parametrize("kind,N,P,scored", [
-    ("f32", 64, 5_000_001, False),    # large: the hint takes a dynamic form
-    ("f32", 100, 70_001, True),       # narrow: the hint keeps the LDS form
-    ("bf16", 129, 3_000_011, True),   # the C4 slot pick's range: dynamic
-    ("bf16", 40, 100_003, False),     # small: the per-tile form stays
-])
-def test_product_entry_with_the_shared_hint(dev, libs, kind, N, P, scored):
-    _lib, L, B = libs
-    seed = 300 + N
-    st = torch.cuda.current_stream(dev).cuda_stream
-    w = synth.cardinalities(seed, N)
-    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)] if scored else None
-    a = torch.tensor(np.array(w, np.float32), device=dev)
-    s = None if sc is None else torch.tensor(np.array(sc, np.float32), device=dev)
-    sp = None if s is None else s.data_ptr()
-    div = float(np.float32(sum(w)))
-    an, sn = np.array(w, np.float32), None if sc is None else np.array(sc, np.float32)
-    if kind == "f32":
-        ldx = (P + 63) // 64 * 64
-        X = torch.empty((N, ldx), dtype=torch.float32, device=dev)
-        _lib.check(B.fa_synth_f32(X.data_ptr(), N, P, ldx, seed, 0, 0, st), "synth", bench=True)
-        exp = OL.fedavg_f32(OL.synth_f32(seed, N, P), an, np.float32(sum(w)), s=sn)
-        for hints in (0, _lib.FA_HINT_SHARED):
-            for _ in range(3):  # back to back: counter slots reused while earlier launches run
-                o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-                _lib.check(L.fa_fedavg_f32_ex(X.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(), hints, st),
-                           "f32_ex")
-                assert _same(o.cpu().numpy(), exp), hints
-        with pytest.raises(ValueError):
-            _lib.check(L.fa_fedavg_f32_ex(X.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(), 6, st), "bad")
-    else:
-        ldx = (P + 63) // 64 * 64
-        X = torch.empty((N, ldx), dtype=torch.bfloat16, device=dev)
-        _lib.check(B.fa_synth_bf16(X.data_ptr(), N, P, ldx, seed, 0, 0, st), "synth", bench=True)
-        ef, eb = OL.fedavg_bf16(OL.synth_bf16(seed, N, P), an, np.float32(sum(w)), s=sn)
-        for hints in (0, _lib.FA_HINT_SHARED):
-            for _ in range(3):
-                o = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-                ob = torch.zeros((P,), dtype=torch.int16, device=dev)
-                _lib.check(L.fa_fedavg_bf16_ex(X.data_ptr(), N, P, ldx, a.data_ptr(), sp, div, o.data_ptr(),
-                                               ob.data_ptr(), hints, st), "bf16_ex")
-                assert _same(o.cpu().numpy(), ef), hints
-                assert np.array_equal(ob.cpu().numpy().view(np.uint16), eb), hints
-
-
-def test_shared_fold_in_place_and_in_a_graph(dev, libs):
-    """In place (out over row 0: one launch reads a column's rows before it
-    writes the column) and captured in a HIP graph (no counter slot under
-    capture: the static form; replays bit-exactly)."""
-    _lib, L, B = libs
-    N, P, seed = 96, 4_000_000, 77
-    st = torch.cuda.current_stream(dev)
-    w = synth.cardinalities(seed, N)
-    a = torch.tensor(np.array(w, np.float32), device=dev)
-    div = float(np.float32(sum(w)))
-    X = torch.empty((N, P), dtype=torch.float32, device=dev)
-    _lib.check(B.fa_synth_f32(X.data_ptr(), N, P, P, seed, 0, 0, st.cuda_stream), "synth", bench=True)
-    exp = OL.fedavg_f32(OL.synth_f32(seed, N, P), np.array(w, np.float32), np.float32(sum(w)))
-    _lib.check(L.fa_fedavg_f32_ex(X.data_ptr(), N, P, P, a.data_ptr(), None, div, X.data_ptr(), 1, st.cuda_stream),
-               "in place")
-    assert _same(X[0].cpu().numpy(), exp)
-    _lib.check(B.fa_synth_f32(X.data_ptr(), N, P, P, seed, 0, 0, st.cuda_stream), "synth", bench=True)
-    out = torch.full((P,), float("nan"), dtype=torch.float32, device=dev)
-    g = torch.cuda.CUDAGraph()
-    side = torch.cuda.Stream(device=dev)
-    side.wait_stream(st)
-    with torch.cuda.stream(side):
-        with torch.cuda.graph(g, stream=side):
-            rc = L.fa_fedavg_f32_ex(X.data_ptr(), N, P, P, a.data_ptr(), None, div, out.data_ptr(), 1,
-                                    side.cuda_stream)
-    _lib.check(rc, "captured")
-    g.replay()
-    torch.cuda.synchronize()
-    assert _same(out.cpu().numpy(), exp)

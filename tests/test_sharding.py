@@ -217,6 +217,100 @@ def test_overlapped_slot_gather_gloo_matches_oracle(world, P, rounds, tail, quan
         assert np.array_equal(out.view(np.uint32), exp.view(np.uint32)), r
 
 
+def _step_form_worker(rank, world, port, cache, phase, N, P, rounds, seed, q):
+    """phase "record": rank 0 records a step form (what "probe" does once it
+    has measured); "restore": a fresh group of processes -- a later FaaS
+    invocation -- runs its first aggregate_slots with one_launch="auto" and
+    must find that form with no probe, no synchronisation and no collective
+    besides the exchange's own all-gathers."""
+    os.environ["FEDAVG_TUNE_CACHE"] = cache  # before the library is loaded in this process
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        agg = ShardedAggregator(fold=_oracle_fold, device_ident="cputest:0")
+        assert agg.one_launch == "auto"
+        lay = SlotLayout(P, world, rounds, shares=tail_shares(rounds, 0.25))
+        X = torch.zeros((N, lay.local_width))
+        for k, (lo, hi) in enumerate(lay.slots(rank)):
+            if hi > lo:
+                X[:, lay.offset(k):lay.offset(k) + hi - lo] = torch.from_numpy(synth.clients_f32(seed, N, lo, hi - lo))
+        w = synth.cardinalities(seed, N)
+        if phase == "record":
+            if rank == 0:
+                agg.record_step_form(X, lay, one_launch=True)
+            dist.barrier()
+            q.put((rank, None))
+            return
+        used = []
+
+        def forbid(name):
+            def f(*a, **k):
+                used.append(name)
+                raise AssertionError(f"{name} called on the first aggregate_slots")
+            return f
+        real = {n: getattr(dist, n) for n in ("all_reduce", "broadcast", "barrier", "broadcast_object_list")}
+        for n in real:
+            setattr(dist, n, forbid(n))
+        real_sync, real_event, real_probe = torch.cuda.synchronize, torch.cuda.Event, ShardedAggregator._record_probe
+        torch.cuda.synchronize = forbid("torch.cuda.synchronize")
+        torch.cuda.Event = forbid("torch.cuda.Event")
+        ShardedAggregator._record_probe = forbid("probe")
+        try:
+            full = agg.aggregate_slots(X, w, None, lay)
+            form = agg.step_form(X, lay)
+        finally:
+            for n, f in real.items():
+                setattr(dist, n, f)
+            torch.cuda.synchronize, torch.cuda.Event, ShardedAggregator._record_probe = real_sync, real_event, real_probe
+        q.put((rank, (form, used, full.numpy().tobytes())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_step_form_restored_in_a_new_process_without_probing(tmp_path):
+    """The step-form choice outlives the process: a
+    world-2 gloo group records it in the tuner's cache file; a second world-2
+    group reads it on its first call with no probe call, no synchronize and
+    no all_reduce, and still reassembles the oracle's model."""
+    from oracle import fedavg_oracle as O
+    N, P, rounds, seed, world = 11, 30011, 4, 29, 2
+    cache = str(tmp_path / "tuner.txt")
+    ctx = mp.get_context("spawn")
+    for phase in ("record", "restore"):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_step_form_worker, args=(r, world, port, cache, phase, N, P, rounds, seed, q))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        got = dict(q.get(timeout=120) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        if phase == "record":
+            text = open(cache).read()
+            assert text.count("fedavg-step ") == 1 and text.rstrip().endswith(" one"), text
+    exp = O.fedavg_stacked(synth.clients_f32(seed, N, 0, P), synth.cardinalities(seed, N))
+    for r in range(world):
+        form, used, out = got[r]
+        assert form == "one launch" and used == [], (r, form, used)
+        assert np.array_equal(np.frombuffer(out, dtype=np.uint32), exp.view(np.uint32)), r
+
+
+def test_step_keys_and_modes():
+    """The decision key names what the choice depends on; bad modes raise."""
+    agg = ShardedAggregator(fold=_oracle_fold, device_ident="gfx950:256")
+    lay = SlotLayout(100_000_000, 8, 4, shares=tail_shares(4, 0.343, 3))
+    X = torch.zeros((200, lay.local_width), dtype=torch.bfloat16)
+    key = agg.step_key(X, lay)
+    assert key == f"gfx950:256 bf16 8 256 100000000 {','.join(map(str, lay.widths))}"
+    assert ShardedAggregator(fold=_oracle_fold).step_key(X, lay) is None  # CPU tensor, no identity: no lookup
+    with pytest.raises(ValueError):
+        ShardedAggregator(one_launch="sometimes")
+    with pytest.raises(ValueError):
+        ShardedAggregator(check="later")
+
+
 def _bf16_slot_worker(rank, world, port, N, P, rounds, seed, q, tail=1.0):
     """BASELINE config 4's layout in miniature: bf16 client rows in round-robin
     slots, fp32 fold per slot, RNE-bf16 slot outputs all-gathered (2 B/param)."""

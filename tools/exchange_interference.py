@@ -9,7 +9,13 @@ only WRITES those bytes into local HBM and runs its own kernels on a few CUs;
 this copy reads and writes them, so it over-states the HBM side and roughly
 matches the CU side.  Prints the fold time per step with and without it.
 
-    python tools/exchange_interference.py [--config c3|c4] [--world 8] [--blocks 16,32,64]
+--copy sdma (round 5) moves each round's received bytes with hipMemcpyAsync
+from page-locked host memory instead (fa_copy_h2d on the copy stream): the
+copy engines (SDMA), no kernel and no CU -- the cost a kernel-free exchange
+(each rank pulling its peers' slots with copy-engine peer copies) would put
+on the fold.  --blocks then only says "with copies" (any nonzero entry).
+
+    python tools/exchange_interference.py [--config c3|c4] [--world 8] [--blocks 16,32,64] [--copy kernel|sdma]
 """
 import argparse
 import os
@@ -51,9 +57,12 @@ def main():
     ap.add_argument("--quantum", default="0",
                     help="round slot widths in whole quanta of columns (SlotLayout quantum): a number, or 'pass' "
                          "(sharding.pass_quantum: one pass of the one-launch step's wide tiles), or 'half'")
-    ap.add_argument("--hint", action="store_true",
-                    help="the product's shared-CU hint (fa_fedavg_*_ex, FA_HINT_SHARED) on the overlapped rounds")
+    ap.add_argument("--copy", default="kernel", choices=["kernel", "sdma"],
+                    help="kernel: fa_bench_copy_f32 on --blocks blocks; sdma: hipMemcpyAsync from page-locked "
+                         "host memory on the copy stream (copy engines, no CUs)")
     args = ap.parse_args()
+    if args.copy == "sdma":
+        args.host_src = True
     dev = torch.device("cuda", 0)
     L, B = _lib.load(), _lib.load_bench()
     if args.config == "c3":
@@ -107,7 +116,15 @@ def main():
     else:
         names = {B.fa_bf16_form_name(i).decode(): i for i in range(B.fa_num_bf16_forms())}
     form = [None]
-    hint_on = [False]  # the shared-CU hint on rounds 1.. (--hint: timed after the tuned forms)
+
+    def copy(k, blocks):
+        """Round k's received bytes ((world - 1) x its slot, x --scale) onto the copy stream."""
+        n = int(lay.width(k) * (args.world - 1) * out_esz * args.scale) // 16 * 4
+        if args.copy == "sdma":
+            _lib.check(L.fa_copy_h2d(dst.data_ptr(), src.data_ptr(), n * 4, xs.cuda_stream), "sdma copy")
+        else:
+            _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
+                       bench=True)
 
     def fold(k):
         off, width = lay.offset(k), lay.width(k)
@@ -123,15 +140,6 @@ def main():
                                        outb.data_ptr() + off * 2, fs.cuda_stream, form[0])
             _lib.check(rc, "form", bench=True)
             return
-        if hint_on[0] and k > 0:
-            if dt == "f32":
-                rc = L.fa_fedavg_f32_ex(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, 1,
-                                        fs.cuda_stream)
-            else:
-                rc = L.fa_fedavg_bf16_ex(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
-                                         outb.data_ptr() + off * 2, 1, fs.cuda_stream)
-            _lib.check(rc, "fold (shared hint)")
-            return
         if dt == "f32":
             rc = L.fa_fedavg_f32(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, fs.cuda_stream)
         else:
@@ -146,9 +154,7 @@ def main():
             ev[k][1].record(fs)
             if blocks:
                 xs.wait_event(ev[k][1])
-                n = int(lay.width(k) * (args.world - 1) * out_esz * args.scale) // 16 * 4
-                _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
-                           bench=True)
+                copy(k, blocks)
         fs.wait_stream(xs)
         if end is not None:
             end.record(fs)
@@ -184,9 +190,7 @@ def main():
                     _lib.check(L.fa_rounds_wait(rs_prod, k, xs.cuda_stream), "rounds wait")
                 else:
                     _lib.check(B.fa_bench_rounds_wait(rs_bench, k, xs.cuda_stream), "rounds wait", bench=True)
-                n = int(lay.width(k) * (args.world - 1) * out_esz * args.scale) // 16 * 4
-                _lib.check(B.fa_bench_copy_f32(dst.data_ptr(), src.data_ptr(), n, blocks, xs.cuda_stream), "copy",
-                           bench=True)
+                copy(k, blocks)
         fs.wait_stream(xs)
         if end is not None:
             end.record(fs)
@@ -196,7 +200,8 @@ def main():
                  for _ in range(lay.rounds)])
     torch.cuda.synchronize()
     print(f"{args.config} rank of {args.world}: widths {lay.widths}, fold CUs {cus - args.fold_free}"
-          f"{' (copy on the others)' if args.copy_on_free else ''}, copy source "
+          f"{' (copy on the others)' if args.copy_on_free else ''}, copy "
+          f"{'hipMemcpyAsync (SDMA)' if args.copy == 'sdma' else 'kernel'} from "
           f"{'host (PCIe)' if args.host_src else 'HBM'}, {args.scale:g} of the received bytes")
     for sform in [f for f in args.step_forms.split(",") if f]:
         for _ in range(3):
@@ -219,17 +224,13 @@ def main():
     tmo = L.fa_rounds_timeouts(rs_prod)
     if tmo:
         print(f"  WARNING: {tmo} round waits timed out", flush=True)
-    variants = [(f, False) for f in args.forms.split(",") if f] or [(None, False)]
-    if args.hint:
-        variants.append((None, True))
-    for fname, hint in variants:
+    for fname in [f for f in args.forms.split(",") if f] or [None]:
         form[0] = None if fname is None else names[fname]
-        hint_on[0] = hint
         for _ in range(2):  # warm the forced form
             step(0, [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in range(lay.rounds)])
         torch.cuda.synchronize()
-        label = (fname or ("hint" if hint else "tuned")) + (" r1+" if fname and args.forced_rounds != "all" else "")
+        label = (fname or "tuned") + (" r1+" if fname and args.forced_rounds != "all" else "")
         for blocks in [0] + [int(b) for b in args.blocks.split(",") if b]:
             folds, spans, steps = [], [], []
             for _ in range(args.steps):

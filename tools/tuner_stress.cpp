@@ -8,6 +8,9 @@
 // measuring, and many threads tuning many shapes at once agree (run under
 // TSan and ASan + UBSan by tools/tuner_stress.sh; no events leak).
 #include <cassert>
+#include <chrono>
+#include <fcntl.h>
+#include <sys/file.h>
 #include <cstring>
 #include <string>
 #include <unistd.h>
@@ -335,6 +338,72 @@ int main() {
         CHECK(launches == 60);
         unlink(p2.c_str());
         unlink((p2 + ".lock").c_str());
+    }
+    // 13. step-form decisions: recorded by one tuner, found by the next without
+    //     measuring; kept beside kernel lines through merges; malformed keys
+    //     and another ABI refused; carried by export / import
+    {
+        const std::string p3 = std::string(dir) + "/steps.txt";
+        const std::string key = "sim:0 bf16 8 256 100000000 3456,2432,1664,1152";
+        {
+            Tuner a(name, from_name, ident, 8);
+            a.set_cache_path(p3);
+            CHECK(a.step_lookup(key) == -1);
+            CHECK(a.step_record(key, true));
+            CHECK(a.step_lookup(key) == 1);
+            CHECK(a.step_lookup("sim:0  bf16 8 256 100000000  3456,2432,1664,1152") == 1);  // canonical spacing
+            CHECK(!a.step_record("sim:0 f16 8 256 100 64", true));       // dtype
+            CHECK(!a.step_record("sim:0 f32 8 255 100 64", true));       // bucket not a power of two
+            CHECK(!a.step_record("sim:0 f32 8 256 100 64,", true));      // trailing comma
+            CHECK(!a.step_record("sim:0 f32 8 256 100 0,64", true));     // empty slot
+            CHECK(!a.step_record("sim:0 f32 8 256 100 1,2,3,4,5,6,7,8,9", true));  // > 8 rounds
+            CHECK(a.step_lookup("sim:0 f32 8 256 100") == -2);
+            SimStream s;
+            call(a, &s, 64, 7100, {1.0, 0.3}, nullptr);  // a kernel line in the same file
+            drain(a);
+            CHECK(a.step_record("sim:0 f32 8 1024 10000000 327680,327680,327680,40960", false));
+        }
+        const std::string text = slurp(p3);
+        CHECK(count_lines(text) == 3 && text.find(" one\n") != std::string::npos && text.find(" per\n") != std::string::npos);
+        {
+            Tuner b(name, from_name, ident, 8);
+            b.set_cache_path(p3);
+            CHECK(b.step_lookup(key) == 1);
+            CHECK(b.step_lookup("sim:0 f32 8 1024 10000000 327680,327680,327680,40960") == 0);
+            CHECK(b.step_record(key, false));  // a new decision replaces the line
+            const std::string ex = b.export_text();
+            Tuner c(name, from_name, ident, 8);
+            c.set_cache_path("");
+            CHECK(c.import_text(ex) == 2 && c.step_lookup(key) == 0);
+        }
+        CHECK(count_lines(slurp(p3)) == 3 && slurp(p3).find(" one\n") == std::string::npos);
+        {
+            Tuner d(name, from_name, ident, 9);  // another ABI: the lines do not count
+            d.set_cache_path(p3);
+            CHECK(d.step_lookup(key) == -1);
+        }
+        // the file lock held elsewhere: a decision returns at once (bounded
+        // retry), stays in memory, and reaches the file on a later call
+        {
+            const int held = open((p3 + ".lock").c_str(), O_RDWR | O_CREAT, 0644);
+            CHECK(held >= 0 && flock(held, LOCK_EX) == 0);
+            Tuner e(name, from_name, ident, 8);
+            e.set_cache_path(p3);
+            const auto t0 = std::chrono::steady_clock::now();
+            CHECK(e.step_record("sim:0 f32 2 64 4096 1024,1024", true));
+            const double ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            CHECK(ms < 500.0);
+            CHECK(e.step_lookup("sim:0 f32 2 64 4096 1024,1024") == 1);
+            CHECK(slurp(p3).find("4096 1024,1024") == std::string::npos);
+            flock(held, LOCK_UN);
+            close(held);
+            CHECK(e.step_record("sim:0 f32 2 64 8192 2048,2048", false));  // flushes both
+            CHECK(slurp(p3).find("4096 1024,1024 one") != std::string::npos);
+            CHECK(slurp(p3).find("8192 2048,2048 per") != std::string::npos);
+        }
+        unlink(p3.c_str());
+        unlink((p3 + ".lock").c_str());
     }
     unlink(path.c_str());
     unlink((path + ".lock").c_str());
