@@ -114,6 +114,10 @@ def parse():
                          "record it in the tuner's cache file (fa_step_record); 'auto' (default) = the form "
                          "recorded for this machine and shape (rank 0's record), or 'probe' when none is")
     ap.add_argument("--per-round-launches", action="store_true", help="same as --step-mode per-round")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "peer_copy"],
+                    help="the one-launch step's exchange: 'rccl' = an all_gather_into_tensor per round behind its "
+                         "wait; 'peer_copy' = copy-engine pulls of the peers' slots through IPC-opened buffers "
+                         "(sharding.PeerExchange, fa_peers); the gathered model is checked against an RCCL step's")
     ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
                          "rounds: shares 1, 1, 0.5, 0.25)")
@@ -429,7 +433,7 @@ def main():
     # ShardedAggregator reads the same record), or, with none, both forms timed
     # below and the faster recorded; "probe": time them whatever is recorded
     from fedlesscan_amd.sharding import device_ident, step_key as make_step_key
-    skey = make_step_key(device_ident(dev), wl.dtype == "bf16", wl.N, lay) if can_one else None
+    skey = make_step_key(device_ident(dev), wl.dtype == "bf16", wl.N, lay, args.exchange) if can_one else None
     recorded = L.fa_step_lookup(skey.encode()) if (can_one and step_mode == "auto") else -1
     if can_one and world > 1:  # every rank runs rank 0's record (ranks may share no cache file)
         t = torch.tensor([recorded], dtype=torch.int64, device=dev)
@@ -505,9 +509,25 @@ def main():
         gs = gather_stream(dev)
         offs = [lay.offset(k) for k in range(rounds + 1)]
 
-    def step_one_launch(ev=None):
+    px = None
+    if can_one and args.exchange == "peer_copy":
+        from fedlesscan_amd.sharding import PeerExchange
+        px = PeerExchange(None, dev, lay, wl.dtype == "bf16")
+
+    def step_one_launch(ev=None, exchange=None):
         """The whole step in one fold launch; round k's all-gather on the gather
-        stream behind a wait for round k's completion flag (mid-launch)."""
+        stream behind a wait for round k's completion flag (mid-launch), or the
+        peer copy (--exchange peer_copy)."""
+        if (exchange or args.exchange) == "peer_copy":
+            if ev is not None:
+                ev[0][0][0].record(stream)
+            px.step(wl.X, wl.weights, wl.scores, full, None, stream, gs)
+            if ev is not None:
+                ev[0][0][1].record(stream)
+            stream.wait_stream(gs)
+            if ev is not None:
+                ev[1].record(stream)
+            return
         if ev is not None:
             ev[0][0][0].record(stream)
         r = engine.fold_rounds(wl.X, wl.weights, wl.scores, offs, out=wl.out, out_bf16=wl.out_bf16)
@@ -624,7 +644,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gather_ok = None
-    if dist_on:  # my slots inside the reassembled model must be my fold output, bit for bit
+    if px is not None:
+        # the whole model the peer copy reassembled must equal an RCCL step's, bit for bit
+        peer_full = full.clone()
+        full.zero_()
+        step_one_launch(exchange="rccl")
+        torch.cuda.synchronize()
+        t = torch.tensor([1 if torch.equal(peer_full.view(torch.uint8), full.view(torch.uint8)) else 0],
+                         dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        gather_ok = bool(t.item())
+        del peer_full
+    elif dist_on:  # my slots inside the reassembled model must be my fold output, bit for bit
         ok = True
         iv = torch.int32 if wl.dtype == "f32" else torch.int16
         for k, (lo, hi) in enumerate(wl.slots):
@@ -662,8 +693,10 @@ def main():
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
     if can_one:  # a round wait that gave up (never expected) let an exchange read an unfinished round
-        t = torch.tensor([max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))],
-                         dtype=torch.int64, device=dev)
+        n_to = max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))
+        if px is not None:
+            n_to += max(0, L.fa_rounds_timeouts(px.state)) + max(0, L.fa_rounds_check(px.state))
+        t = torch.tensor([n_to], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
         timeouts = int(t.item())
 
@@ -750,6 +783,7 @@ def main():
                 "fold_form_ranks_agreed": forms_agree,
                 "fold_form_rank0_broadcast": bool(dist_on and world > 1 and args.variant == 0 and per_round_possible),
                 "step_mode": step_mode if dist_on and rounds > 1 else None,
+                "exchange": (args.exchange if one_launch else "rccl") if dist_on else None,
                 "step_mode_probe": mode_probe,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
                 (B.fa_variant_name if wl.dtype == "f32" else B.fa_bf16_variant_name)(args.variant).decode(),
@@ -803,6 +837,8 @@ def main():
             # line above is reported, the run fails (ShardedAggregator raises the same)
             from fedlesscan_amd.aggregator.exceptions import AggregationError
             raise AggregationError(f"{timeouts} round wait(s) timed out during the run")
+    if px is not None:
+        px.close()
     if dist_on:
         dist.destroy_process_group()
 

@@ -60,6 +60,15 @@ _PROTOS = {
     "fa_rounds_check": (_int, [_vp]),
     "fa_rounds_timeouts": (_int, [_vp]),
     "fa_rounds_form": (ctypes.c_char_p, [_int]),
+    "fa_peers_create": (_int, [_vp, _int, _int, _int, _i64]),
+    "fa_peers_destroy": (_int, [_vp]),
+    "fa_peers_handle_bytes": (_int, []),
+    "fa_peers_handle": (_int, [_vp, _vp]),
+    "fa_peers_open": (_int, [_vp, _vp]),
+    "fa_peers_send": (_vp, [_vp]),
+    "fa_peers_rounds": (_vp, [_vp]),
+    "fa_peers_fence": (_int, [_vp, _vp]),
+    "fa_peers_exchange": (_int, [_vp, _int, _vp, _vp, _vp, _vp]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i64": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),

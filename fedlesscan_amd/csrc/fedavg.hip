@@ -8,6 +8,7 @@
 // calibration kernel live in libfedavg_hip_bench.so (fedavg_bench.hip), which
 // bench.py and the variant tests load; nothing here depends on them.
 #include "fold_kernels.hpp"
+#include "peer_exchange.hpp"
 
 #include <mutex>
 
@@ -213,8 +214,7 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const f
     return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
 }
 
-// ---- one launch per exchange step -------------------------------------------
-struct fa_rounds : RoundsState {};
+// ---- one launch per exchange step (struct fa_rounds: peer_exchange.hpp) ------
 
 int fa_rounds_create(fa_rounds** r, int device) {
     if (!r) return fail(FA_ERR_ARG, "fa_rounds_create: null handle");
@@ -277,6 +277,67 @@ int fa_rounds_timeouts(fa_rounds* r) {
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return -fail(FA_ERR_HIP, "fa_rounds_timeouts: %s", hipGetErrorString(e));
     return (int)v;
+}
+
+// ---- kernel-free peer exchange ----------------------------------------------
+int fa_peers_create(fa_peers** x, int device, int world, int rank, int64_t send_bytes) {
+    if (!x) return fail(FA_ERR_ARG, "fa_peers_create: null handle");
+    *x = nullptr;
+    fa_peers* o = new fa_peers();
+    const int rc = peers_init(*o, device, world, rank, send_bytes);
+    if (rc) {
+        peers_free(*o);
+        delete o;
+        return rc;
+    }
+    *x = o;
+    g_err[0] = 0;
+    return FA_OK;
+}
+
+int fa_peers_destroy(fa_peers* x) {
+    if (!x) return FA_OK;
+    peers_free(*x);
+    delete x;
+    return FA_OK;
+}
+
+int fa_peers_handle_bytes(void) { return kPeerHandleBytes; }
+
+int fa_peers_handle(fa_peers* x, void* out) {
+    if (!x || !out) return fail(FA_ERR_ARG, "fa_peers_handle: null argument");
+    StreamDevice on_device(nullptr);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(x->device);
+    const int rc = peers_handle(*x, out);
+    (void)hipSetDevice(prev);
+    if (!rc) g_err[0] = 0;
+    return rc;
+}
+
+int fa_peers_open(fa_peers* x, const void* all_handles) {
+    if (!x || !all_handles) return fail(FA_ERR_ARG, "fa_peers_open: null argument");
+    const int rc = peers_open(*x, static_cast<const uint8_t*>(all_handles));
+    if (!rc) g_err[0] = 0;
+    return rc;
+}
+
+void* fa_peers_send(fa_peers* x) { return x ? x->send : nullptr; }
+
+fa_rounds* fa_peers_rounds(fa_peers* x) { return x ? &x->R : nullptr; }
+
+int fa_peers_fence(fa_peers* x, void* stream) {
+    if (!x) return fail(FA_ERR_ARG, "null fa_peers");
+    StreamDevice on_stream_device(stream);
+    return peers_fence(*x, (hipStream_t)stream);
+}
+
+int fa_peers_exchange(fa_peers* x, int rounds, const int64_t* src_offsets, void* dst, const int64_t* dst_offsets,
+                      void* stream) {
+    if (!x) return fail(FA_ERR_ARG, "null fa_peers");
+    StreamDevice on_stream_device(stream);
+    return peers_exchange(*x, rounds, src_offsets, dst, dst_offsets, (hipStream_t)stream);
 }
 
 int fa_step_lookup(const char* key) {

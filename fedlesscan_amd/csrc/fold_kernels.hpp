@@ -1335,11 +1335,36 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
 // A 16-byte non-temporal output store
 __device__ __forceinline__ void st16(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
+// One row group of U rows x C octets: loaded (ld) and folded in row order (add)
+template <int U, int C>
+__device__ __forceinline__ void octets_ld(u32x4 (&v)[U][C], const u32x4* __restrict__ p, int64_t i, int64_t ldo) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * kBlock);
+}
+template <int U, int C, bool SCORED>
+__device__ __forceinline__ void octets_add(f32x4 (&ev)[C], f32x4 (&od)[C], const u32x4 (&v)[U][C],
+                                           const float* __restrict__ a, const float* __restrict__ s, int64_t i) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(v[u][c], e, o);
+            ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
+            od[c] = add4(od[c], term4<SCORED>(o, ai, si));
+        }
+    }
+}
+
 template <int U, int C, bool SCORED, int B = kBlock>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
                                             int64_t o0) {
+    static_assert(B == kBlock, "octet tiles are kBlock lanes wide");
     f32x4 ev[C], od[C];
     {
         const float a0 = a[0], s0 = SCORED ? s[0] : 1.0f;
@@ -1354,23 +1379,10 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
     int64_t i = 1;
     for (; i + U <= N; i += U) {
         u32x4 v[U][C];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int c = 0; c < C; ++c) v[u][c] = __builtin_nontemporal_load(p + (i + u) * ldo + c * B);
+        octets_ld<U, C>(v, p, i, ldo);
         // deep unrolls: every load of the group issued before the first add
         if constexpr (U >= 16) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float ai = a[i + u], si = SCORED ? s[i + u] : 1.0f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                f32x4 e, o;
-                unpack_bf16x8(v[u][c], e, o);
-                ev[c] = add4(ev[c], term4<SCORED>(e, ai, si));
-                od[c] = add4(od[c], term4<SCORED>(o, ai, si));
-            }
-        }
+        octets_add<U, C, SCORED>(ev, od, v, a, s, i);
     }
     for (; i < N; ++i) {
         const float ai = a[i], si = SCORED ? s[i] : 1.0f;
@@ -1495,10 +1507,13 @@ struct StepTable {
     int64_t static_tiles;
     int32_t segs;
     int32_t rounds;
+    int32_t sys;    // publish the rounds at system scope: other GPUs read them (fa_peers, the peer exchange)
+    int32_t noacq;  // (A/B only) the completing block skips its acquire fence
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
 // [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
 constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
+constexpr int kStatusWords = kMaxRounds + 1;  // a timeout record per round + the peer exchange's buffer fence
 
 template <class Tile>
 __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Tile tile) {
@@ -1538,22 +1553,34 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
             // The block leaves round k (its tiles come in round order): publish
             // its tiles of the round once (MI355X_MICROARCH.md, valid producer
             // form): every storing wave waits for its stores, a barrier, then
-            // one lane writes the XCD's L2 back (agent release) and, after
-            // waiting for that, counts the tiles with an agent-scope add.  The
-            // add that completes the round is acq_rel (it acquires what every
-            // other block released before its own add) and raises the round's
-            // flag with a release store, so whoever acquires the flag sees the
-            // whole round -- not only on this hardware's write-back ordering.
+            // one lane writes the XCD's L2 back (agent release fence) and counts
+            // the tiles with an agent-scope add (every block's adds form one
+            // release sequence).  The block whose add completes the round takes
+            // an acquire fence -- it synchronises with every other block's
+            // release -- and raises the round's flag with a release store, so
+            // whoever acquires the flag sees the whole round by the memory
+            // model, not only by this hardware's write-back order.  One acquire
+            // per round: an acq_rel add in every block (an L2 invalidate each,
+            // 256 x rounds per step) cost the C4 rank's step ~7 %.
+            // (T.sys: the same at system scope, for peers that read the round
+            // over xGMI -- fa_peers.)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (T.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const unsigned int nk = (unsigned int)T.round_tiles[k];
-                if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) +
+                if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
                         cnt == nk) {  // the round's last tiles
                     __hip_atomic_store(&sig[kSigDone + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (T.sys) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                        __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    } else {
+                        if (!T.noacq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
             }
             cnt = 0;
@@ -1829,8 +1856,10 @@ inline const char* f32_pick_name(F32Pick p) {
 }
 // bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
 enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
-                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
-constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4,
+                      // round 5: two blocks per CU (twice the bytes in flight per CU)
+                      kBands2xU8C4, kBands2xU8C2, kBands2xU4C4 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kBands2xU4C4 + 1;
 inline const char* bf16_form_name(Bf16Form f) {
     switch (f) {
         case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
@@ -1844,6 +1873,9 @@ inline const char* bf16_form_name(Bf16Form f) {
         case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
         case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
         case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
+        case Bf16Form::kBands2xU8C4: return "bf16_bands4x2_u8c4";
+        case Bf16Form::kBands2xU8C2: return "bf16_bands4x2_u8c2";
+        case Bf16Form::kBands2xU4C4: return "bf16_bands4x2_u4c4";
     }
     return "";
 }
@@ -2107,20 +2139,21 @@ void launch_bf16_gs(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, in
                            a, s, d, out, outb, tiles);
 }
 
+// per_cu: blocks per CU of each band's balanced launch (a pass is per_cu x CUs tiles)
 template <int U, int C>
 void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
-                       const float* a, const float* s, float d, float* out, uint16_t* outb) {
+                       const float* a, const float* s, float d, float* out, uint16_t* outb, int per_cu = 1) {
     const int64_t to = (int64_t)kBlock * C;  // octets per tile
     const int64_t units = (P >> 3) + ((P & 7) ? 1 : 0);
     const int64_t tiles = (units + to - 1) / to;
-    const int64_t per_band = (int64_t)passes * cu_count();
+    const int64_t per_band = (int64_t)passes * per_cu * cu_count();
     const int64_t nb = (tiles + per_band - 1) / per_band;
     const int64_t band_tiles = (tiles + nb - 1) / nb;
     for (int64_t b = 0; b < nb; ++b) {
         const int64_t c0 = b * band_tiles * to * 8;
         if (c0 >= P) break;
         const int64_t pb = (P - c0) < band_tiles * to * 8 ? (P - c0) : band_tiles * to * 8;
-        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
+        launch_bf16_gs<U, C>(st, -per_cu, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
     }
 }
 
@@ -2135,6 +2168,7 @@ struct StepSpec {
     int ub, cb, us, cs, pool100;
     bool last_only = false;   // the pool never reaches past the last round's columns
     bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
+    bool noacq = false;       // (A/B only) no acquire fence in the block that completes a round
 };
 // The policy's two forms and two bf16 comparison forms (the bench library
 // and the GPU tests run every one).  Round 4 measured 41 forms on the whole
@@ -2159,6 +2193,8 @@ constexpr StepSpec kStepSpecs[] = {
     {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75},
     {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, true},
     {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0},
+    // round 5 A/B: the policy without the completing block's acquire fence
+    {"bf16_step_rt_u8c4n8c2_p100_last_noacq", true, 8, 4, 8, 2, 100, true, true, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2181,13 +2217,15 @@ inline int pick_step(bool bf16) {
 struct RoundsState {
     int device = 0;
     unsigned int* sig = nullptr;          // kSigWords, zeroed at creation
-    unsigned int* status_host = nullptr;  // [kMaxRounds] page-locked, mapped: the epoch whose round-k wait timed out
+    unsigned int* status_host = nullptr;  // [kStatusWords] page-locked, mapped: the epoch whose round-k wait timed
+                                          // out ([kMaxRounds]: a peer exchange's buffer fence, fa_peers)
     unsigned int* status_dev = nullptr;   // the same words as the device addresses them
     unsigned int epoch = 0;               // of the last launch (0: none yet)
     unsigned int checked = 0;             // epochs up to this one were reported by rounds_check
     int rounds = 0;                       // of the last launch
     bool launched = false;                // the last launch was enqueued
     long long max_ticks = 0;              // a waiter's give-up time in wall-clock ticks
+    bool sys = false;                     // publish rounds at system scope (a peer exchange's state)
     hipEvent_t start = nullptr;           // recorded on the launch's stream just before the launch: a waiter's
                                           // stream waits for it, so its give-up clock starts with the fold
     hipEvent_t done = nullptr;            // recorded just after the launch: the next launch with this state
@@ -2282,10 +2320,10 @@ inline int rounds_state_init(RoundsState& o, int device) {
     hipError_t e = hipMalloc((void**)&o.sig, kSigWords * sizeof(unsigned int));
     if (e == hipSuccess) e = hipMemset(o.sig, 0, kSigWords * sizeof(unsigned int));
     if (e == hipSuccess)
-        e = hipHostMalloc((void**)&o.status_host, kMaxRounds * sizeof(unsigned int),
+        e = hipHostMalloc((void**)&o.status_host, kStatusWords * sizeof(unsigned int),
                           hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) {
-        memset(o.status_host, 0, kMaxRounds * sizeof(unsigned int));
+        memset(o.status_host, 0, kStatusWords * sizeof(unsigned int));
         e = hipHostGetDevicePointer((void**)&o.status_dev, o.status_host, 0);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&o.start, hipEventDisableTiming);
@@ -2331,7 +2369,7 @@ inline int rounds_wait(RoundsState& o, int round, hipStream_t st) {
 inline int rounds_check(RoundsState& o) {
     if (!o.status_host) return 0;
     int n = 0;
-    for (int k = 0; k < kMaxRounds; ++k) {
+    for (int k = 0; k < kStatusWords; ++k) {
         const unsigned int v = __atomic_load_n(&o.status_host[k], __ATOMIC_ACQUIRE);
         if (v != 0 && (int)(v - o.checked) > 0 && (int)(v - o.epoch) <= 0) ++n;
     }
@@ -2361,6 +2399,8 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     StepTable T;
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
+    T.sys = R.sys ? 1 : 0;
+    T.noacq = sp.noacq ? 1 : 0;
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
@@ -2798,6 +2838,15 @@ inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int6
             break;
         case Bf16Form::kGsBalU8C2: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case Bf16Form::kGs1U8C4: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
+        case Bf16Form::kBands2xU8C4:
+            launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
+            break;
+        case Bf16Form::kBands2xU8C2:
+            launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
+            break;
+        case Bf16Form::kBands2xU4C4:
+            launch_bf16_bands<4, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
+            break;
     }
 #undef FA_BF
 }

@@ -295,7 +295,8 @@ class Tuner {
 
     // ---- step-form decisions ------------------------------------------------
     // key: "<ident> <dtype> <world> <client bucket> <P> <w0,w1,...>" (the
-    // caller's device identity, "f32" or "bf16", the slot widths of its
+    // caller's device identity, "f32" or "bf16" -- "f32.peer" / "bf16.peer"
+    // for steps whose exchange is the peer copy -- the slot widths of its
     // layout).  lookup: 1 one launch, 0 per-round launches, -1 no decision
     // (the file is read on the first lookup; -2: a malformed key).
     int step_lookup(const std::string& key) {
@@ -436,13 +437,14 @@ class Tuner {
     // "<ident> <dtype> <world> <bucket> <P> <widths>" -> the same fields
     // re-printed (canonical), or false
     static bool canon_step_key(const std::string& key, std::string& out) {
-        char id[128], dt[8], widths[400];
+        char id[128], dt[16], widths[400];
         long long world = 0, nb = 0, P = 0;
         char tail = 0;
         if (key.size() > 500) return false;
-        if (sscanf(key.c_str(), "%127s %7s %lld %lld %lld %399s %c", id, dt, &world, &nb, &P, widths, &tail) != 6)
+        if (sscanf(key.c_str(), "%127s %15s %lld %lld %lld %399s %c", id, dt, &world, &nb, &P, widths, &tail) != 6)
             return false;
-        if ((strcmp(dt, "f32") != 0 && strcmp(dt, "bf16") != 0) || world < 1 || world > 4096 || nb < 1 ||
+        if ((strcmp(dt, "f32") != 0 && strcmp(dt, "bf16") != 0 && strcmp(dt, "f32.peer") != 0 &&
+             strcmp(dt, "bf16.peer") != 0) || world < 1 || world > 4096 || nb < 1 ||
             (nb & (nb - 1)) || P < 1)
             return false;
         // widths: 1..8 positive integers separated by commas

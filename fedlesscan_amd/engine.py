@@ -315,14 +315,16 @@ def rounds_state(device: torch.device, stream: Optional[int] = None) -> ctypes.c
 
 
 def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], offsets: Sequence[int], *,
-                out: torch.Tensor, out_bf16: Optional[torch.Tensor] = None, total=None) -> ctypes.c_void_p:
+                out, out_bf16=None, total=None, state: Optional[ctypes.c_void_p] = None) -> ctypes.c_void_p:
     """Every exchange round of a step in ONE launch (fa_fedavg_*_rounds): round
     k folds the columns [offsets[k], offsets[k+1]) of X (fp32 or bf16 rows)
     into the same columns of out (and of out_bf16, the RNE copy, for bf16 X),
-    on the current stream.  Returns that stream's rounds state for
-    `wait_round`: the exchange of round k may start, on another stream, as soon
-    as round k is complete, while the launch goes on.  Same bits as
-    fold_stacked on each round's columns."""
+    on the current stream.  Returns the rounds state for `wait_round` (the
+    current stream's, or `state`: a peer exchange's, fa_peers_rounds): the
+    exchange of round k may start, on another stream, as soon as round k is
+    complete, while the launch goes on.  Same bits as fold_stacked on each
+    round's columns.  out / out_bf16: tensors or raw device addresses (a peer
+    exchange's send buffer)."""
     N, W, ldx = _check_matrix(X)
     if len(weights) != N or (scores is not None and len(scores) != N):
         raise InvalidParameterShapeError(f"{N} rows but {len(weights)} weights")
@@ -334,13 +336,14 @@ def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], 
     rounds = len(offsets) - 1
     offs = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     st = stream_ptr(dev)
-    r = rounds_state(dev, st)
+    r = state if state is not None else rounds_state(dev, st)
+    addr = (lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr()))
     if X.dtype == torch.bfloat16:
         _lib.call("fa_fedavg_bf16_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
-                  out.data_ptr(), _ptr(out_bf16), rounds, offs, st)
+                  addr(out), addr(out_bf16), rounds, offs, st)
     elif X.dtype == torch.float32:
         _lib.call("fa_fedavg_f32_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
-                  out.data_ptr(), rounds, offs, st)
+                  addr(out), rounds, offs, st)
     else:
         raise InvalidParameterShapeError(f"the rounds fold takes float32 or bfloat16 rows, got {X.dtype}")
     return r

@@ -37,7 +37,8 @@ HOSTFAST_SRC = os.path.join(CSRC, "hostfast.c")
 HOSTFAST = os.path.join(OUT_DIR, "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))  # = _lib.HOSTFAST_PATH
 # library -> (sources compiled into it, files it depends on)
 TARGETS = {
-    LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, TUNER, HDR, *HOST_SRCS, os.path.join(CSRC, "host_copy.hpp")]),
+    LIB: ([SRC, *HOST_SRCS], [SRC, KERNELS, TUNER, HDR, *HOST_SRCS, os.path.join(CSRC, "host_copy.hpp"),
+                              os.path.join(CSRC, "peer_exchange.hpp")]),
     BENCH_LIB: ([BENCH_SRC], [BENCH_SRC, KERNELS, TUNER, HDR, BENCH_HDR]),
     HOSTFAST: ([HOSTFAST_SRC], [HOSTFAST_SRC]),
 }

@@ -219,14 +219,85 @@ def device_ident(device) -> str:
     return f"{arch}:{p.multi_processor_count}".replace(" ", "_")
 
 
-def step_key(ident: str, bf16: bool, n_clients: int, layout: "SlotLayout") -> str:
+def step_key(ident: str, bf16: bool, n_clients: int, layout: "SlotLayout", exchange: str = "rccl") -> str:
     """The key of a step-form decision (fa_step_lookup / fa_step_record):
-    device identity, dtype, world size, client-count bucket (the count moves
-    from round to round with stragglers; a form's advantage does not), P and
-    the layout's slot widths."""
+    device identity, dtype (".peer" appended for the peer-copy exchange),
+    world size, client-count bucket (the count moves from round to round with
+    stragglers; a form's advantage does not), P and the layout's slot widths."""
     bucket = 1 << max(0, int(n_clients) - 1).bit_length()
-    return (f"{ident} {'bf16' if bf16 else 'f32'} {layout.world} {bucket} {layout.P} "
-            f"{','.join(str(w) for w in layout.widths)}")
+    dt = ("bf16" if bf16 else "f32") + (".peer" if exchange == "peer_copy" else "")
+    return f"{ident} {dt} {layout.world} {bucket} {layout.P} {','.join(str(w) for w in layout.widths)}"
+
+
+class PeerExchange:
+    """The kernel-free exchange of one rank (fa_peers, csrc/peer_exchange.hpp)
+    for one slot layout and dtype: this rank's send buffer (the step's fold
+    writes its slots there), its IPC handles all-gathered once over the group,
+    and per step a fence, the one-launch fold on the exchange's own rounds
+    state, and copy-engine pulls of every rank's round-k slot as soon as that
+    rank has completed round k.  Creating one is a collective."""
+
+    def __init__(self, group, device, layout: "SlotLayout", bf16: bool):
+        import ctypes
+
+        from . import _lib
+        L = _lib.load()
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = torch.device(device)
+        self.layout, self.bf16 = layout, bf16
+        eb = 2 if bf16 else 4
+        send_bytes = -(-layout.local_width * eb // 16) * 16
+        h = ctypes.c_void_p()
+        _lib.call("fa_peers_create", ctypes.byref(h), self.device.index, self.world, self.rank, send_bytes)
+        self.h = h
+        nb = L.fa_peers_handle_bytes()
+        mine = (ctypes.c_uint8 * nb)()
+        _lib.call("fa_peers_handle", h, mine)
+        if self.world > 1:
+            every = [None] * self.world
+            dist.all_gather_object(every, bytes(mine), group=group)
+        else:
+            every = [bytes(mine)]
+        joined = b"".join(every)
+        _lib.call("fa_peers_open", h, ctypes.create_string_buffer(joined, len(joined)))
+        self.state = ctypes.c_void_p(L.fa_peers_rounds(h))
+        self.send = int(L.fa_peers_send(h))
+        R = layout.rounds
+        self.offsets = [layout.offset(k) for k in range(R + 1)]
+        self.src = (ctypes.c_int64 * (R + 1))(*[o * eb for o in self.offsets])
+        self.dst = (ctypes.c_int64 * (R * self.world))(
+            *[(layout.round_range(k)[0] + q * layout.width(k)) * eb for k in range(R) for q in range(self.world)])
+
+    def step(self, X_local, weights, scores, full, total, fold_stream_, other_stream):
+        """Fence, fold (every round in one launch) on fold_stream_, exchange on
+        other_stream into `full`; returns (event after the waits, state)."""
+        from . import _lib, engine
+        _lib.call("fa_peers_fence", self.h, fold_stream_.cuda_stream)
+        if self.bf16:
+            local = torch.empty(self.layout.local_width, dtype=torch.float32, device=self.device)
+            engine.fold_rounds(X_local, weights, scores, self.offsets, out=local, out_bf16=self.send, total=total,
+                               state=self.state)
+            local.record_stream(fold_stream_)
+        else:
+            engine.fold_rounds(X_local, weights, scores, self.offsets, out=self.send, total=total, state=self.state)
+        _lib.call("fa_peers_exchange", self.h, self.layout.rounds, self.src, full.data_ptr(), self.dst,
+                  other_stream.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(other_stream)
+        return done, self.state
+
+    def close(self) -> None:
+        """Collective: every rank's exchanges are complete before any buffer goes."""
+        from . import _lib
+        if self.h is None:
+            return
+        torch.cuda.synchronize(self.device)
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        _lib.call("fa_peers_destroy", self.h)
+        self.h = None
 
 
 class ShardedAggregator:
@@ -266,13 +337,24 @@ class ShardedAggregator:
                   must be called before the results are used.
     device_ident -- the identity decisions are keyed by (default: the GPU's
       arch and CU count, device_ident()).
+    exchange -- how a one-launch step reassembles the model:
+      "rccl"       (default) one all_gather_into_tensor per round behind its wait
+                   (RCCL over xGMI under "nccl": copy kernels on a few CUs);
+      "peer_copy"  each rank pulls its peers' finished slots with copy-engine
+                   copies through IPC-opened buffers (PeerExchange, fa_peers):
+                   no kernel beside the fold but one wave per round that polls
+                   the ranks' flags.  Needs the one-launch step on every rank
+                   (checked once per layout with a collective; otherwise
+                   "rccl"); one_launch=False keeps per-round launches with RCCL.
+                   close() releases the buffers (a collective).
     """
 
     # calls per step form the "probe" mode times before it keeps the faster
     PROBE_CALLS = 2
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None,
-                 one_launch="auto", check: str = "sync", device_ident: Optional[str] = None):
+                 one_launch="auto", check: str = "sync", device_ident: Optional[str] = None,
+                 exchange: str = "rccl"):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -285,6 +367,10 @@ class ShardedAggregator:
             raise ValueError(f"one_launch must be True, False, 'auto' or 'probe', not {one_launch!r}")
         if check not in ("sync", "deferred"):
             raise ValueError(f"check must be 'sync' or 'deferred', not {check!r}")
+        if exchange not in ("rccl", "peer_copy"):
+            raise ValueError(f"exchange must be 'rccl' or 'peer_copy', not {exchange!r}")
+        self.exchange = exchange
+        self._peers: dict = {}  # (layout widths, P, world, bf16, device) -> PeerExchange, or None: not every rank can
         self.one_launch = one_launch
         self.check = check
         self.ident = device_ident
@@ -300,7 +386,7 @@ class ShardedAggregator:
             if not X_local.is_cuda:
                 return None
             ident = self.ident = device_ident(X_local.device)
-        return step_key(ident, X_local.dtype == torch.bfloat16, int(X_local.shape[0]), layout)
+        return step_key(ident, X_local.dtype == torch.bfloat16, int(X_local.shape[0]), layout, self.exchange)
 
     def step_form(self, X_local: torch.Tensor, layout: "SlotLayout") -> Optional[str]:
         """The recorded step form for this shape ("one launch" / "per round"),
@@ -426,7 +512,18 @@ class ShardedAggregator:
             if probing:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(fs)
-            if one:
+            px = self._peer_exchange(X_local, weights, scores, layout, total) if (
+                one and self.exchange == "peer_copy") else None
+            if px is not None:
+                odt = torch.bfloat16 if px.bf16 else torch.float32
+                full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
+                if full.dtype != odt or full.numel() < layout.padded_total or not full.is_contiguous():
+                    raise ValueError(f"out needs {layout.padded_total} contiguous {odt} elements")
+                gs = gather_stream(X_local.device)
+                waited = px.step(X_local, weights, scores, full, total, fs, gs)
+                fs.wait_stream(gs)
+                full = full[: layout.P]
+            elif one:
                 full, waited = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
             else:
                 full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
@@ -479,6 +576,30 @@ class ShardedAggregator:
             pending[-1][0].synchronize()  # the waits complete in stream order
         self._raise_on_timeouts(self._timed_out([p[1] for p in pending]))
 
+    def close(self) -> None:
+        """Release the peer exchanges' buffers (exchange="peer_copy"): a
+        collective, after every rank's last step."""
+        for px in self._peers.values():
+            if px is not None:
+                px.close()
+        self._peers.clear()
+
+    def _peer_exchange(self, X_local, weights, scores, layout, total):
+        """This layout's PeerExchange, created on first use (a collective: the
+        ranks' handles are all-gathered, and every rank must be able to run the
+        one-launch step, else None: the RCCL exchange)."""
+        bf16 = X_local.dtype == torch.bfloat16
+        key = (tuple(layout.widths), layout.P, layout.world, bf16, X_local.device)
+        if key not in self._peers:
+            ok = self._one_launch_ok(X_local, weights, scores, layout, total)
+            if self.world > 1:
+                t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                 device=X_local.device if dist.get_backend(self.group) == "nccl" else "cpu")
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+                ok = bool(t.item())
+            self._peers[key] = PeerExchange(self.group, X_local.device, layout, bf16) if ok else None
+        return self._peers[key]
+
     def _record_probe(self, probing, ev, X_local, layout) -> None:
         """One timed call of the "probe" mode: its device time (max over the
         group's ranks, so every rank keeps the same form); after PROBE_CALLS
@@ -494,6 +615,63 @@ class ShardedAggregator:
         if len(got["one"]) >= self.PROBE_CALLS and len(got["per"]) >= self.PROBE_CALLS:
             del self._probe[key]
             self.record_step_form(X_local, layout, min(got["one"]) <= min(got["per"]))
+
+    def _one_launch_ok(self, X_local, weights, scores, layout, total) -> bool:
+        import numpy as np
+
+        from .engine import result_dtype
+        if not (self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
+            return False
+        if X_local.dtype not in (torch.float32, torch.bfloat16) or X_local.stride(1) != 1:
+            return False
+        if X_local.shape[0] < 1 or min(layout.widths) < 1:
+            return False
+        align = 8 if X_local.dtype == torch.bfloat16 else 4
+        if any(layout.offset(k) % align for k in range(layout.rounds)) or X_local.stride(0) % align:
+            return False
+        if X_local.data_ptr() % 16:
+            return False
+        return result_dtype(np.dtype(np.float32), list(weights), scores, total) == np.float32
+
+    def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total):
+        """Every round's fold in ONE launch on the current (fold) stream; round
+        k's exchange issued on the gather stream behind a wait for round k, so
+        it runs while the launch folds the later rounds.  Returns the model and
+        (an event after the last wait, the rounds state) for the timeout check."""
+        from . import engine
+        dev = X_local.device
+        bf16 = X_local.dtype == torch.bfloat16
+        odt = torch.bfloat16 if bf16 else torch.float32
+        full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
+        if full.dtype != odt or full.numel() < layout.padded_total:
+            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
+        local = torch.empty(layout.local_width, dtype=torch.float32, device=dev)
+        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=dev) if bf16 else None
+        offs = [layout.offset(k) for k in range(layout.rounds + 1)]
+        r = engine.fold_rounds(X_local, weights, scores, offs, out=local, out_bf16=local_b, total=total)
+        fs = torch.cuda.current_stream(dev)
+        gs = gather_stream(dev)
+        send_all = local_b if bf16 else local
+        send_all.record_stream(gs)
+        works = []
+        waits_done = torch.cuda.Event()
+        for k in range(layout.rounds):
+            engine.wait_round(r, k, gs)
+            if k == layout.rounds - 1:
+                waits_done.record(gs)  # every round's wait has run (the timeout check)
+            lo, hi = layout.round_range(k)
+            send = send_all[layout.offset(k):layout.offset(k + 1)]
+            with torch.cuda.stream(gs):
+                if self.world == 1:
+                    full[lo:hi].copy_(send)
+                    continue
+                w = gather_into(full[lo:hi], send, self.group, async_op=True)
+            if w is not None:
+                works.append(w)
+        for w in works:
+            w.wait()  # the fold stream waits for the collectives
+        fs.wait_stream(gs)
+        return full[: layout.P], (waits_done, r)
 
     def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
         bf16 = X_local.dtype == torch.bfloat16

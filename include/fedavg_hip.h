@@ -163,6 +163,48 @@ int fa_rounds_timeouts(fa_rounds* r);
 /* [host] the kernel form fa_fedavg_bf16_rounds (bf16 != 0) / _f32_rounds runs */
 const char* fa_rounds_form(int bf16);
 
+/* ---- kernel-free peer exchange of a step (ABI 4) ------------------------------
+ * The reference saves ONE global model per round (aggregation.py:125-138 ->
+ * ParameterDao.save, client_daos.py:351-378); at N > 1 every rank folds its
+ * slots and needs every other rank's.  An RCCL all-gather runs copy kernels on
+ * a few CUs beside the next round's fold; here each rank PULLS its peers'
+ * finished slots with hipMemcpyAsync on copy streams (the copy engines: no
+ * CU) from their send buffers, opened once through IPC handles.  One object
+ * per rank and layout; every call below that names a step is made by every
+ * rank of the group, in the same order.
+ *   fa_peers_create:  this rank's send buffer (send_bytes, 16-B multiple), its
+ *                     ack words and its own rounds state (device memory)
+ *   fa_peers_handle_bytes / fa_peers_handle: [host] this rank's IPC handles
+ *   fa_peers_open:    [host] every rank's handles, world x handle_bytes in rank
+ *                     order (all-gathered by the caller); opens the peers'
+ *   fa_peers_send:    [host] the send buffer: the step's fold writes this
+ *                     rank's slots there (out_bf16 for bf16 rows, out for fp32)
+ *   fa_peers_rounds:  [host] the rounds state (owned by the fa_peers) to pass
+ *                     to fa_fedavg_*_rounds: its launches publish every round
+ *                     at system scope
+ *   fa_peers_fence:   enqueue on the fold stream, before the fold launch: wait
+ *                     until every peer has pulled the previous step out of this
+ *                     rank's send buffer
+ *   fa_peers_exchange: enqueue, after the launch, on another stream: per round
+ *                     k, a wait until every rank has completed round k, then
+ *                     rank q's bytes [src_offsets[k], src_offsets[k+1]) of its
+ *                     send buffer are copied to dst + dst_offsets[k * world + q]
+ *                     (this rank's own slot included); then this rank tells
+ *                     every peer it is done reading their buffers.  A wait that
+ *                     gives up is reported by fa_rounds_check(fa_peers_rounds).
+ *   fa_peers_destroy: after every rank's last exchange (a barrier) */
+typedef struct fa_peers fa_peers;
+int fa_peers_create(fa_peers** x, int device, int world, int rank, int64_t send_bytes);
+int fa_peers_destroy(fa_peers* x);
+int fa_peers_handle_bytes(void);
+int fa_peers_handle(fa_peers* x, void* out);
+int fa_peers_open(fa_peers* x, const void* all_handles);
+void* fa_peers_send(fa_peers* x);
+fa_rounds* fa_peers_rounds(fa_peers* x);
+int fa_peers_fence(fa_peers* x, void* stream);
+int fa_peers_exchange(fa_peers* x, int rounds, const int64_t* src_offsets, void* dst, const int64_t* dst_offsets,
+                      void* stream);
+
 /* The same folds with the per-client factors a[0..N), s[0..N) (s may be
  * NULL) in HOST memory, as the reference's caller holds them (Python numbers,
  * fed_avg_aggregator.py:32-41).  The library copies them into a page-locked

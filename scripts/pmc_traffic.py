@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--bytes", type=float, required=True, help="algorithmic bytes per fold call")
     ap.add_argument("--dispatches-per-call", type=int, default=1,
                     help="kernel dispatches one fa_fedavg_f32 call makes (column bands); bytes are summed per call")
+    ap.add_argument("--calls", type=int, default=0,
+                    help="instead of whole calls of --dispatches-per-call: the total over every matching dispatch "
+                         "divided by this many calls (steps whose per-round launches use several kernels)")
+    ap.add_argument("--sq", default="", help="a --pmc SQ_* pass of the same command: per-kernel wave-state fractions")
     ap.add_argument("--out", required=True)
     ap.add_argument("--provenance", default="", help="where the passes ran (commit, date, command)")
     a = ap.parse_args()
@@ -52,11 +56,14 @@ def main():
     if not fetch or not write:
         raise SystemExit(f"no counter rows for {a.kernel}: fetch={len(fetch)} write={len(write)}")
     k = a.dispatches_per_call
-    if len(fetch) % k or len(write) % k:
-        raise SystemExit(f"{len(fetch)}/{len(write)} dispatches are not whole calls of {k}")
-    # per call: the sum over its k consecutive band dispatches, median over calls
-    f_kib = statistics.median(sum(fetch[i:i + k]) for i in range(0, len(fetch), k))
-    w_kib = statistics.median(sum(write[i:i + k]) for i in range(0, len(write), k))
+    if a.calls:
+        f_kib, w_kib = sum(fetch) / a.calls, sum(write) / a.calls
+    else:
+        if len(fetch) % k or len(write) % k:
+            raise SystemExit(f"{len(fetch)}/{len(write)} dispatches are not whole calls of {k}")
+        # per call: the sum over its k consecutive band dispatches, median over calls
+        f_kib = statistics.median(sum(fetch[i:i + k]) for i in range(0, len(fetch), k))
+        w_kib = statistics.median(sum(write[i:i + k]) for i in range(0, len(write), k))
     read_bytes = 2.0 * f_kib * 1024.0   # gfx950: FETCH_SIZE = 1/2 of a wide streaming read
     write_bytes = w_kib * 1024.0
     res = {
@@ -74,6 +81,22 @@ def main():
                       "write = WRITE_SIZE x 1024",
         "provenance": a.provenance,
     }
+    if a.calls:
+        res["calls"] = a.calls
+        res["dispatches_per_call"] = None
+    if a.sq:
+        rows = counter_rows(a.sq)
+        tot = {}
+        for r in rows:
+            if a.kernel not in r.get("Kernel_Name", ""):
+                continue
+            tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        res["sq_totals"] = tot
+        cyc = tot.get("SQ_WAVE_CYCLES")
+        if cyc:
+            res["sq_fractions_of_wave_cycles"] = {n: v / cyc for n, v in tot.items()
+                                                  if n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                                                           "SQ_BUSY_CYCLES")}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)

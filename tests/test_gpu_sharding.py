@@ -139,7 +139,9 @@ def test_step_form_restored_from_the_cache_file(bf16, recorded, monkeypatch):
     from fedlesscan_amd import _lib, engine
     from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
     dev = torch.device("cuda", 0)
-    N, P, seed = 70, 200_003 + (8 if bf16 else 0), 31 + (recorded == "one")
+    # a key of its own per case (P): this process already holds what earlier cases recorded
+    N, seed = 70, 31 + (recorded == "one")
+    P = 200_003 + (8 if bf16 else 0) + {"one": 0, "per": 4096, None: 8192}[recorded]
     lay = SlotLayout(P, 1, 4)
     Xin, w, sc, exp = _slots_input(bf16, N, P, seed, lay, dev)
     agg = ShardedAggregator()
@@ -203,6 +205,38 @@ def test_round_wait_timeout_raises_on_every_path(monkeypatch):
     assert np.array_equal(got, expb)
 
 
+@pytest.mark.parametrize("one_launch", ["auto", True])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_aggregate_slots_captures_into_hip_graph(one_launch, bf16):
+    """Under a HIP graph capture aggregate_slots takes the per-round launches
+    (the one launch refuses capture: its epochs would replay) and times
+    nothing; the graph replays bit-exactly on new client rows."""
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    dev = torch.device("cuda", 0)
+    N, P = 24, 100_003
+    lay = SlotLayout(P, 1, 4)
+    Xin, w, sc, _ = _slots_input(bf16, N, P, 61, lay, dev)
+    agg = ShardedAggregator(one_launch=one_launch)
+    agg.aggregate_slots(Xin, w, sc, lay)  # the tuner's first calls of the slot shapes, outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        full = agg.aggregate_slots(Xin, w, sc, lay)
+    for seed in (62, 63):
+        src, _, _, exp = _slots_input(bf16, N, P, seed, lay, dev)
+        Xin.copy_(src)
+        g.replay()
+        torch.cuda.synchronize()
+        got = _bits(full, bf16)
+        # the weights are the captured ones (seed 61's); the expected bits with them
+        from oracle import fedavg_oracle as O
+        if bf16:
+            _, exp = O.fedavg_stacked_bf16(synth.clients_bf16(seed, N, 0, P), w, sc)
+        else:
+            exp = O.fedavg_stacked(synth.clients_f32(seed, N, 0, P), w, sc).view(np.uint32)
+        assert np.array_equal(got, exp), seed
+
+
 @pytest.mark.parametrize("one_launch", [True, False])
 @pytest.mark.parametrize("bf16", [False, True])
 def test_quantised_layout_world1(one_launch, bf16):
@@ -251,7 +285,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, N, P, rounds, seed, bf16, q):
+def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl"):
     import torch as T
     import torch.distributed as dist
     from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
@@ -272,27 +306,48 @@ def _rank(rank, world, port, N, P, rounds, seed, bf16, q):
                 X[:, k * lay.sub:k * lay.sub + hi - lo] = T.from_numpy(part).to(dev)
         w = synth.cardinalities(seed, N)
         sc = _scores(seed, N)
-        agg = ShardedAggregator(one_launch="probe")  # the probe's all-reduce runs over the group
+        Xin = X.view(T.bfloat16) if bf16 else X
         outs = []
-        for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
-            full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc, lay)
-            outs.append(full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes())
+        if exchange == "rccl":
+            agg = ShardedAggregator(one_launch="probe")  # the probe's all-reduce runs over the group
+            for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
+                full = agg.aggregate_slots(Xin, w, sc, lay)
+                outs.append(full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes())
+            assert agg.step_form(Xin, lay) in ("one launch", "per round")
+        else:
+            # the peer-copy exchange: IPC-opened send buffers, flags polled across
+            # processes, copy-engine pulls; steps back to back (the fence keeps a
+            # send buffer until every peer has pulled it), then sync and deferred
+            agg = ShardedAggregator(one_launch=True, exchange=exchange)
+            fulls = [agg.aggregate_slots(Xin, w, sc, lay) for _ in range(4)]
+            outs = [f.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes() for f in fulls]
+            deferred = ShardedAggregator(one_launch=True, exchange=exchange, check="deferred")
+            fulls = [deferred.aggregate_slots(Xin, w, sc, lay) for _ in range(3)]
+            deferred.check_timeouts()
+            outs += [f.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes() for f in fulls]
+            assert len(agg._peers) == 1 and next(iter(agg._peers.values())) is not None
+            agg.close()
+            deferred.close()
         assert all(o == outs[0] for o in outs)
-        assert agg.step_form(X.view(T.bfloat16) if bf16 else X, lay) in ("one launch", "per round")
         q.put((rank, outs[0]))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("exchange", ["rccl", "peer_copy"])
 @pytest.mark.parametrize("bf16", [False, True])
-def test_two_ranks_on_one_gpu(bf16):
+def test_two_ranks_on_one_gpu(bf16, exchange):
+    """Two ranks share the GPU over gloo: the slot exchange through the group
+    ("rccl": gloo host-staged here), or the kernel-free peer copy (IPC handles
+    of the same device, cross-process flags and acks), bit-exact."""
     import torch.multiprocessing as mp
     from oracle import fedavg_oracle as O
     N, P, rounds, seed, world = 17, 20011, 3, 8, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, N, P, rounds, seed, bf16, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, N, P, rounds, seed, bf16, q, exchange))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=100) for _ in range(world))
