@@ -37,12 +37,56 @@ struct FactorRing {
 };
 FactorRing g_factor_rings[16];
 
+// Under a HIP graph capture the ring cannot be used (waiting for a slot's
+// event is not allowed while a stream captures, and a captured copy would read
+// the slot again at every replay, after later calls rewrote it): the factors
+// become kernel arguments of fill kernels -- captured by value -- that write a
+// stream-ordered allocation of the graph, freed after the fold.
+constexpr int kFillFloats = 480;
+struct FillArgs {
+    float v[kFillFloats];
+};
+__global__ __launch_bounds__(64) void k_fill_factors(float* dst, FillArgs f, int n) {
+    for (int i = threadIdx.x; i < n; i += 64) dst[i] = f.v[i];
+}
+
+template <class Launch>
+int with_captured_factors(const float* a, const float* s, int64_t N, hipStream_t st, Launch launch) {
+    const int64_t need = N * (s ? 2 : 1);
+    float* d = nullptr;
+    hipError_t e = hipMallocAsync((void**)&d, (size_t)need * sizeof(float), st);
+    if (e != hipSuccess) return fail(FA_ERR_HIP, "captured factors: hipMallocAsync: %s", hipGetErrorString(e));
+    for (int64_t off = 0; off < need; off += kFillFloats) {
+        FillArgs f;
+        const int n = (int)(need - off < kFillFloats ? need - off : kFillFloats);
+        for (int i = 0; i < n; ++i) {
+            const int64_t j = off + i;
+            f.v[i] = j < N ? a[j] : s[j - N];
+        }
+        hipLaunchKernelGGL(k_fill_factors, dim3(1), dim3(64), 0, st, d + off, f, n);
+        const int rc = check_launch("captured factors");
+        if (rc) return rc;
+    }
+    const int rc = launch((const float*)d, s ? (const float*)(d + N) : (const float*)nullptr);
+    e = hipFreeAsync(d, st);
+    if (e != hipSuccess && !rc) return fail(FA_ERR_HIP, "captured factors: hipFreeAsync: %s", hipGetErrorString(e));
+    return rc;
+}
+
 // Stage a[0..N) (and s[0..N) when s != NULL) and run launch(a_dev, s_dev) on
 // `stream` with the ring slot held; the slot's event is recorded after it.
 template <class Launch>
 int with_host_factors(const float* a, const float* s, int64_t N, void* stream, Launch launch) {
     if (N <= 0) return launch((const float*)nullptr, (const float*)nullptr);  // the entry's own checks report
     if (!a) return fail(FA_ERR_ARG, "null host factor pointer");
+    {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) (void)hipGetLastError();
+        else if (cs != hipStreamCaptureStatusNone) {
+            StreamDevice on_stream_device(stream);
+            return with_captured_factors(a, s, N, (hipStream_t)stream, launch);
+        }
+    }
     // the slot (and its device buffer) of the GPU that owns the stream, not of
     // the calling thread's current device
     StreamDevice on_stream_device(stream);
@@ -283,6 +327,9 @@ int fa_rounds_timeouts(fa_rounds* r) {
 int fa_peers_create(fa_peers** x, int device, int world, int rank, int64_t send_bytes) {
     if (!x) return fail(FA_ERR_ARG, "fa_peers_create: null handle");
     *x = nullptr;
+    if (world < 1 || world > kMaxPeers || rank < 0 || rank >= world || send_bytes < 16 || send_bytes % 16)
+        return fail(FA_ERR_ARG, "fa_peers_create: world %d (1..%d), rank %d, send_bytes %lld (16-B multiple)", world,
+                    kMaxPeers, rank, (long long)send_bytes);
     fa_peers* o = new fa_peers();
     const int rc = peers_init(*o, device, world, rank, send_bytes);
     if (rc) {

@@ -1508,12 +1508,119 @@ struct StepTable {
     int32_t segs;
     int32_t rounds;
     int32_t sys;    // publish the rounds at system scope: other GPUs read them (fa_peers, the peer exchange)
-    int32_t noacq;  // (A/B only) the completing block skips its acquire fence
+    int64_t stride[kMaxSegs];  // balanced rounds (step_tiles_bal): static segment g dealt over stride[g] blocks
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
 // [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
 constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
 constexpr int kStatusWords = kMaxRounds + 1;  // a timeout record per round + the peer exchange's buffer fence
+
+// A block leaves round k (its tiles come in round order): publish its cnt
+// tiles of the round once (MI355X_MICROARCH.md, valid producer form): every
+// storing wave waits for its stores, a barrier, then one lane writes the XCD's
+// L2 back (agent release fence) and counts the tiles with an agent-scope add
+// (every block's adds form one release sequence).  The block whose add
+// completes the round takes an acquire fence -- it synchronises with every
+// other block's release -- and raises the round's flag with a release store,
+// so whoever acquires the flag sees the whole round by the memory model, not
+// only by this hardware's write-back order.  One acquire per round: it costs
+// nothing measurable (1.044 ms per C4 rank step with and without it, one box,
+// profiles/r05_step/), where an acq_rel add in every block (256 x rounds per
+// step) cost ~4 %.
+// T.sys: the same at system scope, for peers that read the round over xGMI
+// (fa_peers).  Block-uniform arguments (every thread calls it).
+__device__ __forceinline__ void step_publish(const StepTable& T, unsigned int* sig, unsigned int epoch, int k,
+                                             unsigned int cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (T.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int nk = (unsigned int)T.round_tiles[k];
+        if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cnt ==
+            nk) {  // the round's last tiles
+            __hip_atomic_store(&sig[kSigDone + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (T.sys) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// The last block out resets the dynamic-tile counters for the next launch.
+__device__ __forceinline__ void step_reset(unsigned int* sig) {
+    if (threadIdx.x == 0) {
+        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {
+            atomicExch(&sig[0], 0u);
+            atomicExch(&sig[1], 0u);
+        }
+    }
+}
+
+// Balanced rounds (round 5): every static segment -- a round's wide tiles --
+// is dealt over its own stride[g] blocks, the fewest that still fold it in
+// the same number of passes (block b < stride[g] folds tiles b, b + stride[g],
+// ...), as the per-round band launches' balanced grids do; the blocks past the
+// stride go straight on to the next round.  So no round ends in a partial
+// pass, without a launch boundary between rounds.  Then the dynamic pool (the
+// last round's last columns), a tile fetched ahead as in step_tiles.  The
+// static segments are wide tiles and the pool's narrow (build_step_table), so
+// each call site inlines one tile body.
+template <class Wide, class Narrow>
+__device__ __forceinline__ void step_tiles_bal(const StepTable& T, unsigned int* sig, unsigned int epoch,
+                                               Wide wide, Narrow narrow) {
+    __shared__ unsigned int nxt[2];
+    const int64_t b = blockIdx.x;
+    const int64_t ntiles = T.seg_end[T.segs - 1];
+    const int64_t Ts = T.static_tiles;
+    int k = -1;
+    unsigned int cnt = 0;
+    int g = 0;
+    for (; g < T.segs; ++g) {
+        const int64_t lo = g ? T.seg_end[g - 1] : 0;
+        if (lo >= Ts) break;
+        if (T.round[g] != k) {
+            if (k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
+            k = T.round[g];
+            cnt = 0;
+        }
+        const int64_t n = T.seg_end[g] - lo, S = T.stride[g];
+        for (int64_t i = b; b < S && i < n; i += S) {
+            wide(g, i);
+            ++cnt;
+        }
+    }
+    if (Ts < ntiles) {  // the dynamic pool
+        int p = 0;
+        if (threadIdx.x == 0) nxt[p] = atomicAdd(&sig[0], 1u);
+        __syncthreads();
+        int64_t t = Ts + nxt[p];
+        p ^= 1;
+        while (t < ntiles) {
+            while (g + 1 < T.segs && t >= T.seg_end[g]) ++g;
+            if (T.round[g] != k) {
+                if (k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
+                k = T.round[g];
+                cnt = 0;
+            }
+            unsigned int nx = 0;
+            if (threadIdx.x == 0) nx = atomicAdd(&sig[0], 1u);  // fetched a tile ahead
+            narrow(g, t - (g ? T.seg_end[g - 1] : 0));
+            ++cnt;
+            if (threadIdx.x == 0) nxt[p] = nx;
+            __syncthreads();
+            t = Ts + nxt[p];
+            p ^= 1;
+        }
+    }
+    if (k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
+    step_reset(sig);
+}
 
 template <class Tile>
 __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Tile tile) {
@@ -1550,82 +1657,67 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
         while (gn < T.segs && tn >= T.seg_end[gn]) ++gn;  // T.segs: no tile left
         const int kn = gn < T.segs ? T.round[gn] : kMaxRounds;
         if (kn != k) {
-            // The block leaves round k (its tiles come in round order): publish
-            // its tiles of the round once (MI355X_MICROARCH.md, valid producer
-            // form): every storing wave waits for its stores, a barrier, then
-            // one lane writes the XCD's L2 back (agent release fence) and counts
-            // the tiles with an agent-scope add (every block's adds form one
-            // release sequence).  The block whose add completes the round takes
-            // an acquire fence -- it synchronises with every other block's
-            // release -- and raises the round's flag with a release store, so
-            // whoever acquires the flag sees the whole round by the memory
-            // model, not only by this hardware's write-back order.  One acquire
-            // per round: an acq_rel add in every block (an L2 invalidate each,
-            // 256 x rounds per step) cost the C4 rank's step ~7 %.
-            // (T.sys: the same at system scope, for peers that read the round
-            // over xGMI -- fa_peers.)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                if (T.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const unsigned int nk = (unsigned int)T.round_tiles[k];
-                if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                        cnt == nk) {  // the round's last tiles
-                    __hip_atomic_store(&sig[kSigDone + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (T.sys) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                        __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                    } else {
-                        if (!T.noacq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                        __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-            }
+            step_publish(T, sig, epoch, k, cnt);
             cnt = 0;
             k = kn;
         }
         t = tn;
         g = gn < T.segs ? gn : g;
     }
-    if (threadIdx.x == 0) {
-        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {  // the last block out resets the tile counters
-            atomicExch(&sig[0], 0u);
-            atomicExch(&sig[1], 0u);
-        }
-    }
+    step_reset(sig);
 }
 
-// wide tiles: UB rows ahead x CB octets (quads) per lane; narrow: US x CS
-template <int UB, int CB, int US, int CS, bool SCORED, int B>
+// wide tiles: UB rows ahead x CB octets (quads) per lane; narrow: US x CS;
+// BAL: balanced rounds (step_tiles_bal).  One schedule per instantiation: both
+// inlined into one kernel made it ~4 % slower (code size: the unrolled tile
+// body four times over; profiles/r05_step/)
+template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false>
 __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
     const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
     unsigned int* sig, unsigned int epoch) {
-    step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+    auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        uint16_t* ob = outb ? outb + c0 : nullptr;
-        if (T.small[g])
-            bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
-        else
-            bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0, ob);
-    });
+        bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
+                                     outb ? outb + c0 : nullptr);
+    };
+    auto narrow = [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
+                                     outb ? outb + c0 : nullptr);
+    };
+    if constexpr (BAL) {
+        step_tiles_bal(T, sig, epoch, wide, narrow);
+    } else {
+        step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+            if (T.small[g]) narrow(g, bid);
+            else wide(g, bid);
+        });
+    }
 }
 
-template <int UB, int CB, int US, int CS, bool SCORED, int B>
+template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false>
 __global__ __launch_bounds__(B) void k_fold_f32_step(
     const float* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
     float divisor, float* __restrict__ out, StepTable T, unsigned int* sig, unsigned int epoch) {
-    step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+    auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        if (T.small[g])
-            fold_tile<US, CS, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                                 divisor, out + c0);
-        else
-            fold_tile<UB, CB, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                                 divisor, out + c0);
-    });
+        fold_tile<UB, CB, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                             divisor, out + c0);
+    };
+    auto narrow = [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        fold_tile<US, CS, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                             divisor, out + c0);
+    };
+    if constexpr (BAL) {
+        step_tiles_bal(T, sig, epoch, wide, narrow);
+    } else {
+        step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+            if (T.small[g]) narrow(g, bid);
+            else wide(g, bid);
+        });
+    }
 }
 
 // Poll round flag `flag` until it reaches `epoch` (wrapping compare), then
@@ -1856,10 +1948,8 @@ inline const char* f32_pick_name(F32Pick p) {
 }
 // bf16 fold forms (the vector path: 16-B aligned rows, ldx % 8 == 0).
 enum class Bf16Form { kV8U2C8, kV8U4C4, kV8U8C2, kV8U8C1, kBandsU8C4, kBandsU8C2, kBandsU2C8, kBandsU4C4,
-                      kBandsU16C2, kGsBalU8C2, kGs1U8C4,
-                      // round 5: two blocks per CU (twice the bytes in flight per CU)
-                      kBands2xU8C4, kBands2xU8C2, kBands2xU4C4 };
-constexpr int kNumBf16Forms = (int)Bf16Form::kBands2xU4C4 + 1;
+                      kBandsU16C2, kGsBalU8C2, kGs1U8C4 };
+constexpr int kNumBf16Forms = (int)Bf16Form::kGs1U8C4 + 1;
 inline const char* bf16_form_name(Bf16Form f) {
     switch (f) {
         case Bf16Form::kV8U2C8: return "bf16_tile_u2c8";
@@ -1873,9 +1963,6 @@ inline const char* bf16_form_name(Bf16Form f) {
         case Bf16Form::kBandsU16C2: return "bf16_bands4_u16c2";
         case Bf16Form::kGsBalU8C2: return "bf16_gsbal_u8c2";
         case Bf16Form::kGs1U8C4: return "bf16_gs1_u8c4";
-        case Bf16Form::kBands2xU8C4: return "bf16_bands4x2_u8c4";
-        case Bf16Form::kBands2xU8C2: return "bf16_bands4x2_u8c2";
-        case Bf16Form::kBands2xU4C4: return "bf16_bands4x2_u4c4";
     }
     return "";
 }
@@ -2139,21 +2226,20 @@ void launch_bf16_gs(hipStream_t st, int per_cu, const uint16_t* X, int64_t N, in
                            a, s, d, out, outb, tiles);
 }
 
-// per_cu: blocks per CU of each band's balanced launch (a pass is per_cu x CUs tiles)
 template <int U, int C>
 void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
-                       const float* a, const float* s, float d, float* out, uint16_t* outb, int per_cu = 1) {
+                       const float* a, const float* s, float d, float* out, uint16_t* outb) {
     const int64_t to = (int64_t)kBlock * C;  // octets per tile
     const int64_t units = (P >> 3) + ((P & 7) ? 1 : 0);
     const int64_t tiles = (units + to - 1) / to;
-    const int64_t per_band = (int64_t)passes * per_cu * cu_count();
+    const int64_t per_band = (int64_t)passes * cu_count();
     const int64_t nb = (tiles + per_band - 1) / per_band;
     const int64_t band_tiles = (tiles + nb - 1) / nb;
     for (int64_t b = 0; b < nb; ++b) {
         const int64_t c0 = b * band_tiles * to * 8;
         if (c0 >= P) break;
         const int64_t pb = (P - c0) < band_tiles * to * 8 ? (P - c0) : band_tiles * to * 8;
-        launch_bf16_gs<U, C>(st, -per_cu, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
+        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
     }
 }
 
@@ -2168,7 +2254,7 @@ struct StepSpec {
     int ub, cb, us, cs, pool100;
     bool last_only = false;   // the pool never reaches past the last round's columns
     bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
-    bool noacq = false;       // (A/B only) no acquire fence in the block that completes a round
+    bool bal = false;         // balanced rounds: each round's wide tiles over its own balanced block count
 };
 // The policy's two forms and two bf16 comparison forms (the bench library
 // and the GPU tests run every one).  Round 4 measured 41 forms on the whole
@@ -2193,8 +2279,12 @@ constexpr StepSpec kStepSpecs[] = {
     {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75},
     {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, true},
     {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0},
-    // round 5 A/B: the policy without the completing block's acquire fence
-    {"bf16_step_rt_u8c4n8c2_p100_last_noacq", true, 8, 4, 8, 2, 100, true, true, true},
+    // round 5 candidates: balanced rounds (step_tiles_bal), no pool / a last-round pool
+    {"bf16_step_bal_u8c4", true, 8, 4, 8, 2, 0, true, false, true},
+    {"bf16_step_bal_u8c4_p50_last", true, 8, 4, 8, 2, 50, true, false, true},
+    {"bf16_step_bal_u8c2", true, 8, 2, 8, 2, 0, true, false, true},
+    {"f32_step_bal_u8c4", false, 8, 4, 16, 1, 0, true, false, true},
+    {"f32_step_bal_u8c4_p75_last", false, 8, 4, 16, 1, 75, true, false, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2228,6 +2318,7 @@ struct RoundsState {
     bool sys = false;                     // publish rounds at system scope (a peer exchange's state)
     hipEvent_t start = nullptr;           // recorded on the launch's stream just before the launch: a waiter's
                                           // stream waits for it, so its give-up clock starts with the fold
+    hipStream_t last_stream = nullptr;    // the stream of the last launch
     hipEvent_t done = nullptr;            // recorded just after the launch: the next launch with this state
                                           // waits for it, whatever stream it is on (a stream handle reused
                                           // after its stream was destroyed cannot overlap two launches)
@@ -2272,13 +2363,16 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
         T.small[g] = small ? 1 : 0;
         T.round_tiles[k] += (units(hi - lo) + per - 1) / per;
         if (is_static) T.static_tiles = total;
+        // balanced: the fewest blocks that fold the segment in the same number of passes
+        const int64_t n = (units(hi - lo) + per - 1) / per, passes = (n + grid - 1) / grid;
+        T.stride[g] = passes > 0 ? (n + passes - 1) / passes : 1;
     };
     for (int pass = 0; pass < 2; ++pass)
         for (int k = 0; k < rounds; ++k) {
             const int64_t w = offsets[k + 1] - offsets[k];
             const int64_t lo = pass == 0 ? 0 : split[k], hi = pass == 0 ? split[k] : w;
             if (hi <= lo) continue;
-            if (pass == 0 && sp.round_tail && k + 1 < rounds) {
+            if (pass == 0 && sp.round_tail && !sp.bal && k + 1 < rounds) {
                 // whole passes of wide tiles, then the rest of the round's static columns narrow
                 const int64_t full = ((hi - lo) / wide_cols / grid) * grid;
                 const int64_t mid = lo + full * wide_cols;
@@ -2400,12 +2494,12 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
     T.sys = R.sys ? 1 : 0;
-    T.noacq = sp.noacq ? 1 : 0;
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
-    // after the previous launch with this state, on whatever stream it ran
-    if (R.epoch != 0 && R.done && hipStreamWaitEvent(st, R.done, 0) != hipSuccess)
+    // after the previous launch with this state: stream order when it ran on
+    // this stream, else a wait for its done event
+    if (R.epoch != 0 && R.done && st != R.last_stream && hipStreamWaitEvent(st, R.done, 0) != hipSuccess)
         return check_launch("rounds fold: previous launch");
     if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
@@ -2413,35 +2507,40 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     // the kernel instantiation is found from the form's tile shapes (never by
     // its index): a form whose shapes no instantiation below has is refused
     bool launched = false;
-#define FA_STB(UB, CB, US, CS)                                                                                   \
-    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS) {                      \
+#define FA_STB(UB, CB, US, CS, BAL)                                                                              \
+    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL) {     \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid),         \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, BAL>), dim3((unsigned)grid),    \
                                dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),        \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, BAL>), dim3((unsigned)grid),   \
                                dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
     }
-#define FA_STF(UB, CB, US, CS)                                                                                    \
-    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS) {                     \
+#define FA_STF(UB, CB, US, CS, BAL)                                                                              \
+    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL) {    \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
-            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock>), dim3((unsigned)grid),            \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock, BAL>), dim3((unsigned)grid),       \
                                dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock>), dim3((unsigned)grid),           \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock, BAL>), dim3((unsigned)grid),      \
                                dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
     }
-    FA_STB(8, 4, 8, 2)
-    FA_STB(8, 4, 8, 4)
-    FA_STF(8, 4, 16, 1)
+    FA_STB(8, 4, 8, 2, false)
+    FA_STB(8, 4, 8, 4, false)
+    FA_STB(8, 4, 8, 2, true)
+    FA_STB(8, 2, 8, 2, true)
+    FA_STF(8, 4, 16, 1, false)
+    FA_STF(8, 4, 16, 1, true)
 #undef FA_STB
 #undef FA_STF
     if (!launched) return fail(FA_ERR_ARG, "step form %s: no kernel for its tile shapes", sp.name);
     rc = check_launch("rounds fold");
     if (rc) return rc;
-    if (R.done && hipEventRecord(R.done, st) != hipSuccess) return check_launch("rounds fold: done event");
+    if (R.done && hipEventRecord(R.done, st) != hipSuccess)
+        return check_launch("rounds fold: done event");
+    R.last_stream = st;
     R.epoch = epoch;
     R.rounds = rounds;
     R.launched = true;
@@ -2838,15 +2937,6 @@ inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int6
             break;
         case Bf16Form::kGsBalU8C2: launch_bf16_gs<8, 2>(st, -1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
         case Bf16Form::kGs1U8C4: launch_bf16_gs<8, 4>(st, 1, X, N, P, ldx, a, s, divisor, out_f32, out_bf16); break;
-        case Bf16Form::kBands2xU8C4:
-            launch_bf16_bands<8, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
-            break;
-        case Bf16Form::kBands2xU8C2:
-            launch_bf16_bands<8, 2>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
-            break;
-        case Bf16Form::kBands2xU4C4:
-            launch_bf16_bands<4, 4>(st, 4, X, N, P, ldx, a, s, divisor, out_f32, out_bf16, 2);
-            break;
     }
 #undef FA_BF
 }

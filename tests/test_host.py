@@ -117,6 +117,27 @@ def test_library_argument_errors_need_no_gpu():
     assert type(ei.value).__name__ == "InsufficientClientResults"
 
 
+def test_exchange_entry_argument_errors_need_no_gpu():
+    """ABI 4's multi-GPU entries validate before any HIP call: bad peer-group
+    shapes, null handles, malformed step-form keys."""
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    for world, rank, nbytes in ((0, 0, 64), (17, 0, 64), (2, 2, 64), (2, -1, 64), (2, 0, 8), (2, 0, 100)):
+        assert L.fa_peers_create(ctypes.byref(h), 0, world, rank, nbytes) == _lib.FA_ERR_ARG, (world, rank, nbytes)
+        assert h.value is None
+    assert L.fa_peers_create(None, 0, 2, 0, 64) == _lib.FA_ERR_ARG
+    assert L.fa_peers_handle_bytes() == 3 * 64  # three hipIpcMemHandle_t
+    assert L.fa_peers_fence(None, None) == _lib.FA_ERR_ARG
+    assert L.fa_peers_exchange(None, 1, None, None, None, None) == _lib.FA_ERR_ARG
+    assert L.fa_peers_send(None) is None and L.fa_peers_rounds(None) is None
+    assert L.fa_peers_destroy(None) == _lib.FA_OK
+    assert L.fa_rounds_check(None) < 0
+    assert L.fa_step_lookup(b"gfx950:256 f16 8 256 100 64") == -2
+    assert L.fa_step_lookup(b"gfx950:256 bf16 8 255 100 64") == -2
+    assert L.fa_step_lookup(None) == -2
+    assert L.fa_step_record(b"not a key", 1) == _lib.FA_ERR_ARG
+
+
 def test_product_package_does_not_import_oracle():
     import pathlib
     pkg = pathlib.Path(_lib.PKG)
