@@ -2256,35 +2256,35 @@ struct StepSpec {
     bool round_tail = false;  // each round but the last: whole passes of wide tiles, the rest in narrow static tiles
     bool bal = false;         // balanced rounds: each round's wide tiles over its own balanced block count
 };
-// The policy's two forms and two bf16 comparison forms (the bench library
-// and the GPU tests run every one).  Round 4 measured 41 forms on the whole
-// step with the exchange proxy's copies included (DESIGN_HISTORY.md R4;
-// profiles/r04_step/): pool sizes, reduced grids, sc1 stores, pass barriers,
-// all-dynamic tiles.  What is left:
-//   bf16_step_rt_u8c4n8c2_p100_last  the bf16 policy (a C4 rank's slots): whole
-//     passes of 8 x 4-octet wide tiles per round, the rest of each round in
-//     8 x 2-octet static tiles over all blocks (the round completes near its
-//     share of the launch instead of a tile-time later), the last round's
-//     columns a one-pass dynamic pool (1.01 ms alone; 1.21-1.26 host / 1.20-2.00
-//     HBM beside the proxy's copies against 1.22-1.30 / 1.25-2.06 per round)
+// The policy's two forms and one comparison form per dtype beside the round-4
+// bf16 policy (the bench library and the GPU tests run every one).  Round 4
+// measured 41 forms on the whole step with the exchange proxy's copies
+// included (DESIGN_HISTORY.md R4; profiles/r04_step/): pool sizes, reduced
+// grids, sc1 stores, pass barriers, all-dynamic tiles; round 5 the balanced
+// rounds (profiles/r05_step/, r05_exchange/).  What is left:
+//   bf16_step_bal_u8c4               the bf16 policy (a C4 rank's slots, round
+//     5): each round's 8 x 4-octet wide tiles dealt over its own balanced
+//     block count (step_tiles_bal), the rounds' remainders in 8 x 2-octet
+//     tiles, no dynamic pool (1.014-1.019 ms alone against 1.042-1.050 for the
+//     round-4 policy; 1.030 / 1.056 beside copy-engine copies; 1.12-1.18 /
+//     1.14-1.19 beside 16-64 copy blocks)
 //   f32_step_sd_u8c4_p75             the fp32 policy (a C3 rank): 8 x 4-quad
 //     static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
-//     6.23-6.27 beside host copies, even with per-round launches)
-//   bf16_step_sd_u8c4w_p100_last     comparison: round 4's first bf16 policy
-//     (no round tails: rounds complete a tile-time after their share)
+//     6.23-6.27 beside host copies, even with per-round launches; balanced
+//     rounds lose: 6.05-6.10 against 5.91-5.95 alone)
+//   bf16_step_rt_u8c4n8c2_p100_last  comparison: round 4's bf16 policy, whole
+//     passes of wide tiles per round, the rest of each round in narrow static
+//     tiles over all blocks, the last round's columns a one-pass dynamic pool
 //   bf16_step_static_u8c4            comparison: every tile static (the one
-//     launch without its dynamic part)
+//     launch without its dynamic part or its balancing)
+//   f32_step_bal_u8c4                comparison: the fp32 step with balanced
+//     rounds
 constexpr StepSpec kStepSpecs[] = {
-    {"bf16_step_rt_u8c4n8c2_p100_last", true, 8, 4, 8, 2, 100, true, true},
-    {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75},
-    {"bf16_step_sd_u8c4w_p100_last", true, 8, 4, 8, 4, 100, true},
-    {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0},
-    // round 5 candidates: balanced rounds (step_tiles_bal), no pool / a last-round pool
     {"bf16_step_bal_u8c4", true, 8, 4, 8, 2, 0, true, false, true},
-    {"bf16_step_bal_u8c4_p50_last", true, 8, 4, 8, 2, 50, true, false, true},
-    {"bf16_step_bal_u8c2", true, 8, 2, 8, 2, 0, true, false, true},
+    {"f32_step_sd_u8c4_p75", false, 8, 4, 16, 1, 75},
+    {"bf16_step_rt_u8c4n8c2_p100_last", true, 8, 4, 8, 2, 100, true, true},
+    {"bf16_step_static_u8c4", true, 8, 4, 8, 4, 0},
     {"f32_step_bal_u8c4", false, 8, 4, 16, 1, 0, true, false, true},
-    {"f32_step_bal_u8c4_p75_last", false, 8, 4, 16, 1, 75, true, false, true},
 };
 constexpr int kNumStepForms = (int)(sizeof(kStepSpecs) / sizeof(kStepSpecs[0]));
 inline const char* step_form_name(int f) { return (f >= 0 && f < kNumStepForms) ? kStepSpecs[f].name : ""; }
@@ -2295,7 +2295,7 @@ constexpr int step_form_index(const char* name) {
     return -1;
 }
 inline int pick_step(bool bf16) {
-    constexpr int kBf16 = step_form_index("bf16_step_rt_u8c4n8c2_p100_last");
+    constexpr int kBf16 = step_form_index("bf16_step_bal_u8c4");
     constexpr int kF32 = step_form_index("f32_step_sd_u8c4_p75");
     static_assert(kBf16 >= 0 && kF32 >= 0, "policy step forms");
     return bf16 ? kBf16 : kF32;
@@ -2530,7 +2530,6 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     FA_STB(8, 4, 8, 2, false)
     FA_STB(8, 4, 8, 4, false)
     FA_STB(8, 4, 8, 2, true)
-    FA_STB(8, 2, 8, 2, true)
     FA_STF(8, 4, 16, 1, false)
     FA_STF(8, 4, 16, 1, true)
 #undef FA_STB

@@ -24,7 +24,7 @@ T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 XI="python3 tools/exchange_interference.py"
 TAG=${TAG:-r05}
 COMMIT=${COMMIT:-unknown}
-S_BF="product,bf16_step_sd_u8c4w_p100_last,bf16_step_static_u8c4"
+S_BF="product,bf16_step_rt_u8c4n8c2_p100_last,bf16_step_static_u8c4"
 S_F32="product"
 C4R="--config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5 --no-cpu-baseline"
 recipe=${1:-}
