@@ -105,7 +105,9 @@ def test_probe_step_form_settles_records_and_stays_exact(bf16, monkeypatch):
     dev = torch.device("cuda", 0)
     agg = ShardedAggregator(one_launch="probe")
     assert ShardedAggregator().one_launch == "auto"
-    for P, rounds in ((300_001, 4), (65_536, 3)):
+    # shapes no other test uses: the cache file is shared by the session (conftest),
+    # and a record another test left for the same key would settle the probe early
+    for P, rounds in ((300_001, 4), (65_544, 3)):
         N, seed = 33, 9
         lay = SlotLayout(P, 1, rounds)
         Xin, w, sc, exp = _slots_input(bf16, N, P, seed, lay, dev)
