@@ -1,0 +1,238 @@
+// step_probe.hip -- the one-launch bf16 step kernel (k_fedavg_bf16_step,
+// csrc/fold_kernels.hpp) timed alone at a C4 rank's slots, beside variants of
+// its tile-dealing loop compiled in the same translation unit, so that a
+// question about the step's code costs one short compile and one GPU call
+// instead of a library build.  Every variant folds the same columns with the
+// same tile body, so every output bit must equal the first variant's.
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I include \
+//         -I fedlesscan_amd/csrc tools/step_probe.hip -o tools/step_probe.bin
+//   tools/step_probe.bin [reps]
+// Variants:
+//   lib_rt    the library kernel, round 4's policy table (rt_u8c4n8c2_p100_last)
+//   lib_bal   the library kernel, balanced rounds (the round-5 policy)
+//   r04_rt    round 4's tile-dealing loop (pass-barrier bookkeeping compiled in,
+//             disabled at run time; relaxed flag exchange), the same tile body
+//   lean_rt   the current loop with the tile lambda reduced to one call site
+#include "fold_kernels.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace {
+
+#define PCHECK(x)                                                                           \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+// round 4's loop (git bd08368), pass barriers never taken (sync_passes 0)
+template <class Tile>
+__device__ __forceinline__ void r04_step_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch,
+                                               int sync_passes, Tile tile) {
+    __shared__ unsigned int nxt[2];
+    const int64_t ntiles = T.seg_end[T.segs - 1];
+    const int64_t Ts = T.static_tiles;
+    const int64_t G = gridDim.x;
+    int p = 0;
+    int64_t t = blockIdx.x;
+    const int S = sync_passes;
+    if (t >= Ts) {
+        for (int i = 0; S && i < 32; ++i) __syncthreads();
+        if (threadIdx.x == 0) nxt[p] = atomicAdd(&sig[0], 1u);
+        __syncthreads();
+        t = Ts + nxt[p];
+        p ^= 1;
+    }
+    int g = 0;
+    while (g + 1 < T.segs && t >= T.seg_end[g]) ++g;
+    int k = T.round[g];
+    unsigned int cnt = 0;
+    while (t < ntiles) {
+        const bool dyn_next = t + G >= Ts;
+        unsigned int nx = 0;
+        if (dyn_next && threadIdx.x == 0) nx = atomicAdd(&sig[0], 1u);
+        tile(g, t - (g ? T.seg_end[g - 1] : 0));
+        ++cnt;
+        int64_t tn = t + G;
+        if (dyn_next) {
+            if (threadIdx.x == 0) nxt[p] = nx;
+            __syncthreads();
+            tn = Ts + nxt[p];
+            p ^= 1;
+        }
+        if (S && t < Ts) {  // never at run time: the bookkeeping round 4 compiled in
+            const int64_t jt = t / G;
+            if (tn < Ts) {
+                const int64_t jn = tn / G;
+                if (jn % S == 0) __syncthreads();
+            } else {
+                for (int64_t i = jt / S + 1; i <= 32; ++i) __syncthreads();
+            }
+        }
+        int gn = g;
+        while (gn < T.segs && tn >= T.seg_end[gn]) ++gn;
+        const int kn = gn < T.segs ? T.round[gn] : kMaxRounds;
+        if (kn != k) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned int nk = (unsigned int)T.round_tiles[k];
+                if (atomicAdd(&sig[kSigDone + k], cnt) + cnt == nk) {
+                    atomicExch(&sig[kSigDone + k], 0u);
+                    atomicExch(&sig[kSigFlag + k], epoch);
+                }
+            }
+            cnt = 0;
+            k = kn;
+        }
+        t = tn;
+        g = gn < T.segs ? gn : g;
+    }
+    if (threadIdx.x == 0) {
+        if (atomicAdd(&sig[1], 1u) == gridDim.x - 1) {
+            atomicExch(&sig[0], 0u);
+            atomicExch(&sig[1], 0u);
+        }
+    }
+}
+
+template <int UB, int CB, int US, int CS>
+__global__ __launch_bounds__(kBlock) void k_r04_step(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
+                                                     const float* __restrict__ a, float divisor,
+                                                     float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
+                                                     unsigned int* sig, unsigned int epoch, int sync_passes) {
+    r04_step_tiles(T, sig, epoch, sync_passes, [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        uint16_t* ob = outb ? outb + c0 : nullptr;
+        if (T.small[g])
+            bf16_tile<US, CS, false, kBlock>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0, ob);
+        else
+            bf16_tile<UB, CB, false, kBlock>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0, ob);
+    });
+}
+
+template <int UB, int CB, int US, int CS>
+__global__ __launch_bounds__(kBlock) void k_lean_step(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
+                                                      const float* __restrict__ a, float divisor,
+                                                      float* __restrict__ out, uint16_t* __restrict__ outb,
+                                                      StepTable T, unsigned int* sig, unsigned int epoch) {
+    step_tiles(T, sig, epoch, [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        uint16_t* ob = outb ? outb + c0 : nullptr;
+        if (T.small[g])
+            bf16_tile<US, CS, false, kBlock>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0, ob);
+        else
+            bf16_tile<UB, CB, false, kBlock>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0, ob);
+    });
+}
+
+__global__ void k_fill(uint16_t* X, int64_t n, uint64_t seed) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        X[i] = (uint16_t)(((z >> 8) & 0x8000u) | ((0x70u + ((z >> 20) & 0xFu)) << 7) | (z & 0x7Fu));
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 30;
+    const int64_t N = 256, rounds = 4;
+    const int64_t offs[5] = {0, 4934912, 4934912 + 3454464, 4934912 + 3454464 + 2418112,
+                             4934912 + 3454464 + 2418112 + 1692672};
+    const int64_t P = offs[4], ldx = P;
+    const int64_t grid = cu_count();
+    uint16_t *X, *outb;
+    float *a, *out;
+    unsigned int* sig;
+    PCHECK(hipMalloc(&X, (size_t)N * ldx * 2));
+    PCHECK(hipMalloc(&a, N * 4));
+    PCHECK(hipMalloc(&out, P * 4));
+    PCHECK(hipMalloc(&outb, P * 2));
+    PCHECK(hipMalloc(&sig, kSigWords * 4));
+    PCHECK(hipMemset(sig, 0, kSigWords * 4));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, X, N * ldx, 777ull);
+    std::vector<float> ha(N);
+    double tot = 0;
+    for (int64_t i = 0; i < N; ++i) tot += (ha[i] = (float)(1 + (i * 7919) % 97));
+    PCHECK(hipMemcpy(a, ha.data(), N * 4, hipMemcpyHostToDevice));
+    const float div = (float)tot;
+    StepTable Trt, Tbal;
+    if (build_step_table(kStepSpecs[step_form_index("bf16_step_rt_u8c4n8c2_p100_last")], (int)rounds, offs, ldx, grid,
+                         Trt) ||
+        build_step_table(kStepSpecs[step_form_index("bf16_step_bal_u8c4")], (int)rounds, offs, ldx, grid, Tbal)) {
+        fprintf(stderr, "step table: %s\n", g_err);
+        return 1;
+    }
+    hipStream_t st;
+    PCHECK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    PCHECK(hipEventCreate(&e0));
+    PCHECK(hipEventCreate(&e1));
+    unsigned int epoch = 0;
+    const double bytes = (double)N * P * 2 + (double)P * 6;
+    printf("C4 rank step: N %lld, P %lld in %lld rounds, grid %lld, %.3f GB per launch, %d reps\n", (long long)N,
+           (long long)P, (long long)rounds, (long long)grid, bytes / 1e9, reps);
+    struct V {
+        const char* name;
+        int which;
+    } vs[] = {{"lib_rt", 0}, {"r04_rt", 2}, {"lean_rt", 3}, {"lib_bal", 1},
+              {"lib_rt", 0}, {"r04_rt", 2}, {"lean_rt", 3}, {"lib_bal", 1}};
+    std::vector<uint32_t> ref(P), cur(P);
+    bool have = false;
+    for (const V& v : vs) {
+        auto launch = [&]() {
+            ++epoch;
+            const unsigned int g = (unsigned int)std::min<int64_t>(grid, (v.which == 1 ? Tbal : Trt).seg_end[
+                                                                             (v.which == 1 ? Tbal : Trt).segs - 1]);
+            switch (v.which) {
+                case 0:
+                    hipLaunchKernelGGL((k_fedavg_bf16_step<8, 4, 8, 2, false, kBlock, false>), dim3(g), dim3(kBlock),
+                                       0, st, X, N, ldx, a, nullptr, div, out, outb, Trt, sig, epoch);
+                    break;
+                case 1:
+                    hipLaunchKernelGGL((k_fedavg_bf16_step<8, 4, 8, 2, false, kBlock, true>), dim3(g), dim3(kBlock),
+                                       0, st, X, N, ldx, a, nullptr, div, out, outb, Tbal, sig, epoch);
+                    break;
+                case 2:
+                    hipLaunchKernelGGL((k_r04_step<8, 4, 8, 2>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
+                                       outb, Trt, sig, epoch, 0);
+                    break;
+                default:
+                    hipLaunchKernelGGL((k_lean_step<8, 4, 8, 2>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div,
+                                       out, outb, Trt, sig, epoch);
+            }
+        };
+        PCHECK(hipMemsetAsync(out, 0xFF, P * 4, st));
+        launch();
+        PCHECK(hipGetLastError());
+        PCHECK(hipStreamSynchronize(st));
+        PCHECK(hipMemcpy(have ? cur.data() : ref.data(), out, P * 4, hipMemcpyDeviceToHost));
+        const bool same = !have || memcmp(ref.data(), cur.data(), P * 4) == 0;
+        have = true;
+        std::vector<float> ms;
+        for (int r = 0; r < reps; ++r) {
+            PCHECK(hipEventRecord(e0, st));
+            launch();
+            PCHECK(hipEventRecord(e1, st));
+            PCHECK(hipEventSynchronize(e1));
+            float t;
+            PCHECK(hipEventElapsedTime(&t, e0, e1));
+            ms.push_back(t);
+        }
+        std::sort(ms.begin(), ms.end());
+        printf("%-8s median %.4f ms (min %.4f)  %.1f GB/s  bits %s\n", v.name, ms[ms.size() / 2], ms[0],
+               bytes / ms[ms.size() / 2] / 1e6, same ? "same" : "DIFFER");
+        fflush(stdout);
+    }
+    return 0;
+}
