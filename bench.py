@@ -211,6 +211,23 @@ def rank_devices(dev) -> list:
     return out
 
 
+def model_digest(bits: torch.Tensor, chunk: int = 1 << 24) -> torch.Tensor:
+    """Two int64 digests of a model's bit patterns (an int16 or int32 view):
+    their sum and a position-weighted sum (weights 1..1021, cycling), both
+    modulo 2^64 -- integer sums wrap, so the order of the reduction does not
+    matter and every rank computes the same digests for the same bits.  Used
+    by gather_check: equal digests on every rank = one model on every rank."""
+    mask = (1 << (8 * bits.element_size())) - 1
+    flat = bits.reshape(-1)
+    s = torch.zeros(2, dtype=torch.int64, device=bits.device)
+    for lo in range(0, flat.numel(), chunk):
+        x = flat[lo:lo + chunk].to(torch.int64) & mask
+        w = torch.arange(lo, lo + x.numel(), dtype=torch.int64, device=bits.device) % 1021 + 1
+        s[0] += x.sum()
+        s[1] += (x * w).sum()
+    return s
+
+
 class Workload:
     """This rank's share of the synthetic round: its parameter slots, all clients.
 
@@ -655,15 +672,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         gather_ok = bool(t.item())
         del peer_full
-    elif dist_on:  # my slots inside the reassembled model must be my fold output, bit for bit
+    elif dist_on:
+        # the whole reassembled model: my slots in my copy are my fold output,
+        # bit for bit, and every rank's copy is the same model (two position-
+        # weighted digests of its bits agree on all ranks), so every rank's
+        # slots are right in every copy
         ok = True
         iv = torch.int32 if wl.dtype == "f32" else torch.int16
         for k, (lo, hi) in enumerate(wl.slots):
             if hi > lo:
                 ok &= torch.equal(full[lo:hi].view(iv), send[lay.offset(k):lay.offset(k) + hi - lo].view(iv))
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        gather_ok = bool(t.item())
+        dig = model_digest(full.view(iv))
+        t = torch.cat([torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev), dig, -dig])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)  # own-slot flags; digests' min and -max
+        gather_ok = bool(t[0].item() == 1 and torch.equal(t[1:3], -t[3:5]))
     if dist_on and one_launch:
         # one fold launch per step: its span (events around it), and the
         # exchange left exposed after it (from the launch's end to the step's)

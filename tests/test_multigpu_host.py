@@ -166,3 +166,24 @@ def test_bench_step_mode_flags(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--step-mode", "sometimes"])
     with pytest.raises(SystemExit):
         bench.parse()
+
+
+def test_model_digest_separates_models():
+    """gather_check's digests: the same bits give the same pair on every rank
+    (chunking and reduction order do not change them); a flipped bit, two
+    swapped elements or a shifted slot give another pair."""
+    import torch
+
+    import bench
+    g = torch.Generator().manual_seed(5)
+    for dt in (torch.int32, torch.int16):
+        bits = torch.randint(-(1 << 15), 1 << 15, (100_003,), generator=g).to(dt)
+        d = bench.model_digest(bits)
+        assert torch.equal(d, bench.model_digest(bits.clone(), chunk=4099))
+        flipped = bits.clone()
+        flipped[777] ^= 1
+        swapped = bits.clone()
+        swapped[[10, 90_000]] = bits[[90_000, 10]]
+        shifted = torch.roll(bits, 64)
+        for other in (flipped, swapped, shifted):
+            assert not torch.equal(d, bench.model_digest(other))
