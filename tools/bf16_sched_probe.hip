@@ -46,6 +46,11 @@ __device__ __forceinline__ void unpack(u32x4 w, f32x4& e, f32x4& o) {
     o = __builtin_bit_cast(f32x4, w & 0xFFFF0000u);
 }
 __device__ __forceinline__ u32x4 ld(const u32x4* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f != f) return (u >> 16) | 0x40u;
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
 
 template <int C>
 __device__ __forceinline__ void add_row(f32x4 (&ev)[C], f32x4 (&od)[C], const u32x4 (&v)[C], float ai) {
@@ -58,11 +63,12 @@ __device__ __forceinline__ void add_row(f32x4 (&ev)[C], f32x4 (&od)[C], const u3
     }
 }
 
-enum { GRP = 0, GRPB = 1, ROLL = 2, DBL = 3, CHUNK = 4 };
+enum { GRP = 0, GRPB = 1, ROLL = 2, DBL = 3, CHUNK = 4, OUTB = 16 };  // OUTB: also the RNE bf16 copy
 
 template <int U, int C, int MODE, int G = 0>
 __device__ __forceinline__ void fold(const u32x4* __restrict__ p, int64_t ldo, int64_t N, const float* __restrict__ a,
-                                     float div, float* __restrict__ out, int64_t o0) {
+                                     float div, float* __restrict__ out, int64_t o0, uint16_t* __restrict__ outb) {
+    constexpr int M = MODE & 15;
     f32x4 ev[C], od[C];
     {
         const float a0 = a[0];
@@ -75,18 +81,18 @@ __device__ __forceinline__ void fold(const u32x4* __restrict__ p, int64_t ldo, i
         }
     }
     int64_t i = 1;
-    if constexpr (MODE == GRP || MODE == GRPB) {
+    if constexpr (M == GRP || M == GRPB) {
         for (; i + U <= N; i += U) {
             u32x4 v[U][C];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int c = 0; c < C; ++c) v[u][c] = ld(p + (i + u) * ldo + c * kB);
-            if constexpr (MODE == GRPB) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (M == GRPB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < U; ++u) add_row<C>(ev, od, v[u], a[i + u]);
         }
-    } else if constexpr (MODE == ROLL) {
+    } else if constexpr (M == ROLL) {
         // ring of U rows: rows i .. i+U-1 in flight on entry of each group
         if (N - 1 >= 2 * U) {
             u32x4 v[U][C];
@@ -110,7 +116,7 @@ __device__ __forceinline__ void fold(const u32x4* __restrict__ p, int64_t ldo, i
             for (int u = 0; u < U; ++u) add_row<C>(ev, od, v[u], a[i + u]);
             i += U;
         }
-    } else if constexpr (MODE == CHUNK) {
+    } else if constexpr (M == CHUNK) {
         static_assert(G % U == 0 && G >= 2 * U, "chunk of whole rings");
         for (; i + G <= N; i += G) {
             u32x4 v[U][C];
@@ -179,6 +185,14 @@ __device__ __forceinline__ void fold(const u32x4* __restrict__ p, int64_t ldo, i
         f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * (o0 + (int64_t)c * kB);
         __builtin_nontemporal_store(f32x4{e.x, o.x, e.y, o.y}, o4);
         __builtin_nontemporal_store(f32x4{e.z, o.z, e.w, o.w}, o4 + 1);
+        if constexpr ((MODE & OUTB) != 0) {
+            u32x4 b;
+            b.x = f2bf(e.x) | (f2bf(o.x) << 16);
+            b.y = f2bf(e.y) | (f2bf(o.y) << 16);
+            b.z = f2bf(e.z) | (f2bf(o.z) << 16);
+            b.w = f2bf(e.w) | (f2bf(o.w) << 16);
+            __builtin_nontemporal_store(b, reinterpret_cast<u32x4*>(outb) + o0 + (int64_t)c * kB);
+        }
     }
 }
 
@@ -186,12 +200,12 @@ __device__ __forceinline__ void fold(const u32x4* __restrict__ p, int64_t ldo, i
 template <int U, int C, int MODE, int WPE, int G = 0>
 __global__ __launch_bounds__(kB, WPE) void k_probe(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
                                                    const float* __restrict__ a, float div, float* __restrict__ out,
-                                                   int64_t ntiles) {
+                                                   int64_t ntiles, uint16_t* __restrict__ outb) {
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
     const int64_t ldo = ldx >> 3;
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t o0 = t * (kB * C) + threadIdx.x;
-        fold<U, C, MODE, G>(X8 + o0, ldo, N, a, div, out, o0);
+        fold<U, C, MODE, G>(X8 + o0, ldo, N, a, div, out, o0, outb);
     }
 }
 
@@ -210,27 +224,36 @@ struct Variant {
     const char* name;
     int C;
     int per_cu;  // blocks per CU in the grid
-    void (*launch)(dim3, hipStream_t, const uint16_t*, int64_t, int64_t, const float*, float, float*, int64_t);
+    void (*launch)(dim3, hipStream_t, const uint16_t*, int64_t, int64_t, const float*, float, float*, int64_t,
+                   uint16_t*);
+    int bands = 1;  // launches over contiguous column bands (the library's band forms)
 };
 
 template <int U, int C, int MODE, int WPE, int G = 0>
 void launch_v(dim3 g, hipStream_t st, const uint16_t* X, int64_t N, int64_t ldx, const float* a, float div, float* out,
-              int64_t nt) {
-    hipLaunchKernelGGL((k_probe<U, C, MODE, WPE, G>), g, dim3(kB), 0, st, X, N, ldx, a, div, out, nt);
+              int64_t nt, uint16_t* outb) {
+    hipLaunchKernelGGL((k_probe<U, C, MODE, WPE, G>), g, dim3(kB), 0, st, X, N, ldx, a, div, out, nt, outb);
 }
 
-#define V(name, U, C, MODE, PER) {name, C, PER, launch_v<U, C, MODE, PER>}
-#define VC(name, U, C, G, PER) {name, C, PER, launch_v<U, C, CHUNK, PER, G>}
+#define V(name, U, C, MODE, PER, NB) {name, C, PER, launch_v<U, C, MODE, PER>, NB}
+#define VC(name, U, C, G, PER, NB) {name, C, PER, launch_v<U, C, CHUNK | OUTB, PER, G>, NB}
+// _ob: the RNE bf16 copy stored too (as the library); _bN: N launches over
+// contiguous column bands (the library's band forms: bands of <= 4 passes)
 static const Variant kVariants[] = {
-    V("grp_u8c4", 8, 4, GRP, 1),     V("grpb_u8c4", 8, 4, GRPB, 1),  V("roll_u8c4", 8, 4, ROLL, 1),
-    V("roll_u4c4", 4, 4, ROLL, 1),   V("roll_u6c4", 6, 4, ROLL, 1),  V("dbl_u4c4", 4, 4, DBL, 1),
-    V("grp_u8c2", 8, 2, GRP, 1),     V("roll_u8c2", 8, 2, ROLL, 1),  V("roll_u16c2", 16, 2, ROLL, 1),
-    V("dbl_u8c2", 8, 2, DBL, 1),     V("grp_u4c4_x2", 4, 4, GRP, 2), V("roll_u4c4_x2", 4, 4, ROLL, 2),
-    V("roll_u8c2_x2", 8, 2, ROLL, 2),
-    VC("chunk32_r8c4", 8, 4, 32, 1), VC("chunk32_r6c4", 6, 4, 36, 1), VC("chunk32_r4c4", 4, 4, 32, 1),
-    VC("chunk64_r4c4", 4, 4, 64, 1), VC("chunk32_r8c2", 8, 2, 32, 1), VC("chunk64_r8c2", 8, 2, 64, 1),
-    VC("chunk64_r12c2", 12, 2, 60, 1), VC("chunk32_r4c4_x2", 4, 4, 32, 2), VC("chunk64_r8c2_x2", 8, 2, 64, 2),
-    V("grp_u8c4", 8, 4, GRP, 1),
+    V("grp_u8c4", 8, 4, GRP, 1, 1),
+    V("grp_u8c4_ob", 8, 4, GRP | OUTB, 1, 1),
+    V("grp_u8c4_ob_b2", 8, 4, GRP | OUTB, 1, 2),
+    V("grp_u8c2_ob_b3", 8, 2, GRP | OUTB, 1, 3),
+    V("grp_u8c2_ob", 8, 2, GRP | OUTB, 1, 1),
+    V("roll_u8c4_ob", 8, 4, ROLL | OUTB, 1, 1),
+    V("roll_u8c4_ob_b2", 8, 4, ROLL | OUTB, 1, 2),
+    VC("chunk64_r4c4_ob", 4, 4, 64, 1, 1),
+    VC("chunk64_r4c4_ob_b2", 4, 4, 64, 1, 2),
+    V("grp_u4c4_x2_ob", 4, 4, GRP | OUTB, 2, 1),
+    V("grp_u8c4_ob_b3", 8, 4, GRP | OUTB, 1, 3),
+    V("grp_u8c4", 8, 4, GRP, 1, 1),
+    V("grp_u8c4_ob_b2", 8, 4, GRP | OUTB, 1, 2),
+    V("grp_u8c2_ob_b3", 8, 2, GRP | OUTB, 1, 3),
 };
 
 int main(int argc, char** argv) {
@@ -244,10 +267,12 @@ int main(int argc, char** argv) {
     const int cus = prop.multiProcessorCount;
     uint16_t* X;
     float *a, *out, *ref;
+    uint16_t* outb;
     CHECK(hipMalloc(&X, (size_t)N * ldx * 2));
     CHECK(hipMalloc(&a, N * 4));
     CHECK(hipMalloc(&out, P * 4));
     CHECK(hipMalloc(&ref, P * 4));
+    CHECK(hipMalloc(&outb, P * 2));
     hipLaunchKernelGGL(k_synth, dim3(4096), dim3(256), 0, 0, X, N * ldx, 12345ull);
     std::vector<float> ha(N);
     double tot = 0;
@@ -259,17 +284,26 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const double bytes = (double)N * P * 2 + (double)P * 4;
+    const double bytes = (double)N * P * 2 + (double)P * 6;  // the f32 result and its bf16 copy
     printf("N %lld P %lld (%.3f GB per launch), %d CUs, %d reps\n", (long long)N, (long long)P, bytes / 1e9, cus, reps);
     std::vector<uint32_t> h0(P), h1(P);
     bool have_ref = false;
     for (const Variant& v : kVariants) {
-        const int64_t ntiles = P / 8 / (kB * v.C);
-        const int64_t slots = (int64_t)cus * v.per_cu;
-        const int64_t passes = (ntiles + slots - 1) / slots;
-        const int64_t grid = (ntiles + passes - 1) / passes;  // balanced passes
+        const int64_t to = (int64_t)kB * v.C;                  // octets per tile
+        const int64_t tiles = P / 8 / to;
+        const int64_t band_tiles = (tiles + v.bands - 1) / v.bands;
+        auto launch = [&]() {
+            for (int64_t t0 = 0; t0 < tiles; t0 += band_tiles) {
+                const int64_t nt = std::min(band_tiles, tiles - t0);
+                const int64_t slots = (int64_t)cus * v.per_cu;
+                const int64_t passes = (nt + slots - 1) / slots;
+                const int64_t grid = (nt + passes - 1) / passes;  // balanced passes
+                const int64_t c0 = t0 * to * 8;                    // first column of the band
+                v.launch(dim3((unsigned)grid), st, X + c0, N, ldx, a, div, out + c0, nt, outb + c0);
+            }
+        };
         CHECK(hipMemsetAsync(out, 0xFF, P * 4, st));
-        v.launch(dim3((unsigned)grid), st, X, N, ldx, a, div, out, ntiles);  // untimed
+        launch();  // untimed
         CHECK(hipGetLastError());
         CHECK(hipStreamSynchronize(st));
         CHECK(hipMemcpy(have_ref ? h1.data() : h0.data(), out, P * 4, hipMemcpyDeviceToHost));
@@ -279,7 +313,7 @@ int main(int argc, char** argv) {
         std::vector<float> ms;
         for (int r = 0; r < reps; ++r) {
             CHECK(hipEventRecord(e0, st));
-            v.launch(dim3((unsigned)grid), st, X, N, ldx, a, div, out, ntiles);
+            launch();
             CHECK(hipEventRecord(e1, st));
             CHECK(hipEventSynchronize(e1));
             float t;
@@ -288,8 +322,8 @@ int main(int argc, char** argv) {
         }
         std::sort(ms.begin(), ms.end());
         const float med = ms[ms.size() / 2];
-        printf("%-14s grid %5lld (%lld passes): median %.4f ms (min %.4f)  %.1f GB/s  bits %s\n", v.name,
-               (long long)grid, (long long)passes, med, ms[0], bytes / med / 1e6, same ? "same" : "DIFFER");
+        printf("%-20s %d band(s): median %.4f ms (min %.4f)  %.1f GB/s  bits %s\n", v.name, v.bands, med, ms[0],
+               bytes / med / 1e6, same ? "same" : "DIFFER");
         fflush(stdout);
     }
     return 0;
