@@ -13,6 +13,13 @@
 //   r04_rt    round 4's tile-dealing loop (pass-barrier bookkeeping compiled in,
 //             disabled at run time; relaxed flag exchange), the same tile body
 //   lean_rt   the current loop with the tile lambda reduced to one call site
+//   bal_nopub the balanced loop with its per-round publication compiled out
+//             (no drain, barrier, write-back or count: timing only)
+//   static    every tile static, block b folding b, b + G, ... across the
+//             rounds (bf16_step_static_u8c4's table)
+//   perround  the rounds as 4 separate balanced grid-stride launches
+//             (launch_bf16_gs, per_cu -1: what per-round launches run)
+//   whole     the step's columns as ONE balanced grid-stride launch
 #include "fold_kernels.hpp"
 
 #include <algorithm>
@@ -132,6 +139,43 @@ __global__ __launch_bounds__(kBlock) void k_lean_step(const uint16_t* __restrict
     });
 }
 
+// step_tiles_bal with the per-round publication optional (PUB false: timing only)
+template <bool PUB, class Wide>
+__device__ __forceinline__ void bal_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Wide wide) {
+    const int64_t b = blockIdx.x;
+    const int64_t Ts = T.static_tiles;
+    int k = -1;
+    unsigned int cnt = 0;
+    for (int g = 0; g < T.segs; ++g) {
+        const int64_t lo = g ? T.seg_end[g - 1] : 0;
+        if (lo >= Ts) break;
+        if (T.round[g] != k) {
+            if (PUB && k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
+            k = T.round[g];
+            cnt = 0;
+        }
+        const int64_t n = T.seg_end[g] - lo, S = T.stride[g];
+        for (int64_t i = b; b < S && i < n; i += S) {
+            wide(g, i);
+            ++cnt;
+        }
+    }
+    if (PUB && k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
+    if (PUB) step_reset(sig);
+}
+
+template <bool PUB>
+__global__ __launch_bounds__(kBlock) void k_bal_step(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
+                                                     const float* __restrict__ a, float divisor,
+                                                     float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
+                                                     unsigned int* sig, unsigned int epoch) {
+    bal_tiles<PUB>(T, sig, epoch, [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        bf16_tile<8, 4, false, kBlock>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0,
+                                       outb ? outb + c0 : nullptr);
+    });
+}
+
 __global__ void k_fill(uint16_t* X, int64_t n, uint64_t seed) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -166,10 +210,11 @@ int main(int argc, char** argv) {
     for (int64_t i = 0; i < N; ++i) tot += (ha[i] = (float)(1 + (i * 7919) % 97));
     PCHECK(hipMemcpy(a, ha.data(), N * 4, hipMemcpyHostToDevice));
     const float div = (float)tot;
-    StepTable Trt, Tbal;
+    StepTable Trt, Tbal, Tst;
     if (build_step_table(kStepSpecs[step_form_index("bf16_step_rt_u8c4n8c2_p100_last")], (int)rounds, offs, ldx, grid,
                          Trt) ||
-        build_step_table(kStepSpecs[step_form_index("bf16_step_bal_u8c4")], (int)rounds, offs, ldx, grid, Tbal)) {
+        build_step_table(kStepSpecs[step_form_index("bf16_step_bal_u8c4")], (int)rounds, offs, ldx, grid, Tbal) ||
+        build_step_table(kStepSpecs[step_form_index("bf16_step_static_u8c4")], (int)rounds, offs, ldx, grid, Tst)) {
         fprintf(stderr, "step table: %s\n", g_err);
         return 1;
     }
@@ -185,15 +230,15 @@ int main(int argc, char** argv) {
     struct V {
         const char* name;
         int which;
-    } vs[] = {{"lib_rt", 0}, {"r04_rt", 2}, {"lean_rt", 3}, {"lib_bal", 1},
-              {"lib_rt", 0}, {"r04_rt", 2}, {"lean_rt", 3}, {"lib_bal", 1}};
+    } vs[] = {{"lib_bal", 1}, {"bal_nopub", 4}, {"static", 5}, {"perround", 6}, {"whole", 7}, {"lib_rt", 0},
+              {"lib_bal", 1}, {"bal_nopub", 4}, {"static", 5}, {"perround", 6}, {"whole", 7}, {"lib_rt", 0}};
     std::vector<uint32_t> ref(P), cur(P);
     bool have = false;
     for (const V& v : vs) {
         auto launch = [&]() {
             ++epoch;
-            const unsigned int g = (unsigned int)std::min<int64_t>(grid, (v.which == 1 ? Tbal : Trt).seg_end[
-                                                                             (v.which == 1 ? Tbal : Trt).segs - 1]);
+            const StepTable& Tv = v.which == 1 || v.which == 4 ? Tbal : v.which == 5 ? Tst : Trt;
+            const unsigned int g = (unsigned int)std::min<int64_t>(grid, Tv.seg_end[Tv.segs - 1]);
             switch (v.which) {
                 case 0:
                     hipLaunchKernelGGL((k_fedavg_bf16_step<8, 4, 8, 2, false, kBlock, false>), dim3(g), dim3(kBlock),
@@ -207,9 +252,25 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_r04_step<8, 4, 8, 2>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
                                        outb, Trt, sig, epoch, 0);
                     break;
-                default:
+                case 3:
                     hipLaunchKernelGGL((k_lean_step<8, 4, 8, 2>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div,
                                        out, outb, Trt, sig, epoch);
+                    break;
+                case 4:
+                    hipLaunchKernelGGL((k_bal_step<false>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
+                                       outb, Tbal, sig, epoch);
+                    break;
+                case 5:
+                    hipLaunchKernelGGL((k_fedavg_bf16_step<8, 4, 8, 4, false, kBlock, false>), dim3(g), dim3(kBlock),
+                                       0, st, X, N, ldx, a, nullptr, div, out, outb, Tst, sig, epoch);
+                    break;
+                case 6:
+                    for (int k = 0; k < rounds; ++k)
+                        launch_bf16_gs<8, 4>(st, -1, X + offs[k], N, offs[k + 1] - offs[k], ldx, a, nullptr, div,
+                                             out + offs[k], outb + offs[k]);
+                    break;
+                default:
+                    launch_bf16_gs<8, 4>(st, -1, X, N, P, ldx, a, nullptr, div, out, outb);
             }
         };
         PCHECK(hipMemsetAsync(out, 0xFF, P * 4, st));
