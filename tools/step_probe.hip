@@ -20,6 +20,12 @@
 //   perround  the rounds as 4 separate balanced grid-stride launches
 //             (launch_bf16_gs, per_cu -1: what per-round launches run)
 //   whole     the step's columns as ONE balanced grid-stride launch
+//   bal_nofence  the balanced loop publishing without the per-block release
+//             fence (plain stores: NOT a valid hand-off, timing only)
+//   bal_sc1   the balanced loop with write-through (sc1) 16-B output stores and
+//             no per-block release fence: every storing wave's vmcnt(0), a
+//             barrier, the count; the completing block acquires and raises
+//             the flag with a release store (MI355X_MICROARCH.md, valid forms)
 #include "fold_kernels.hpp"
 
 #include <algorithm>
@@ -139,6 +145,131 @@ __global__ __launch_bounds__(kBlock) void k_lean_step(const uint16_t* __restrict
     });
 }
 
+// a 16-B write-through store (sc1: the line leaves the XCD's L2 for memory)
+__device__ __forceinline__ void st16_sc1(void* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// bf16_tile / fold_octets (csrc/fold_kernels.hpp) with the output stores
+// chosen: SC1 write-through, else non-temporal.  Unscored.
+template <int U, int C, bool SC1>
+__device__ __forceinline__ void fold_octets_st(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
+                                               const float* __restrict__ a, float divisor, float* __restrict__ out,
+                                               uint16_t* __restrict__ outb, int64_t o0) {
+    f32x4 ev[C], od[C];
+    {
+        const float a0 = a[0];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + c * kBlock), e, o);
+            ev[c] = term4<false>(e, a0, 1.0f);
+            od[c] = term4<false>(o, a0, 1.0f);
+        }
+    }
+    int64_t i = 1;
+    for (; i + U <= N; i += U) {
+        u32x4 v[U][C];
+        octets_ld<U, C>(v, p, i, ldo);
+        octets_add<U, C, false>(ev, od, v, a, nullptr, i);
+    }
+    for (; i < N; ++i) {
+        const float ai = a[i];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            f32x4 e, o;
+            unpack_bf16x8(__builtin_nontemporal_load(p + i * ldo + c * kBlock), e, o);
+            ev[c] = add4(ev[c], term4<false>(e, ai, 1.0f));
+            od[c] = add4(od[c], term4<false>(o, ai, 1.0f));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
+        const int64_t oc = o0 + (int64_t)c * kBlock;
+        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
+        const u32x4 lo = __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y});
+        const u32x4 hi = __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w});
+        u32x4 b;
+        b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
+        b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
+        b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
+        b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
+        if constexpr (SC1) {
+            st16_sc1(o4, lo);
+            st16_sc1(o4 + 1, hi);
+            st16_sc1(reinterpret_cast<u32x4*>(outb) + oc, b);
+        } else {
+            st16(o4, lo);
+            st16(o4 + 1, hi);
+            st16(reinterpret_cast<u32x4*>(outb) + oc, b);
+        }
+    }
+}
+
+template <int U, int C, bool SC1>
+__device__ __forceinline__ void bf16_tile_st(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
+                                             int64_t ldx, const float* __restrict__ a, float divisor,
+                                             float* __restrict__ out, uint16_t* __restrict__ outb) {
+    const int64_t no = P >> 3, ldo = ldx >> 3;  // P % 8 == 0 here (64-aligned slots)
+    const int64_t o0 = bid * (kBlock * C) + threadIdx.x;
+    const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
+    if (o0 + (int64_t)(C - 1) * kBlock < no) {
+        fold_octets_st<U, C, SC1>(X8 + o0, ldo, N, a, divisor, out, outb, o0);
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int64_t o = o0 + (int64_t)c * kBlock;
+        if (o < no) fold_octets_st<U, 1, SC1>(X8 + o, ldo, N, a, divisor, out, outb, o);
+    }
+}
+
+// the round's publication without the per-block release fence: every storing
+// wave drained, a barrier, one lane counts; the completing block acquires and
+// raises the flag with a release store
+__device__ __forceinline__ void publish_nofence(const StepTable& T, unsigned int* sig, unsigned int epoch, int k,
+                                                unsigned int cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned int nk = (unsigned int)T.round_tiles[k];
+        if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cnt ==
+            nk) {
+            __hip_atomic_store(&sig[kSigDone + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(&sig[kSigFlag + k], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <bool SC1>
+__global__ __launch_bounds__(kBlock) void k_bal_nofence(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
+                                                        const float* __restrict__ a, float divisor,
+                                                        float* __restrict__ out, uint16_t* __restrict__ outb,
+                                                        StepTable T, unsigned int* sig, unsigned int epoch) {
+    const int64_t b = blockIdx.x;
+    int k = -1;
+    unsigned int cnt = 0;
+    for (int g = 0; g < T.segs; ++g) {
+        const int64_t lo = g ? T.seg_end[g - 1] : 0;
+        if (lo >= T.static_tiles) break;
+        if (T.round[g] != k) {
+            if (k >= 0 && cnt) publish_nofence(T, sig, epoch, k, cnt);
+            k = T.round[g];
+            cnt = 0;
+        }
+        const int64_t n = T.seg_end[g] - lo, S = T.stride[g];
+        const int64_t c0 = T.col0[g];
+        for (int64_t i = b; b < S && i < n; i += S) {
+            bf16_tile_st<8, 4, SC1>(i, X + c0, N, T.width[g], ldx, a, divisor, out + c0, outb + c0);
+            ++cnt;
+        }
+    }
+    if (k >= 0 && cnt) publish_nofence(T, sig, epoch, k, cnt);
+    step_reset(sig);
+}
+
 // step_tiles_bal with the per-round publication optional (PUB false: timing only)
 template <bool PUB, class Wide>
 __device__ __forceinline__ void bal_tiles(const StepTable& T, unsigned int* sig, unsigned int epoch, Wide wide) {
@@ -230,14 +361,15 @@ int main(int argc, char** argv) {
     struct V {
         const char* name;
         int which;
-    } vs[] = {{"lib_bal", 1}, {"bal_nopub", 4}, {"static", 5}, {"perround", 6}, {"whole", 7}, {"lib_rt", 0},
-              {"lib_bal", 1}, {"bal_nopub", 4}, {"static", 5}, {"perround", 6}, {"whole", 7}, {"lib_rt", 0}};
+    } vs[] = {{"lib_bal", 1}, {"bal_nopub", 4}, {"bal_nofence", 8}, {"bal_sc1", 9}, {"perround", 6},
+              {"lib_bal", 1}, {"bal_nopub", 4}, {"bal_nofence", 8}, {"bal_sc1", 9}, {"perround", 6},
+              {"lib_bal", 1}, {"bal_sc1", 9}};
     std::vector<uint32_t> ref(P), cur(P);
     bool have = false;
     for (const V& v : vs) {
         auto launch = [&]() {
             ++epoch;
-            const StepTable& Tv = v.which == 1 || v.which == 4 ? Tbal : v.which == 5 ? Tst : Trt;
+            const StepTable& Tv = v.which == 1 || v.which == 4 || v.which >= 8 ? Tbal : v.which == 5 ? Tst : Trt;
             const unsigned int g = (unsigned int)std::min<int64_t>(grid, Tv.seg_end[Tv.segs - 1]);
             switch (v.which) {
                 case 0:
@@ -263,6 +395,14 @@ int main(int argc, char** argv) {
                 case 5:
                     hipLaunchKernelGGL((k_fedavg_bf16_step<8, 4, 8, 4, false, kBlock, false>), dim3(g), dim3(kBlock),
                                        0, st, X, N, ldx, a, nullptr, div, out, outb, Tst, sig, epoch);
+                    break;
+                case 8:
+                    hipLaunchKernelGGL((k_bal_nofence<false>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
+                                       outb, Tbal, sig, epoch);
+                    break;
+                case 9:
+                    hipLaunchKernelGGL((k_bal_nofence<true>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
+                                       outb, Tbal, sig, epoch);
                     break;
                 case 6:
                     for (int k = 0; k < rounds; ++k)
