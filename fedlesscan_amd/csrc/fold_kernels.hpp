@@ -1335,6 +1335,25 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
 // A 16-byte non-temporal output store
 __device__ __forceinline__ void st16(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
+// Write-through (sc1) 16-byte stores for the one-launch step (round 5): the
+// line goes to memory, not only the XCD's L2, so a block that publishes a
+// round needs no L2 write-back (an agent release fence per block and round
+// cost the C4 rank step 3.5 %, tools/step_probe.hip).  A raw buffer store
+// over a wave-uniform base (the tile's first octet: readfirstlane of a value
+// every lane shares) with a small per-lane offset; cache-policy operand 16 =
+// sc1 on gfx950.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, int byte_off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+}
+
 // One row group of U rows x C octets: loaded (ld) and folded in row order (add)
 template <int U, int C>
 __device__ __forceinline__ void octets_ld(u32x4 (&v)[U][C], const u32x4* __restrict__ p, int64_t i, int64_t ldo) {
@@ -1359,7 +1378,7 @@ __device__ __forceinline__ void octets_add(f32x4 (&ev)[C], f32x4 (&od)[C], const
     }
 }
 
-template <int U, int C, bool SCORED, int B = kBlock>
+template <int U, int C, bool SCORED, int B = kBlock, bool WT = false>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -1394,27 +1413,39 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
             od[c] = add4(od[c], term4<SCORED>(o, ai, si));
         }
     }
+    // WT: the stores' base is the first octet of the lane's tile, shared by
+    // every lane (o0 - threadIdx.x), so the per-lane offsets stay small
+    const int64_t ob = WT ? uniform64(o0 - (int64_t)threadIdx.x) : 0;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
         const int64_t oc = o0 + (int64_t)c * B;
-        f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
-        st16(o4, __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y}));
-        st16(o4 + 1, __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w}));
+        const u32x4 lo = __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y});
+        const u32x4 hi = __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w});
+        if constexpr (WT) {
+            const __amdgpu_buffer_rsrc_t r = wt_rsrc(out + 8 * ob);
+            st16_wt(r, (int)(32 * (oc - ob)), lo);
+            st16_wt(r, (int)(32 * (oc - ob)) + 16, hi);
+        } else {
+            f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
+            st16(o4, lo);
+            st16(o4 + 1, hi);
+        }
         if (outb) {
             u32x4 b;
             b.x = (uint32_t)f2bf_rne(e.x) | ((uint32_t)f2bf_rne(o.x) << 16);
             b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
             b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
             b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
-            st16(reinterpret_cast<u32x4*>(outb) + oc, b);
+            if constexpr (WT) st16_wt(wt_rsrc(outb + 8 * ob), (int)(16 * (oc - ob)), b);
+            else st16(reinterpret_cast<u32x4*>(outb) + oc, b);
         }
     }
 }
 
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
-template <int U, int C, bool SCORED, int B = kBlock>
+template <int U, int C, bool SCORED, int B = kBlock, bool WT = false>
 __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
@@ -1423,13 +1454,13 @@ __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restric
     const int64_t o0 = bid * (B * C) + threadIdx.x;
     const u32x4* X8 = reinterpret_cast<const u32x4*>(X);
     if (o0 + (int64_t)(C - 1) * B < no) {
-        fold_octets<U, C, SCORED, B>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
+        fold_octets<U, C, SCORED, B, WT>(X8 + o0, ldo, N, a, s, divisor, out, outb, o0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int64_t o = o0 + (int64_t)c * B;
-        if (o < no) fold_octets<U, 1, SCORED, B>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
+        if (o < no) fold_octets<U, 1, SCORED, B, WT>(X8 + o, ldo, N, a, s, divisor, out, outb, o);
     }
     const int64_t tb = no / (B * C), tl = (no % (B * C)) % B;
     if ((P & 7) && bid == tb && (int64_t)threadIdx.x == tl) {
@@ -1441,6 +1472,8 @@ __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restric
             out[col] = acc;
             if (outb) outb[col] = f2bf_rne(acc);
         }
+        // WT: these few plain stores are written back before the block publishes
+        if constexpr (WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
 }
 
@@ -1508,6 +1541,7 @@ struct StepTable {
     int32_t segs;
     int32_t rounds;
     int32_t sys;    // publish the rounds at system scope: other GPUs read them (fa_peers, the peer exchange)
+    int32_t wt;     // the tiles' output stores are write-through (bf16 steps): no per-block L2 write-back
     int64_t stride[kMaxSegs];  // balanced rounds (step_tiles_bal): static segment g dealt over stride[g] blocks
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
@@ -1527,15 +1561,22 @@ constexpr int kStatusWords = kMaxRounds + 1;  // a timeout record per round + th
 // nothing measurable (1.044 ms per C4 rank step with and without it, one box,
 // profiles/r05_step/), where an acq_rel add in every block (256 x rounds per
 // step) cost ~4 %.
+// T.wt (bf16 steps, round 5): the tiles stored write-through (sc1), so after
+// every storing wave's wait the bytes are in memory and the block needs no L2
+// write-back before it counts (MI355X_MICROARCH.md, valid forms: sc1 stores,
+// vmcnt(0), barrier, one lane's agent-scope add; the consumers load behind a
+// kernel boundary) -- the per-block release fence cost 3.5 % of the C4 rank
+// step (tools/step_probe.hip, profiles/r05_step/step_probe_*.log).
 // T.sys: the same at system scope, for peers that read the round over xGMI
-// (fa_peers).  Block-uniform arguments (every thread calls it).
+// (fa_peers), with the release fence kept.  Block-uniform arguments (every
+// thread calls it).
 __device__ __forceinline__ void step_publish(const StepTable& T, unsigned int* sig, unsigned int epoch, int k,
                                              unsigned int cnt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         if (T.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        else if (!T.wt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned int nk = (unsigned int)T.round_tiles[k];
         if (__hip_atomic_fetch_add(&sig[kSigDone + k], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cnt ==
@@ -1678,12 +1719,12 @@ __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     unsigned int* sig, unsigned int epoch) {
     auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        bf16_tile<UB, CB, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
+        bf16_tile<UB, CB, SCORED, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
                                      outb ? outb + c0 : nullptr);
     };
     auto narrow = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        bf16_tile<US, CS, SCORED, B>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
+        bf16_tile<US, CS, SCORED, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
                                      outb ? outb + c0 : nullptr);
     };
     if constexpr (BAL) {
@@ -2264,10 +2305,10 @@ struct StepSpec {
 // rounds (profiles/r05_step/, r05_exchange/).  What is left:
 //   bf16_step_bal_u8c4               the bf16 policy (a C4 rank's slots, round
 //     5): each round's 8 x 4-octet wide tiles dealt over its own balanced
-//     block count (step_tiles_bal), the rounds' remainders in 8 x 2-octet
-//     tiles, no dynamic pool (1.014-1.019 ms alone against 1.042-1.050 for the
-//     round-4 policy; 1.030 / 1.056 beside copy-engine copies; 1.12-1.18 /
-//     1.14-1.19 beside 16-64 copy blocks)
+//     block count (step_tiles_bal), no dynamic pool; with the write-through
+//     tile stores 0.978-0.989 ms alone against 1.011-1.017 for the round-4
+//     policy, 1.013-1.018 / 1.046-1.050 beside copy-engine copies, the whole
+//     step 1.15-1.18 / 1.20-1.22 beside 32-64 copy blocks (profiles/r05_step/wt/)
 //   f32_step_sd_u8c4_p75             the fp32 policy (a C3 rank): 8 x 4-quad
 //     static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
 //     6.23-6.27 beside host copies, even with per-round launches; balanced
@@ -2494,6 +2535,7 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
     T.sys = R.sys ? 1 : 0;
+    T.wt = sp.bf16 ? 1 : 0;  // k_fedavg_bf16_step stores write-through (bf16_tile<..., WT>)
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;

@@ -145,9 +145,14 @@ __global__ __launch_bounds__(kBlock) void k_lean_step(const uint16_t* __restrict
     });
 }
 
-// a 16-B write-through store (sc1: the line leaves the XCD's L2 for memory)
-__device__ __forceinline__ void st16_sc1(void* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// a 16-B write-through store (sc1: the line leaves the XCD's L2 for memory):
+// a raw buffer store over a wave-uniform base, cache-policy operand 8 = sc1
+// (gfx94x/gfx950 encoding of the operand: 1 sc0, 2 nt, 16 sc1)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int64_t byte_off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)byte_off, 0, 16);
 }
 
 // bf16_tile / fold_octets (csrc/fold_kernels.hpp) with the output stores
@@ -196,9 +201,10 @@ __device__ __forceinline__ void fold_octets_st(const u32x4* __restrict__ p, int6
         b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
         b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
         if constexpr (SC1) {
-            st16_sc1(o4, lo);
-            st16_sc1(o4 + 1, hi);
-            st16_sc1(reinterpret_cast<u32x4*>(outb) + oc, b);
+            const __amdgpu_buffer_rsrc_t ro = wt_rsrc(out), rb = wt_rsrc(outb);
+            st16_sc1(ro, 32 * oc, lo);
+            st16_sc1(ro, 32 * oc + 16, hi);
+            st16_sc1(rb, 16 * oc, b);
         } else {
             st16(o4, lo);
             st16(o4 + 1, hi);
@@ -243,7 +249,7 @@ __device__ __forceinline__ void publish_nofence(const StepTable& T, unsigned int
     }
 }
 
-template <bool SC1>
+template <bool SC1, bool LIBTILE = false>
 __global__ __launch_bounds__(kBlock) void k_bal_nofence(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
                                                         const float* __restrict__ a, float divisor,
                                                         float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -262,7 +268,11 @@ __global__ __launch_bounds__(kBlock) void k_bal_nofence(const uint16_t* __restri
         const int64_t n = T.seg_end[g] - lo, S = T.stride[g];
         const int64_t c0 = T.col0[g];
         for (int64_t i = b; b < S && i < n; i += S) {
-            bf16_tile_st<8, 4, SC1>(i, X + c0, N, T.width[g], ldx, a, divisor, out + c0, outb + c0);
+            if constexpr (LIBTILE)
+                bf16_tile<8, 4, false, kBlock, true>(i, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0,
+                                                     outb + c0);
+            else
+                bf16_tile_st<8, 4, SC1>(i, X + c0, N, T.width[g], ldx, a, divisor, out + c0, outb + c0);
             ++cnt;
         }
     }
@@ -293,6 +303,19 @@ __device__ __forceinline__ void bal_tiles(const StepTable& T, unsigned int* sig,
     }
     if (PUB && k >= 0 && cnt) step_publish(T, sig, epoch, k, cnt);
     if (PUB) step_reset(sig);
+}
+
+// the library's step_tiles_bal with one tile body for wide and narrow tiles
+__global__ __launch_bounds__(kBlock) void k_lib_bal_wide_only(const uint16_t* __restrict__ X, int64_t N, int64_t ldx,
+                                                              const float* __restrict__ a, float divisor,
+                                                              float* __restrict__ out, uint16_t* __restrict__ outb,
+                                                              StepTable T, unsigned int* sig, unsigned int epoch) {
+    auto wide = [&](int g, int64_t bid) {
+        const int64_t c0 = T.col0[g];
+        bf16_tile<8, 4, false, kBlock, true>(bid, X + c0, N, T.width[g], ldx, a, nullptr, divisor, out + c0,
+                                             outb ? outb + c0 : nullptr);
+    };
+    step_tiles_bal(T, sig, epoch, wide, wide);
 }
 
 template <bool PUB>
@@ -349,6 +372,7 @@ int main(int argc, char** argv) {
         fprintf(stderr, "step table: %s\n", g_err);
         return 1;
     }
+    Trt.wt = Tbal.wt = Tst.wt = 1;  // as launch_step sets it for the bf16 step (write-through tiles)
     hipStream_t st;
     PCHECK(hipStreamCreate(&st));
     hipEvent_t e0, e1;
@@ -361,15 +385,16 @@ int main(int argc, char** argv) {
     struct V {
         const char* name;
         int which;
-    } vs[] = {{"lib_bal", 1}, {"bal_nopub", 4}, {"bal_nofence", 8}, {"bal_sc1", 9}, {"perround", 6},
-              {"lib_bal", 1}, {"bal_nopub", 4}, {"bal_nofence", 8}, {"bal_sc1", 9}, {"perround", 6},
-              {"lib_bal", 1}, {"bal_sc1", 9}};
+    } vs[] = {{"lib_bal", 1}, {"bal_sc1", 9}, {"bal_libtile", 10}, {"lib_bal_wide", 11}, {"perround", 6},
+              {"lib_bal", 1}, {"bal_sc1", 9}, {"bal_libtile", 10}, {"lib_bal_wide", 11}, {"perround", 6},
+              {"lib_bal", 1}, {"bal_sc1", 9}, {"bal_libtile", 10}, {"lib_bal_wide", 11}};
     std::vector<uint32_t> ref(P), cur(P);
     bool have = false;
     for (const V& v : vs) {
         auto launch = [&]() {
             ++epoch;
             const StepTable& Tv = v.which == 1 || v.which == 4 || v.which >= 8 ? Tbal : v.which == 5 ? Tst : Trt;
+            (void)Tv;
             const unsigned int g = (unsigned int)std::min<int64_t>(grid, Tv.seg_end[Tv.segs - 1]);
             switch (v.which) {
                 case 0:
@@ -404,6 +429,17 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_bal_nofence<true>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out,
                                        outb, Tbal, sig, epoch);
                     break;
+                case 10:
+                    hipLaunchKernelGGL((k_bal_nofence<true, true>), dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div,
+                                       out, outb, Tbal, sig, epoch);
+                    break;
+                case 11: {
+                    StepTable Tw = Tbal;
+                    Tw.wt = 1;
+                    hipLaunchKernelGGL(k_lib_bal_wide_only, dim3(g), dim3(kBlock), 0, st, X, N, ldx, a, div, out, outb,
+                                       Tw, sig, epoch);
+                    break;
+                }
                 case 6:
                     for (int k = 0; k < rounds; ++k)
                         launch_bf16_gs<8, 4>(st, -1, X + offs[k], N, offs[k + 1] - offs[k], ldx, a, nullptr, div,
