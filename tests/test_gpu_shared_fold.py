@@ -5,7 +5,9 @@ per-round waits, bit for bit against the C oracle of fed_avg_aggregator.py:24-42
 
 Covered: the slot widths an 8-GPU C4 rank folds (sharding.overlap_layout(100M,
 8, "bf16"): 256 clients, every column checked), a C3 rank's layout, eight
-small rounds with an odd client count, stall-aware, each round's result
+small rounds with an odd client count, a last round ending off an octet
+boundary (its tail columns stored plainly beside write-through tiles),
+stall-aware, each round's result
 copied behind its wait on another stream the moment it is flagged, four
 launches back to back on one state, and the argument checks.
 """
@@ -186,6 +188,56 @@ def test_one_launch_steps_many_small_rounds(dev, libs, bf16):
         exp = OL.fedavg_f32(OL.synth_f32(seed, N, W), an, np.float32(sum(w)), s=sn)
         for name, (o, _) in one.items():
             assert _same(o, exp), name
+
+
+class _Ragged:
+    """A rounds layout whose last round ends off an 8-column boundary (only
+    the last round may: every round starts 8-aligned)."""
+
+    def __init__(self, offsets):
+        self.offsets = list(offsets)
+        self.rounds = len(offsets) - 1
+
+    def offset(self, k):
+        return self.offsets[k]
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_one_launch_steps_ragged_last_round(dev, libs, bf16):
+    """The last round's width is not a multiple of 8, so its trailing columns
+    are folded by one lane with plain stores (bf16: behind that lane's release
+    fence, the rest of the step being stored write-through): every step form
+    and the product's rounds fold with its waits, bit for bit, and the columns
+    past the last round untouched."""
+    from fedlesscan_amd.sharding import ALIGN
+    _lib, L, B = libs
+    N, seed = 19, 41
+    total = 16_384 + 8 * 8192 + 77_781          # ends 5 columns past an octet
+    W = (total + ALIGN - 1) // ALIGN * ALIGN     # the row pitch (ldx)
+    lay = _Ragged([0, 16_384, 16_384 + 8 * 8192, total])
+    st = torch.cuda.current_stream(dev).cuda_stream
+    X = torch.empty((N, W), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
+    gen = B.fa_synth_bf16 if bf16 else B.fa_synth_f32
+    _lib.check(gen(X.data_ptr(), N, W, W, seed, 0, 0, st), "synth", bench=True)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    s = torch.tensor(np.array(sc, np.float32), device=dev)
+    div = float(np.float32(sum(w)))
+    one = _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16=bf16)
+    an, sn = np.array(w, np.float32), np.array(sc, np.float32)
+    if bf16:
+        ef, eb = OL.fedavg_bf16(OL.synth_bf16(seed, N, W), an, np.float32(sum(w)), s=sn)
+        for name, (o, ob) in one.items():
+            if o is not None:
+                assert _same(o[:total], ef[:total]), name
+                if "copied" not in name:
+                    assert np.isnan(o[total:]).all(), name
+            assert np.array_equal(ob[:total], eb[:total]), name
+    else:
+        exp = OL.fedavg_f32(OL.synth_f32(seed, N, W), an, np.float32(sum(w)), s=sn)
+        for name, (o, _) in one.items():
+            assert _same(o[:total], exp[:total]), name
 
 
 def test_rounds_entry_errors(dev, libs):
