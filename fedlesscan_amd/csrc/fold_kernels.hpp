@@ -112,6 +112,25 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 }
 
 // ---------------------------------------------------------------------------
+// Write-through (sc1) 16-byte stores for the one-launch step (round 5): the
+// line goes to memory, not only the XCD's L2, so a block that publishes a
+// round needs no L2 write-back (an agent release fence per block and round
+// cost the C4 rank step 3.5 %, tools/step_probe.hip).  A raw buffer store
+// over a wave-uniform base (the tile's first octet: readfirstlane of a value
+// every lane shares) with a small per-lane offset; cache-policy operand 16 =
+// sc1 on gfx950.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, int byte_off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+}
+
 // fp32 fold over a stacked matrix, 16 B per lane per client row.
 //   X viewed as [N][ldq] f32x4 (ldq = ldx/4), 16-byte aligned rows.
 //   A lane owns C quads spaced kBlock apart (a block covers C*kBlock quads =
@@ -121,7 +140,7 @@ __device__ __forceinline__ float term1(float x, float a, float s) {
 // lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
 // multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
 // ---------------------------------------------------------------------------
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock, bool WT = false>
 __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
                                            const float* __restrict__ a, const float* __restrict__ s,
                                            const f32x4* acc_in, float divisor, f32x4* out) {
@@ -157,6 +176,16 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
 #pragma unroll
         for (int c = 0; c < C; ++c) acc[c] = add4(acc[c], term4<SCORED>(ld4<NT>(p + i * ldq + c * B), ai, si));
     }
+    if constexpr (WT) {  // write-through over the lane's tile base (out - threadIdx.x, shared by every lane)
+        const __amdgpu_buffer_rsrc_t rs = wt_rsrc(reinterpret_cast<const void*>(
+            (uintptr_t)uniform64((int64_t)(uintptr_t)(out - threadIdx.x))));
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
+            st16_wt(rs, (int)(16 * ((int)threadIdx.x + c * B)), __builtin_bit_cast(u32x4, r));
+        }
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
@@ -165,7 +194,7 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
     }
 }
 // One tile: C*kBlock quads of every client row (tile index bid).
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock, bool WT = false>
 __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           const float* acc_in, float divisor, float* out) {
@@ -177,15 +206,16 @@ __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__
     f32x4* O4 = reinterpret_cast<f32x4*>(out);
     if (q0 + (int64_t)(C - 1) * B < nq) {
         // every quad of this lane is in range (all blocks but the last)
-        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS, B>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
-                                                    O4 + q0);
+        fold_quads<U, C, NT, SCORED, ACC, FIN, NTS, B, WT>(X4 + q0, ldq, N, a, s, ACC ? A4 + q0 : nullptr, divisor,
+                                                        O4 + q0);
         return;
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int64_t q = q0 + (int64_t)c * B;
         if (q < nq)
-            fold_quads<U, 1, NT, SCORED, ACC, FIN, false, B>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor, O4 + q);
+            fold_quads<U, 1, NT, SCORED, ACC, FIN, false, B, WT>(X4 + q, ldq, N, a, s, ACC ? A4 + q : nullptr, divisor,
+                                                             O4 + q);
     }
     // column tail: at most 3 columns, folded by the lane that would own quad
     // index nq under the C-quads-per-lane mapping (scalar loads, same order)
@@ -204,6 +234,8 @@ __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__
             if constexpr (FIN) acc = acc / divisor;
             out[col] = acc;
         }
+        // WT: these few plain stores are written back before the block publishes
+        if constexpr (WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
 }
 
@@ -1335,24 +1367,6 @@ __device__ __forceinline__ void unpack_bf16x8(u32x4 w, f32x4& even, f32x4& odd) 
 // A 16-byte non-temporal output store
 __device__ __forceinline__ void st16(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
-// Write-through (sc1) 16-byte stores for the one-launch step (round 5): the
-// line goes to memory, not only the XCD's L2, so a block that publishes a
-// round needs no L2 write-back (an agent release fence per block and round
-// cost the C4 rank step 3.5 %, tools/step_probe.hip).  A raw buffer store
-// over a wave-uniform base (the tile's first octet: readfirstlane of a value
-// every lane shares) with a small per-lane offset; cache-policy operand 16 =
-// sc1 on gfx950.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
-}
-__device__ __forceinline__ int64_t uniform64(int64_t v) {
-    const uint64_t u = (uint64_t)v;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, int byte_off, u32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
-}
 
 // One row group of U rows x C octets: loaded (ld) and folded in row order (add)
 template <int U, int C>
@@ -1541,7 +1555,7 @@ struct StepTable {
     int32_t segs;
     int32_t rounds;
     int32_t sys;    // publish the rounds at system scope: other GPUs read them (fa_peers, the peer exchange)
-    int32_t wt;     // the tiles' output stores are write-through (bf16 steps): no per-block L2 write-back
+    int32_t wt;     // the tiles' output stores are write-through: no per-block L2 write-back
     int64_t stride[kMaxSegs];  // balanced rounds (step_tiles_bal): static segment g dealt over stride[g] blocks
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
@@ -1561,7 +1575,7 @@ constexpr int kStatusWords = kMaxRounds + 1;  // a timeout record per round + th
 // nothing measurable (1.044 ms per C4 rank step with and without it, one box,
 // profiles/r05_step/), where an acq_rel add in every block (256 x rounds per
 // step) cost ~4 %.
-// T.wt (bf16 steps, round 5): the tiles stored write-through (sc1), so after
+// T.wt (round 5): the tiles stored write-through (sc1), so after
 // every storing wave's wait the bytes are in memory and the block needs no L2
 // write-back before it counts (MI355X_MICROARCH.md, valid forms: sc1 stores,
 // vmcnt(0), barrier, one lane's agent-scope add; the consumers load behind a
@@ -1743,13 +1757,13 @@ __global__ __launch_bounds__(B) void k_fold_f32_step(
     float divisor, float* __restrict__ out, StepTable T, unsigned int* sig, unsigned int epoch) {
     auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        fold_tile<UB, CB, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                             divisor, out + c0);
+        fold_tile<UB, CB, true, SCORED, false, true, true, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                                   divisor, out + c0);
     };
     auto narrow = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        fold_tile<US, CS, true, SCORED, false, true, true, B>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                             divisor, out + c0);
+        fold_tile<US, CS, true, SCORED, false, true, true, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+                                                                   divisor, out + c0);
     };
     if constexpr (BAL) {
         step_tiles_bal(T, sig, epoch, wide, narrow);
@@ -2310,9 +2324,11 @@ struct StepSpec {
 //     policy, 1.013-1.018 / 1.046-1.050 beside copy-engine copies, the whole
 //     step 1.15-1.18 / 1.20-1.22 beside 32-64 copy blocks (profiles/r05_step/wt/)
 //   f32_step_sd_u8c4_p75             the fp32 policy (a C3 rank): 8 x 4-quad
-//     static tiles and a 0.75-pass pool of 16 x 1-quad tiles (5.92 alone,
-//     6.23-6.27 beside host copies, even with per-round launches; balanced
-//     rounds lose: 6.05-6.10 against 5.91-5.95 alone)
+//     static tiles and a 0.75-pass pool of 16 x 1-quad tiles; with the
+//     write-through tile stores 5.81 ms alone against 5.80-5.81 per round,
+//     the fold 5.90-5.93 beside 16-64 host-copy blocks against 6.06-6.18
+//     (profiles/r05_step/wt_f32/); balanced rounds lost (6.05-6.10 against
+//     5.91-5.95 alone, before the write-through stores)
 //   bf16_step_rt_u8c4n8c2_p100_last  comparison: round 4's bf16 policy, whole
 //     passes of wide tiles per round, the rest of each round in narrow static
 //     tiles over all blocks, the last round's columns a one-pass dynamic pool
@@ -2535,7 +2551,7 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
     T.sys = R.sys ? 1 : 0;
-    T.wt = sp.bf16 ? 1 : 0;  // k_fedavg_bf16_step stores write-through (bf16_tile<..., WT>)
+    T.wt = 1;  // both step kernels store their tiles write-through (bf16_tile / fold_tile <..., WT>)
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
     const unsigned int epoch = R.epoch + 1 == 0 ? 1 : R.epoch + 1;
