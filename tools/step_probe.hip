@@ -26,6 +26,11 @@
 //             no per-block release fence: every storing wave's vmcnt(0), a
 //             barrier, the count; the completing block acquires and raises
 //             the flag with a release store (MI355X_MICROARCH.md, valid forms)
+//   bal_libtile  the same loop over the library's write-through tile body
+//   lib_bal_wide the library's step_tiles_bal with one tile body for both
+//             tile kinds
+// (The list run is the vs[] table in main; the library's tables get wt = 1,
+// as launch_step sets it.)
 #include "fold_kernels.hpp"
 
 #include <algorithm>
