@@ -118,6 +118,15 @@ def parse():
                     help="the one-launch step's exchange: 'rccl' = an all_gather_into_tensor per round behind its "
                          "wait; 'peer_copy' = copy-engine pulls of the peers' slots through IPC-opened buffers "
                          "(sharding.PeerExchange, fa_peers); the gathered model is checked against an RCCL step's")
+    ap.add_argument("--step-impl", default="product", choices=["product", "loop"],
+                    help="under a process group: 'product' (default) = every step is one call of the shipped "
+                         "ShardedAggregator.aggregate_slots (sharding.py; --step-mode and --exchange map onto its "
+                         "one_launch and exchange, --check onto its check); 'loop' = this file's own step loop "
+                         "over the same library calls, for comparison")
+    ap.add_argument("--check", default="sync", choices=["sync", "deferred"],
+                    help="--step-impl product: ShardedAggregator's round-wait check, 'sync' (its default: every "
+                         "call waits for its waits and agrees over the ranks) or 'deferred' (one check_timeouts() "
+                         "after the K timed steps, inside the timed region)")
     ap.add_argument("--tail-steps", type=int, default=None,
                     help="rounds over which the slots shrink geometrically to --tail (2 with --tail 0.25 and 4 "
                          "rounds: shares 1, 1, 0.5, 0.25)")
@@ -235,7 +244,8 @@ class Workload:
     slots k*world + r (k < rounds), stored side by side in X [N, rounds*sub].
     With rounds=1 that is one contiguous bucket per rank."""
 
-    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0, tail=1.0, tail_steps=1):
+    def __init__(self, cfg, rank, world, dev, rounds, align=None, pitch_extra=0, tail=1.0, tail_steps=1,
+                 exchange_step=False):
         self.N, P, self.dtype, self.scored, self.seed, card_hi, self.scaling, self.desc = cfg
         self.P_total = P * world if self.scaling == "weak" else P
         self.layout = SlotLayout(self.P_total, world, rounds, align=ALIGN if align is None else align,
@@ -266,10 +276,14 @@ class Workload:
         # bf16 models also write the RNE bf16 copy of the result (the form the
         # multi-GPU gather moves: half the xGMI bytes of the fp32 result)
         self.out_bf16 = torch.empty(W, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else None
+        # an exchange step of bf16 rows stores only the bf16 copy it exchanges
+        # (ABI 5: no fp32 result, as ShardedAggregator); one GPU alone writes both
+        self.write_f32 = not (exchange_step and self.dtype == "bf16")
         elt = 4 if self.dtype == "f32" else 2
-        # algorithmic bytes per step on this rank: every real input element once + the fp32 output once
-        # (+ the bf16 copy of the output for bf16 models)
-        self.bytes = self.N * self.P * elt + self.P * 4 + (self.P * 2 if self.dtype == "bf16" else 0)
+        # algorithmic bytes per step on this rank: every real input element once + each output written once
+        # (fp32 4 B, the bf16 copy 2 B per param)
+        self.bytes = (self.N * self.P * elt + (self.P * 4 if self.write_f32 else 0)
+                      + (self.P * 2 if self.dtype == "bf16" else 0))
         torch.cuda.synchronize()
 
     def launch(self, variant=0, k=0):
@@ -281,7 +295,7 @@ class Workload:
         s = None if self.s is None else self.s.data_ptr()
         off, sub = self.layout.offset(k), self.layout.width(k)
         x = self.X.data_ptr() + off * self.X.element_size()
-        o = self.out.data_ptr() + off * 4
+        o = self.out.data_ptr() + off * 4 if self.write_f32 else None
         ob = None if self.out_bf16 is None else self.out_bf16.data_ptr() + off * 2
         bench = variant > 0
         if self.dtype == "f32" and variant < 0:  # opt-in split-client fold
@@ -334,9 +348,12 @@ def cpu_baseline(wl: Workload, ncols: int, reps: int = 3):
         t0 = time.perf_counter()
         ref_omp = OL.fedavg_f32(Xh, a, np.float32(wl.div), s=s, nthreads=threads)
         t_omp.append(time.perf_counter() - t0)
-    gpu = wl.out[:ncols].cpu().numpy()
-    exact = bool(np.array_equal(gpu.view(np.uint32), ref.view(np.uint32)) and
-                 np.array_equal(ref_omp.view(np.uint32), ref.view(np.uint32)))
+    if wl.write_f32:
+        gpu_same = np.array_equal(wl.out[:ncols].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    else:  # a bf16 exchange step stores only the RNE-bf16 copy of the result
+        gpu_same = np.array_equal(wl.out_bf16[:ncols].view(torch.int16).cpu().numpy().view(np.uint16),
+                                  synth.f32_to_bf16_bits(ref))
+    exact = bool(gpu_same and np.array_equal(ref_omp.view(np.uint32), ref.view(np.uint32)))
     visible = len(os.sched_getaffinity(0))
     return {
         "value": round(sample_bytes / t_np / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
@@ -423,7 +440,10 @@ def main():
         args.variant = -1
     wl = Workload(cfg, rank, world, dev, rounds, align=1 if args.unpadded else None, pitch_extra=args.pitch_extra,
                   tail=(args.tail if args.tail is not None else DEFAULT_TAIL[cfg[2]][0]) if rounds > 1 else 1.0,
-                  tail_steps=args.tail_steps if args.tail_steps is not None else DEFAULT_TAIL[cfg[2]][1])
+                  tail_steps=args.tail_steps if args.tail_steps is not None else DEFAULT_TAIL[cfg[2]][1],
+                  exchange_step=dist_on)
+    # the shipped class steps the multi-GPU run (a sweep or a split fold times this file's own launches)
+    product = dist_on and args.step_impl == "product" and args.variant == 0 and not args.sweep
     B = _lib.load_bench()
     lay = wl.layout
     full = torch.empty(lay.padded_total, dtype=torch.float32 if wl.dtype == "f32" else torch.bfloat16,
@@ -456,9 +476,10 @@ def main():
         t = torch.tensor([recorded], dtype=torch.int64, device=dev)
         dist.broadcast(t, src=0)
         recorded = int(t.item())
-    probe_modes = can_one and step_mode in ("auto", "probe") and recorded < 0
+    # the product's own probe (ShardedAggregator one_launch="probe") decides during the warm-up
+    probe_modes = can_one and step_mode in ("auto", "probe") and recorded < 0 and not product
     one_launch = can_one and (recorded != 0)
-    per_round_possible = not can_one or probe_modes
+    per_round_possible = not can_one or probe_modes or (product and step_mode != "one")
     if args.variant == 0 and L.fa_set_autotune(-1) == 1 and per_round_possible:
         for tune_calls in range(1, 201):
             for k in range(rounds):
@@ -527,7 +548,12 @@ def main():
         offs = [lay.offset(k) for k in range(rounds + 1)]
 
     px = None
-    if can_one and args.exchange == "peer_copy":
+    agg = None
+    if product:
+        from fedlesscan_amd.sharding import ShardedAggregator
+        ol = {"auto": "probe", "probe": "probe", "one": True, "per-round": False}[step_mode] if can_one else False
+        agg = ShardedAggregator(one_launch=ol, exchange=args.exchange, check=args.check)
+    elif can_one and args.exchange == "peer_copy":
         from fedlesscan_amd.sharding import PeerExchange
         px = PeerExchange(None, dev, lay, wl.dtype == "bf16")
 
@@ -547,7 +573,8 @@ def main():
             return
         if ev is not None:
             ev[0][0][0].record(stream)
-        r = engine.fold_rounds(wl.X, wl.weights, wl.scores, offs, out=wl.out, out_bf16=wl.out_bf16)
+        r = engine.fold_rounds(wl.X, wl.weights, wl.scores, offs, out=wl.out if wl.write_f32 else None,
+                               out_bf16=wl.out_bf16)
         if ev is not None:
             ev[0][0][1].record(stream)
         works = []
@@ -566,7 +593,11 @@ def main():
 
     def step(ev=None, mode=None):
         """ev = (fold events per round, end event) for the timed steps; mode
-        "one" / "per-round" overrides the chosen step form (the probe)."""
+        "one" / "per-round" overrides the chosen step form (the probe).  The
+        product: one aggregate_slots call (its own events: agg.trace)."""
+        if product:
+            agg.aggregate_slots(wl.X, wl.weights, wl.scores, lay, out=full)
+            return
         if (one_launch if mode is None else mode == "one"):
             step_one_launch(ev)
             return
@@ -587,7 +618,12 @@ def main():
         if ev is not None:
             ev[1].record(stream)
 
-    torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
+    if product:
+        # the caller's stream is the default stream: aggregate_slots moves its
+        # folds onto the high-priority fold stream itself and joins back
+        stream = torch.cuda.current_stream(dev)
+    else:
+        torch.cuda.set_stream(stream)  # the folds and the collectives' waits run on `stream` from here on
     mode_probe = None
     if probe_modes:
         # which step form is faster depends on how much the exchange kernels
@@ -637,8 +673,29 @@ def main():
             warm_extra = int(t.item())
         for _ in range(warm_extra):
             step()
+    if product and agg.one_launch == "probe" and rounds > 1:
+        # the class's probe alternates the forms over its first 2 x PROBE_CALLS
+        # calls of the shape; the timed steps run the form it keeps (the same
+        # count of calls on every rank: its decision is max-over-ranks timing)
+        for _ in range(2 * agg.PROBE_CALLS):
+            if agg.step_form(wl.X, lay) is not None:
+                break
+            step()
+            warm_extra += 1
+        pkey = agg.step_key(wl.X, lay)
+        got = agg.probed.get(pkey)
+        mode_probe = ({"chosen": agg.step_form(wl.X, lay), "recorded": pkey,
+                       "one_launch_ms": [round(x, 4) for x in got["one"]],
+                       "per_round_ms": [round(x, 4) for x in got["per"]],
+                       "how": "ShardedAggregator(one_launch='probe'): its first 2 x PROBE_CALLS calls alternate "
+                              "the forms (device time per call, max over ranks), the best call of each compared"}
+                      if got else {"chosen": agg.step_form(wl.X, lay), "restored": pkey,
+                                   "how": "recorded in the tuner's cache file (fa_step_lookup), rank 0's record "
+                                          "broadcast: no timing run"})
     evs = [([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(rounds)], torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if product:
+        agg.trace = []  # the class records its own fold / end events per call
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -651,6 +708,8 @@ def main():
     region[0].record(stream)
     for k in range(args.steps):
         step(evs[k] if dist_on else None)
+    if product and args.check == "deferred":
+        agg.check_timeouts()  # the pipelined caller's check, inside the timed region
     region[1].record(stream)
     torch.cuda.synchronize()
     if dist_on:
@@ -660,6 +719,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if product:
+        evs, agg.trace = agg.trace, None
+        # the form the timed calls ran: one fold launch per call, or one per round
+        one_launch = rounds > 1 and all(len(folds) == 1 for folds, _ in evs)
+        # this rank's own slots folded by the per-round product launches: the
+        # gather check's and the CPU baseline's reference for the product's model
+        for k in range(rounds):
+            wl.launch(0, k)
+        torch.cuda.synchronize()
     gather_ok = None
     if px is not None:
         # the whole model the peer copy reassembled must equal an RCCL step's, bit for bit
@@ -715,9 +783,11 @@ def main():
         kern_avg, exposed_avg = float(t[0].item()), float(t[1].item())
         round_ms = [round(float(x), 4) for x in t[2:].tolist()]
     if can_one:  # a round wait that gave up (never expected) let an exchange read an unfinished round
-        n_to = max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, stream.cuda_stream)))
-        if px is not None:
-            n_to += max(0, L.fa_rounds_timeouts(px.state)) + max(0, L.fa_rounds_check(px.state))
+        fstream = sharding_fold_stream(dev) if product else stream  # where the step's fold launches ran
+        n_to = max(0, L.fa_rounds_timeouts(engine.rounds_state(dev, fstream.cuda_stream)))
+        for p in ([px] if px is not None else []) + ([q for q in agg._peers.values() if q is not None]
+                                                     if product else []):
+            n_to += max(0, L.fa_rounds_timeouts(p.state)) + max(0, L.fa_rounds_check(p.state))
         t = torch.tensor([n_to], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
         timeouts = int(t.item())
@@ -805,6 +875,12 @@ def main():
                 "fold_form_ranks_agreed": forms_agree,
                 "fold_form_rank0_broadcast": bool(dist_on and world > 1 and args.variant == 0 and per_round_possible),
                 "step_mode": step_mode if dist_on and rounds > 1 else None,
+                "step_impl": ("product: ShardedAggregator(one_launch=%r, exchange=%r, check=%r).aggregate_slots per "
+                              "step" % (agg.one_launch, agg.exchange, agg.check)) if product else
+                             ("loop (bench.py's own step)" if dist_on else None),
+                "outputs": ("fp32" if wl.dtype == "f32" else
+                            "RNE bf16 only (the exchanged form; no fp32 result, ABI 5)" if not wl.write_f32 else
+                            "fp32 + RNE bf16"),
                 "exchange": (args.exchange if one_launch else "rccl") if dist_on else None,
                 "step_mode_probe": mode_probe,
                 "variant": "splitn (opt-in, not bit-exact)" if args.variant < 0 else
@@ -861,6 +937,8 @@ def main():
             raise AggregationError(f"{timeouts} round wait(s) timed out during the run")
     if px is not None:
         px.close()
+    if agg is not None:
+        agg.close()
     if dist_on:
         dist.destroy_process_group()
 

@@ -27,7 +27,7 @@ BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
 HOSTFAST_PATH = os.path.join(PKG, "_native", "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FA_OK, FA_ERR_ARG, FA_ERR_NO_CLIENTS, FA_ERR_SHAPE, FA_ERR_HIP = range(5)
 
@@ -56,6 +56,8 @@ _PROTOS = {
     "fa_rounds_destroy": (_int, [_vp]),
     "fa_fedavg_f32_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
     "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
+    "fa_fedavg_f32_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
+    "fa_fedavg_bf16_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
     "fa_rounds_wait": (_int, [_vp, _int, _vp]),
     "fa_rounds_check": (_int, [_vp]),
     "fa_rounds_timeouts": (_int, [_vp]),
@@ -67,7 +69,6 @@ _PROTOS = {
     "fa_peers_open": (_int, [_vp, _vp]),
     "fa_peers_send": (_vp, [_vp]),
     "fa_peers_rounds": (_vp, [_vp]),
-    "fa_peers_fence": (_int, [_vp, _vp]),
     "fa_peers_exchange": (_int, [_vp, _int, _vp, _vp, _vp, _vp]),
     "fa_fedavg_f64": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _vp]),
     "fa_fedavg_i32": (_int, [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp]),
@@ -130,6 +131,7 @@ _BENCH_PROTOS = {
     "fa_bench_rounds_destroy": (_int, [_vp]),
     "fa_fedavg_rounds_form": (_int, [_vp, _int, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
     "fa_bench_rounds_wait": (_int, [_vp, _int, _vp]),
+    "fa_bench_rounds_set_sys": (_int, [_vp, _int]),
     "fa_num_ptrs_variants": (_int, []),
     "fa_ptrs_variant_name": (ctypes.c_char_p, [_int]),
 }

@@ -7,9 +7,11 @@ Drop-in for fedless/aggregator/fed_avg_aggregator.py:
   StreamFedAvgAggregator.chunks / .aggregate   :95-153
 
 Same constructor signatures, argument meaning, return types and exceptions.
-`select_aggregation_candidates` takes a result store with the ClientResultDao
-query methods (fedlesscan_amd.store.InMemoryClientResultStore) where the
-reference takes a pymongo client.
+`select_aggregation_candidates(mongo_client, session_id, round_id)` takes a
+result store with the ClientResultDao query methods (the reference's DAO, or
+fedlesscan_amd.store.InMemoryClientResultStore), or a pymongo client, which
+it wraps into the reference's ClientResultDao as the reference does
+(parameter_aggregator.result_store).
 """
 from __future__ import annotations
 
@@ -22,7 +24,7 @@ from .. import engine
 from ..common.models import ClientResult, Parameters, TestMetrics
 from ..common.serialization import deserialize_parameters
 from .exceptions import InsufficientClientResults, UnknownCardinalityError
-from .parameter_aggregator import ParameterAggregator
+from .parameter_aggregator import ParameterAggregator, result_store
 
 logger = logging.getLogger(__name__)
 
@@ -96,7 +98,10 @@ class FedAvgAggregator(ParameterAggregator):
     def _aggregate(self, parameters: List[List[np.ndarray]], weights: List[float]) -> List[np.ndarray]:
         return engine.aggregate_layers(parameters, weights, None, device=self.device, devices=self.devices)
 
-    def select_aggregation_candidates(self, store, session_id, round_id):
+    def select_aggregation_candidates(self, mongo_client, session_id, round_id):
+        """fed_avg_aggregator.py:44-55; mongo_client: a result store or a
+        MongoClient (parameter_aggregator.result_store)."""
+        store = result_store(mongo_client)
         dicts, candidates = store.load_results_for_round(session_id=session_id, round_id=round_id)
         # The reference tests `if not round_candidates` (:51-54), and round_candidates
         # is the generator _retrieve_result_files returns (client_daos.py:125,161):

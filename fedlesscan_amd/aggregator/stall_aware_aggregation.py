@@ -22,7 +22,7 @@ from .. import engine
 from ..common.models import AggregationHyperParams, ClientResult, Parameters, TestMetrics
 from .exceptions import InsufficientClientResults
 from .fed_avg_aggregator import chunked, decode_results, decoded_rows
-from .parameter_aggregator import ParameterAggregator
+from .parameter_aggregator import ParameterAggregator, result_store
 
 
 class StallAwareAggregator(ParameterAggregator):
@@ -43,7 +43,10 @@ class StallAwareAggregator(ParameterAggregator):
         return engine.aggregate_layers(parameters, weights, self._score_clients(client_feats),
                                        device=self.device, devices=self.devices)
 
-    def select_aggregation_candidates(self, store, session_id, round_id):
+    def select_aggregation_candidates(self, mongo_client, session_id, round_id):
+        """stall_aware_aggregation.py:69-80; mongo_client: a result store or a
+        MongoClient (parameter_aggregator.result_store)."""
+        store = result_store(mongo_client)
         dicts, candidates = store.load_results_for_session(session_id=session_id, round_id=round_id,
                                                            tolerance=self.tolerance)
         # always-truthy generator, as in the reference (:76-79): see FedAvgAggregator

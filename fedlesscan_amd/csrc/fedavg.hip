@@ -370,15 +370,9 @@ int fa_peers_open(fa_peers* x, const void* all_handles) {
     return rc;
 }
 
-void* fa_peers_send(fa_peers* x) { return x ? x->send : nullptr; }
+void* fa_peers_send(fa_peers* x) { return x ? peers_next_send(*x) : nullptr; }
 
 fa_rounds* fa_peers_rounds(fa_peers* x) { return x ? &x->R : nullptr; }
-
-int fa_peers_fence(fa_peers* x, void* stream) {
-    if (!x) return fail(FA_ERR_ARG, "null fa_peers");
-    StreamDevice on_stream_device(stream);
-    return peers_fence(*x, (hipStream_t)stream);
-}
 
 int fa_peers_exchange(fa_peers* x, int rounds, const int64_t* src_offsets, void* dst, const int64_t* dst_offsets,
                       void* stream) {
@@ -506,6 +500,23 @@ int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, c
                          float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
     return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
         return bf16_auto(X, N, P, ldx, ad, sd, divisor, out_f32, out_bf16, stream);
+    });
+}
+
+int fa_fedavg_f32_rounds_hostf(fa_rounds* r, const float* X, int64_t N, int64_t ldx, const float* a, const float* s,
+                               float divisor, float* out, int rounds, const int64_t* offsets, void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
+    return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
+        return fa_fedavg_f32_rounds(r, X, N, ldx, ad, sd, divisor, out, rounds, offsets, stream);
+    });
+}
+
+int fa_fedavg_bf16_rounds_hostf(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx, const float* a,
+                                const float* s, float divisor, float* out_f32, uint16_t* out_bf16, int rounds,
+                                const int64_t* offsets, void* stream) {
+    if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
+    return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
+        return fa_fedavg_bf16_rounds(r, X, N, ldx, ad, sd, divisor, out_f32, out_bf16, rounds, offsets, stream);
     });
 }
 

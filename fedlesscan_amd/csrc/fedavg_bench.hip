@@ -565,6 +565,14 @@ int fa_bench_rounds_wait(void* r, int round, void* stream) {
     return rounds_wait(*o, round, (hipStream_t)stream);
 }
 
+int fa_bench_rounds_set_sys(void* r, int sys) {
+    RoundsState* o = static_cast<RoundsState*>(r);
+    if (!o) return fail(FA_ERR_ARG, "null rounds state");
+    if (sys < 0 || sys > 2) return fail(FA_ERR_ARG, "sys must be 0, 1 or 2");
+    o->sys = sys;
+    return FA_OK;
+}
+
 int fa_num_bf16_forms(void) { return kNumBf16Forms; }
 const char* fa_bf16_form_name(int form) {
     return (form >= 0 && form < kNumBf16Forms) ? bf16_form_name((Bf16Form)form) : "";
@@ -572,7 +580,7 @@ const char* fa_bf16_form_name(int form) {
 int fa_fedavg_bf16_form(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
                         float divisor, float* out_f32, uint16_t* out_bf16, void* stream, int form) {
     if (form < 0 || form >= kNumBf16Forms) return fail(FA_ERR_ARG, "unknown bf16 form %d", form);
-    int rc = check_common(N, P, ldx, X, a, out_f32);
+    int rc = check_common(N, P, ldx, X, a, bf16_any_out(out_f32, out_bf16));
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     if (!aligned16(X) || (ldx % 8) || !aligned16(out_f32) || (out_bf16 && !aligned16(out_bf16)))
@@ -595,7 +603,7 @@ int fa_fedavg_bf16_variant(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                            int variant) {
     if (variant < 0 || variant >= kNumBf16Variants) return fail(FA_ERR_ARG, "unknown bf16 variant %d", variant);
     if (variant == 0) return bf16_auto(X, N, P, ldx, a, s, divisor, out_f32, out_bf16, stream);
-    int rc = check_common(N, P, ldx, X, a, out_f32);
+    int rc = check_common(N, P, ldx, X, a, bf16_any_out(out_f32, out_bf16));
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     if (!aligned16(X) || (ldx % 8) || !aligned16(out_f32) || (out_bf16 && !aligned16(out_bf16)))

@@ -127,8 +127,22 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+// WT (the tile functions' template argument): 0 plain stores; kWtAgent sc1
+// (write-through to memory: the one-launch step on this GPU); kWtSystem sc0
+// sc1 (system-coherent: a peer exchange's step, whose rounds other GPUs' copy
+// engines read).  Cache-policy operand: sc0 = 1, sc1 = 16 on gfx950.
+constexpr int kWtAgent = 1, kWtSystem = 2;
+template <int WT>
 __device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, int byte_off, u32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+    static_assert(WT == kWtAgent || WT == kWtSystem, "write-through flavour");
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, WT == kWtSystem ? 17 : 16);
+}
+// After a tile's few plain tail stores: write them back before the block
+// publishes (the wide stores are write-through already).
+template <int WT>
+__device__ __forceinline__ void wt_tail_release() {
+    if constexpr (WT == kWtSystem) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else if constexpr (WT == kWtAgent) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 // fp32 fold over a stacked matrix, 16 B per lane per client row.
@@ -140,7 +154,7 @@ __device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, int byte_off, 
 // lane; NT = non-temporal (read-once) loads; SCORED = stall-aware second
 // multiply; ACC = continue a fold from acc_in; FIN = divide at the end.
 // ---------------------------------------------------------------------------
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock, bool WT = false>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS = false, int B = kBlock, int WT = 0>
 __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t ldq, int64_t N,
                                            const float* __restrict__ a, const float* __restrict__ s,
                                            const f32x4* acc_in, float divisor, f32x4* out) {
@@ -182,7 +196,7 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             const f32x4 r = FIN ? div4(acc[c], divisor) : acc[c];
-            st16_wt(rs, (int)(16 * ((int)threadIdx.x + c * B)), __builtin_bit_cast(u32x4, r));
+            st16_wt<WT>(rs, (int)(16 * ((int)threadIdx.x + c * B)), __builtin_bit_cast(u32x4, r));
         }
         return;
     }
@@ -194,7 +208,7 @@ __device__ __forceinline__ void fold_quads(const f32x4* __restrict__ p, int64_t 
     }
 }
 // One tile: C*kBlock quads of every client row (tile index bid).
-template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock, bool WT = false>
+template <int U, int C, bool NT, bool SCORED, bool ACC, bool FIN, bool NTS, int B = kBlock, int WT = 0>
 __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           const float* acc_in, float divisor, float* out) {
@@ -235,7 +249,7 @@ __device__ __forceinline__ void fold_tile(int64_t bid, const float* __restrict__
             out[col] = acc;
         }
         // WT: these few plain stores are written back before the block publishes
-        if constexpr (WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        wt_tail_release<WT>();
     }
 }
 
@@ -1392,7 +1406,7 @@ __device__ __forceinline__ void octets_add(f32x4 (&ev)[C], f32x4 (&od)[C], const
     }
 }
 
-template <int U, int C, bool SCORED, int B = kBlock, bool WT = false>
+template <int U, int C, bool SCORED, int B = kBlock, int WT = 0>
 __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t ldo, int64_t N,
                                             const float* __restrict__ a, const float* __restrict__ s,
                                             float divisor, float* __restrict__ out, uint16_t* __restrict__ outb,
@@ -1434,16 +1448,20 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
     for (int c = 0; c < C; ++c) {
         const f32x4 e = div4(ev[c], divisor), o = div4(od[c], divisor);
         const int64_t oc = o0 + (int64_t)c * B;
-        const u32x4 lo = __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y});
-        const u32x4 hi = __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w});
-        if constexpr (WT) {
-            const __amdgpu_buffer_rsrc_t r = wt_rsrc(out + 8 * ob);
-            st16_wt(r, (int)(32 * (oc - ob)), lo);
-            st16_wt(r, (int)(32 * (oc - ob)) + 16, hi);
-        } else {
-            f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
-            st16(o4, lo);
-            st16(o4 + 1, hi);
+        // out (fp32) and outb (RNE bf16) are each optional, one of them given
+        // (ABI 5): a step that exchanges only the bf16 copy stores no fp32
+        if (out) {
+            const u32x4 lo = __builtin_bit_cast(u32x4, f32x4{e.x, o.x, e.y, o.y});
+            const u32x4 hi = __builtin_bit_cast(u32x4, f32x4{e.z, o.z, e.w, o.w});
+            if constexpr (WT) {
+                const __amdgpu_buffer_rsrc_t r = wt_rsrc(out + 8 * ob);
+                st16_wt<WT>(r, (int)(32 * (oc - ob)), lo);
+                st16_wt<WT>(r, (int)(32 * (oc - ob)) + 16, hi);
+            } else {
+                f32x4* o4 = reinterpret_cast<f32x4*>(out) + 2 * oc;
+                st16(o4, lo);
+                st16(o4 + 1, hi);
+            }
         }
         if (outb) {
             u32x4 b;
@@ -1451,7 +1469,7 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
             b.y = (uint32_t)f2bf_rne(e.y) | ((uint32_t)f2bf_rne(o.y) << 16);
             b.z = (uint32_t)f2bf_rne(e.z) | ((uint32_t)f2bf_rne(o.z) << 16);
             b.w = (uint32_t)f2bf_rne(e.w) | ((uint32_t)f2bf_rne(o.w) << 16);
-            if constexpr (WT) st16_wt(wt_rsrc(outb + 8 * ob), (int)(16 * (oc - ob)), b);
+            if constexpr (WT) st16_wt<WT>(wt_rsrc(outb + 8 * ob), (int)(16 * (oc - ob)), b);
             else st16(reinterpret_cast<u32x4*>(outb) + oc, b);
         }
     }
@@ -1459,7 +1477,7 @@ __device__ __forceinline__ void fold_octets(const u32x4* __restrict__ p, int64_t
 
 // bf16 rows: a lane owns C octets (8 columns, one 16-byte load per row each)
 // spaced kBlock apart; the trailing P%8 columns go to the lane with o0 == P/8.
-template <int U, int C, bool SCORED, int B = kBlock, bool WT = false>
+template <int U, int C, bool SCORED, int B = kBlock, int WT = 0>
 __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restrict__ X, int64_t N, int64_t P,
                                           int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
                                           float divisor, float* __restrict__ out, uint16_t* __restrict__ outb) {
@@ -1483,11 +1501,11 @@ __device__ __forceinline__ void bf16_tile(int64_t bid, const uint16_t* __restric
             for (int64_t i = 1; i < N; ++i)
                 acc = acc + term1<SCORED>(bf2f(X[i * ldx + col]), a[i], SCORED ? s[i] : 1.0f);
             acc = acc / divisor;
-            out[col] = acc;
+            if (out) out[col] = acc;
             if (outb) outb[col] = f2bf_rne(acc);
         }
         // WT: these few plain stores are written back before the block publishes
-        if constexpr (WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        wt_tail_release<WT>();
     }
 }
 
@@ -1556,40 +1574,49 @@ struct StepTable {
     int32_t rounds;
     int32_t sys;    // publish the rounds at system scope: other GPUs read them (fa_peers, the peer exchange)
     int32_t wt;     // the tiles' output stores are write-through: no per-block L2 write-back
+    int32_t sysfence;  // sys with sc1 tile stores: a system release fence per block and round (round 5's
+                       // publication; bench-library A/B only: the product's sys launches store sc0 sc1)
     int64_t stride[kMaxSegs];  // balanced rounds (step_tiles_bal): static segment g dealt over stride[g] blocks
 };
 // signal words: [0] next dynamic tile, [1] blocks done, [2, 2+R) tiles done per round,
 // [2+R, 2+2R) round flags (the epoch of the launch that completed the round), [2+2R] waits timed out
 constexpr int kSigDone = 2, kSigFlag = 2 + kMaxRounds, kSigTimeout = 2 + 2 * kMaxRounds, kSigWords = 3 + 2 * kMaxRounds;
-constexpr int kStatusWords = kMaxRounds + 1;  // a timeout record per round + the peer exchange's buffer fence
+constexpr int kStatusWords = kMaxRounds;  // a timeout record per round
 
 // A block leaves round k (its tiles come in round order): publish its cnt
-// tiles of the round once (MI355X_MICROARCH.md, valid producer form): every
-// storing wave waits for its stores, a barrier, then one lane writes the XCD's
-// L2 back (agent release fence) and counts the tiles with an agent-scope add
-// (every block's adds form one release sequence).  The block whose add
-// completes the round takes an acquire fence -- it synchronises with every
-// other block's release -- and raises the round's flag with a release store,
-// so whoever acquires the flag sees the whole round by the memory model, not
-// only by this hardware's write-back order.  One acquire per round: it costs
-// nothing measurable (1.044 ms per C4 rank step with and without it, one box,
-// profiles/r05_step/), where an acq_rel add in every block (256 x rounds per
-// step) cost ~4 %.
-// T.wt (round 5): the tiles stored write-through (sc1), so after
-// every storing wave's wait the bytes are in memory and the block needs no L2
-// write-back before it counts (MI355X_MICROARCH.md, valid forms: sc1 stores,
-// vmcnt(0), barrier, one lane's agent-scope add; the consumers load behind a
-// kernel boundary) -- the per-block release fence cost 3.5 % of the C4 rank
-// step (tools/step_probe.hip, profiles/r05_step/step_probe_*.log).
-// T.sys: the same at system scope, for peers that read the round over xGMI
-// (fa_peers), with the release fence kept.  Block-uniform arguments (every
-// thread calls it).
+// tiles of the round once.  Every storing wave waits for its stores
+// (vmcnt(0)), a barrier, then one lane counts the block's tiles with an
+// agent-scope add; the block whose add completes the round raises the round's
+// flag with a release store (after an acquire fence, one per round: it cost
+// nothing measurable, profiles/r05_step/, where an acq_rel add in every block
+// cost ~4 %).
+// Which stores make that a hand-off:
+//   !T.wt: plain tile stores, so the lane first writes the XCD's L2 back
+//     (agent release fence) -- MI355X_MICROARCH.md's first valid producer
+//     form, ordered by the memory model (every block's release, the last
+//     block's acquire);
+//   T.wt (the step kernels, round 5): the tiles are stored write-through
+//     (sc1; the tail's few plain stores behind their own release,
+//     wt_tail_release), so once every storing wave's vmcnt(0) wait has
+//     returned the bytes are in memory and the block adds with no fence --
+//     the per-block release cost 3.5 % of the C4 rank step
+//     (tools/step_probe.hip).  The non-completing blocks' relaxed adds carry
+//     no release, so this guarantee is ISA-level (MI355X_MICROARCH.md, "Valid
+//     forms": sc1 stores, vmcnt(0), a barrier, one lane's agent-scope add;
+//     the consumers load behind a kernel boundary), not the HIP memory
+//     model's;
+//   T.sys (a peer exchange's state, read by other GPUs' copy engines over
+//     xGMI): the same at system scope -- the tiles stored sc0 sc1 (system
+//     coherent, kWtSystem) and the flag's release store system-scope; round
+//     5 kept a system release fence per block instead (T.sysfence, sc1 tile
+//     stores: now only the bench library's A/B, fa_bench_rounds_set_sys).
+// Block-uniform arguments (every thread calls it).
 __device__ __forceinline__ void step_publish(const StepTable& T, unsigned int* sig, unsigned int epoch, int k,
                                              unsigned int cnt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (T.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (T.sysfence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         else if (!T.wt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned int nk = (unsigned int)T.round_tiles[k];
@@ -1726,20 +1753,20 @@ __device__ __forceinline__ void step_tiles(const StepTable& T, unsigned int* sig
 // BAL: balanced rounds (step_tiles_bal).  One schedule per instantiation: both
 // inlined into one kernel made it ~4 % slower (code size: the unrolled tile
 // body four times over; profiles/r05_step/)
-template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false>
+template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false, int WTM = kWtAgent>
 __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const uint16_t* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a,
     const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
     unsigned int* sig, unsigned int epoch) {
     auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        bf16_tile<UB, CB, SCORED, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
-                                     outb ? outb + c0 : nullptr);
+        bf16_tile<UB, CB, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + c0 : nullptr,
+                                          outb ? outb + c0 : nullptr);
     };
     auto narrow = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        bf16_tile<US, CS, SCORED, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out + c0,
-                                     outb ? outb + c0 : nullptr);
+        bf16_tile<US, CS, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + c0 : nullptr,
+                                          outb ? outb + c0 : nullptr);
     };
     if constexpr (BAL) {
         step_tiles_bal(T, sig, epoch, wide, narrow);
@@ -1751,18 +1778,18 @@ __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     }
 }
 
-template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false>
+template <int UB, int CB, int US, int CS, bool SCORED, int B, bool BAL = false, int WTM = kWtAgent>
 __global__ __launch_bounds__(B) void k_fold_f32_step(
     const float* __restrict__ X, int64_t N, int64_t ldx, const float* __restrict__ a, const float* __restrict__ s,
     float divisor, float* __restrict__ out, StepTable T, unsigned int* sig, unsigned int epoch) {
     auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        fold_tile<UB, CB, true, SCORED, false, true, true, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+        fold_tile<UB, CB, true, SCORED, false, true, true, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
                                                                    divisor, out + c0);
     };
     auto narrow = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
-        fold_tile<US, CS, true, SCORED, false, true, true, B, true>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
+        fold_tile<US, CS, true, SCORED, false, true, true, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
                                                                    divisor, out + c0);
     };
     if constexpr (BAL) {
@@ -1810,7 +1837,7 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_bf16_scalar(
     for (int64_t i = 1; i < N; ++i)
         acc = acc + term1<SCORED>(bf2f(X[i * ldx + c]), a[i], SCORED ? s[i] : 1.0f);
     acc = acc / divisor;
-    out[c] = acc;
+    if (out) out[c] = acc;
     if (outb) outb[c] = f2bf_rne(acc);
 }
 
@@ -1903,6 +1930,12 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_int(
 // host-side dispatch
 // ---------------------------------------------------------------------------
 inline dim3 grid_for(int64_t lanes) { return dim3((unsigned)((lanes + kBlock - 1) / kBlock)); }
+
+// The output a bf16 fold's pointer checks look at: out_f32 and out_bf16 are
+// each optional (ABI 5), one of them required.
+inline const void* bf16_any_out(const float* out_f32, const uint16_t* out_bf16) {
+    return out_f32 ? static_cast<const void*>(out_f32) : static_cast<const void*>(out_bf16);
+}
 
 int check_common(int64_t N, int64_t P, int64_t ldx, const void* X, const void* a, const void* out) {
     if (N < 0 || P < 0) return fail(FA_ERR_ARG, "negative size (N=%lld, P=%lld)", (long long)N, (long long)P);
@@ -2294,7 +2327,7 @@ void launch_bf16_bands(hipStream_t st, int passes, const uint16_t* X, int64_t N,
         const int64_t c0 = b * band_tiles * to * 8;
         if (c0 >= P) break;
         const int64_t pb = (P - c0) < band_tiles * to * 8 ? (P - c0) : band_tiles * to * 8;
-        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out + c0, outb ? outb + c0 : nullptr);
+        launch_bf16_gs<U, C>(st, -1, X + c0, N, pb, ldx, a, s, d, out ? out + c0 : nullptr, outb ? outb + c0 : nullptr);
     }
 }
 
@@ -2365,20 +2398,25 @@ struct RoundsState {
     int device = 0;
     unsigned int* sig = nullptr;          // kSigWords, zeroed at creation
     unsigned int* status_host = nullptr;  // [kStatusWords] page-locked, mapped: the epoch whose round-k wait timed
-                                          // out ([kMaxRounds]: a peer exchange's buffer fence, fa_peers)
+                                          // out (fa_rounds_wait's waiter, or a peer exchange's, fa_peers)
     unsigned int* status_dev = nullptr;   // the same words as the device addresses them
     unsigned int epoch = 0;               // of the last launch (0: none yet)
     unsigned int checked = 0;             // epochs up to this one were reported by rounds_check
     int rounds = 0;                       // of the last launch
     bool launched = false;                // the last launch was enqueued
     long long max_ticks = 0;              // a waiter's give-up time in wall-clock ticks
-    bool sys = false;                     // publish rounds at system scope (a peer exchange's state)
+    int sys = 0;                          // publish rounds at system scope (a peer exchange's state): 1 = sc0 sc1
+                                          // tile stores, no per-block fence (the product); 2 = sc1 tile stores
+                                          // and a system release fence per block and round (round 5's form,
+                                          // fa_bench_rounds_set_sys A/B only); 0 = agent scope
     hipEvent_t start = nullptr;           // recorded on the launch's stream just before the launch: a waiter's
                                           // stream waits for it, so its give-up clock starts with the fold
     hipStream_t last_stream = nullptr;    // the stream of the last launch
     hipEvent_t done = nullptr;            // recorded just after the launch: the next launch with this state
                                           // waits for it, whatever stream it is on (a stream handle reused
                                           // after its stream was destroyed cannot overlap two launches)
+    hipEvent_t gate = nullptr;            // a peer exchange's state (fa_peers): recorded at the end of each
+    bool gated = false;                   // exchange, and the next launch waits for it (peer_exchange.hpp)
 };
 
 // The segments of one step launch over `rounds` slots at local columns
@@ -2502,9 +2540,11 @@ inline void rounds_state_free(RoundsState& o) {
     if (o.status_host) (void)hipHostFree(o.status_host);
     if (o.start) (void)hipEventDestroy(o.start);
     if (o.done) (void)hipEventDestroy(o.done);
+    if (o.gate) (void)hipEventDestroy(o.gate);
     o.sig = nullptr;
     o.status_host = o.status_dev = nullptr;
-    o.start = o.done = nullptr;
+    o.start = o.done = o.gate = nullptr;
+    o.gated = false;
     (void)hipSetDevice(prev);
 }
 inline int rounds_wait(RoundsState& o, int round, hipStream_t st) {
@@ -2538,7 +2578,10 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     if (rounds < 1 || rounds > kMaxRounds || !offsets) return fail(FA_ERR_ARG, "rounds must be 1..%d", kMaxRounds);
     const StepSpec& sp = kStepSpecs[f];
     const int64_t col_align = sp.bf16 ? 8 : 4;
-    if (!X || !a || !out || N < 1) return fail(FA_ERR_ARG, "null X/a/out or N < 1");
+    // fp32 rows write out; bf16 rows out and/or outb (ABI 5: out may be null)
+    if (!X || !a || N < 1 || (sp.bf16 ? (!out && !outb) : !out))
+        return fail(FA_ERR_ARG, sp.bf16 ? "null X/a, no output (out_f32 and out_bf16 both null) or N < 1"
+                                        : "null X/a/out or N < 1");
     if (ldx % col_align || !aligned16(X) || !aligned16(out) || (outb && !aligned16(outb)))
         return fail(FA_ERR_ARG, "rounds fold needs 16-B aligned X/out and ldx %% %lld == 0", (long long)col_align);
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -2551,6 +2594,8 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
     if (rc) return rc;
     T.sys = R.sys ? 1 : 0;
+    T.sysfence = R.sys == 2 ? 1 : 0;
+    const int wtm = R.sys == 1 ? kWtSystem : kWtAgent;  // the tiles' store flavour (a template argument)
     T.wt = 1;  // both step kernels store their tiles write-through (bf16_tile / fold_tile <..., WT>)
     const int64_t total = T.seg_end[T.segs - 1];
     if (grid > total) grid = total;
@@ -2559,40 +2604,51 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     // this stream, else a wait for its done event
     if (R.epoch != 0 && R.done && st != R.last_stream && hipStreamWaitEvent(st, R.done, 0) != hipSuccess)
         return check_launch("rounds fold: previous launch");
+    // a peer exchange's state: after the exchange of the previous launch
+    if (R.gated && R.gate && hipStreamWaitEvent(st, R.gate, 0) != hipSuccess)
+        return check_launch("rounds fold: previous exchange");
     if (R.start && hipEventRecord(R.start, st) != hipSuccess) return check_launch("rounds fold: start event");
     const uint16_t* Xb = static_cast<const uint16_t*>(X);
     const float* Xf = static_cast<const float*>(X);
     // the kernel instantiation is found from the form's tile shapes (never by
     // its index): a form whose shapes no instantiation below has is refused
     bool launched = false;
-#define FA_STB(UB, CB, US, CS, BAL)                                                                              \
-    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL) {     \
+#define FA_STB(UB, CB, US, CS, BAL, WTM)                                                                         \
+    if (!launched && sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL &&     \
+        wtm == WTM) {                                                                                            \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, BAL>), dim3((unsigned)grid),    \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, true, kBlock, BAL, WTM>), dim3((unsigned)grid), \
                                dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, BAL>), dim3((unsigned)grid),   \
-                               dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, R.sig, epoch);     \
+            hipLaunchKernelGGL((k_fedavg_bf16_step<UB, CB, US, CS, false, kBlock, BAL, WTM>),                    \
+                               dim3((unsigned)grid), dim3(kBlock), 0, st, Xb, N, ldx, a, s, divisor, out, outb, T, \
+                               R.sig, epoch);                                                                    \
     }
-#define FA_STF(UB, CB, US, CS, BAL)                                                                              \
-    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL) {    \
+#define FA_STF(UB, CB, US, CS, BAL, WTM)                                                                         \
+    if (!launched && !sp.bf16 && sp.ub == UB && sp.cb == CB && sp.us == US && sp.cs == CS && sp.bal == BAL &&    \
+        wtm == WTM) {                                                                                            \
         launched = true;                                                                                         \
         if (s)                                                                                                   \
-            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock, BAL>), dim3((unsigned)grid),       \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, true, kBlock, BAL, WTM>), dim3((unsigned)grid),  \
                                dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock, BAL>), dim3((unsigned)grid),      \
+            hipLaunchKernelGGL((k_fold_f32_step<UB, CB, US, CS, false, kBlock, BAL, WTM>), dim3((unsigned)grid), \
                                dim3(kBlock), 0, st, Xf, N, ldx, a, s, divisor, out, T, R.sig, epoch);           \
     }
-    FA_STB(8, 4, 8, 2, false)
-    FA_STB(8, 4, 8, 4, false)
-    FA_STB(8, 4, 8, 2, true)
-    FA_STF(8, 4, 16, 1, false)
-    FA_STF(8, 4, 16, 1, true)
+    FA_STB(8, 4, 8, 2, false, kWtAgent)
+    FA_STB(8, 4, 8, 4, false, kWtAgent)
+    FA_STB(8, 4, 8, 2, true, kWtAgent)
+    FA_STF(8, 4, 16, 1, false, kWtAgent)
+    FA_STF(8, 4, 16, 1, true, kWtAgent)
+    // system-coherent stores: the two policy forms only (a peer exchange's launches)
+    FA_STB(8, 4, 8, 2, true, kWtSystem)
+    FA_STF(8, 4, 16, 1, false, kWtSystem)
 #undef FA_STB
 #undef FA_STF
-    if (!launched) return fail(FA_ERR_ARG, "step form %s: no kernel for its tile shapes", sp.name);
+    if (!launched)
+        return fail(FA_ERR_ARG, "step form %s: no kernel for its tile shapes%s", sp.name,
+                    wtm == kWtSystem ? " with system-coherent stores (the policy forms only)" : "");
     rc = check_launch("rounds fold");
     if (rc) return rc;
     if (R.done && hipEventRecord(R.done, st) != hipSuccess)
@@ -3001,12 +3057,12 @@ inline void launch_bf16_form(Bf16Form f, hipStream_t st, const uint16_t* X, int6
 // The product bf16 fold (exact upcast, fp32 fold in order, optional RNE bf16 copy).
 inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
                      float divisor, float* out_f32, uint16_t* out_bf16, void* stream) {
-    int rc = check_common(N, P, ldx, X, a, out_f32);
+    int rc = check_common(N, P, ldx, X, a, bf16_any_out(out_f32, out_bf16));
     if (rc) return rc;
     if (P == 0) { g_err[0] = 0; return FA_OK; }
     hipStream_t st = (hipStream_t)stream;
     StreamDevice on_stream_device(stream);
-    const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && (!out_bf16 || aligned16(out_bf16));
+    const bool vec = aligned16(X) && (ldx % 8 == 0) && aligned16(out_f32) && aligned16(out_bf16);
     if (!vec) {
         if (s)
             hipLaunchKernelGGL(k_fedavg_bf16_scalar<true>, grid_for(P), dim3(kBlock), 0, st, X, N, P, ldx, a, s,
@@ -3018,7 +3074,8 @@ inline int bf16_auto(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, const
     }
     const Bf16Form policy = pick_bf16(N, P);
     const size_t xbytes = ((size_t)(N - 1) * ldx + P) * 2;
-    if (overlaps(out_f32, (size_t)P * 4, X, xbytes) || (out_bf16 && overlaps(out_bf16, (size_t)P * 2, X, xbytes))) {
+    if ((out_f32 && overlaps(out_f32, (size_t)P * 4, X, xbytes)) ||
+        (out_bf16 && overlaps(out_bf16, (size_t)P * 2, X, xbytes))) {
         launch_bf16_form(policy, st, X, N, P, ldx, a, s, divisor, out_f32, out_bf16);  // in place: one launch
         return check_launch("fedavg_bf16");
     }

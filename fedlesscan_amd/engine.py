@@ -228,16 +228,18 @@ def _check_matrix(X: torch.Tensor) -> tuple[int, int, int]:
 
 def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] = None, *,
                  out: Optional[torch.Tensor] = None, want_bf16: bool = False, total=None,
-                 exact: bool = True):
+                 exact: bool = True, out_bf16: Optional[torch.Tensor] = None):
     """FedAvg (scores None) / stall-aware fold over the rows of X, in row order.
 
     `total` overrides the divisor sum (used when zip() truncated the rows but
     the reference still divides by the sum of every weight).  Returns `out`
-    ([P] tensor in the result dtype); with bf16 input and want_bf16=True
-    returns (out_f32, out_bf16).  exact=False (fp32 only) opts into the
-    split-client fold, fa_fedavg_f32_splitn: faster on very narrow models,
-    deterministic, but NOT bit-identical to the reference (a different
-    association of the same sum).
+    ([P] tensor in the result dtype).  bf16 input: want_bf16=True returns
+    (out_f32, out_bf16); out_bf16= (a [P] bfloat16 tensor) receives the RNE
+    copy in place -- without out it is the only output (no fp32 result is
+    stored, ABI 5) and is returned alone, with out the pair is returned.
+    exact=False (fp32 only) opts into the split-client fold,
+    fa_fedavg_f32_splitn: faster on very narrow models, deterministic, but NOT
+    bit-identical to the reference (a different association of the same sum).
     """
     N, P, ldx = _check_matrix(X)
     if len(weights) != N or (scores is not None and len(scores) != N):
@@ -245,13 +247,26 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
                                          + ("" if scores is None else f" / {len(scores)} scores"))
     dev = X.device
     st = stream_ptr(dev)
+    if out_bf16 is not None and X.dtype != torch.bfloat16:
+        raise InvalidParameterShapeError("out_bf16 is for bfloat16 rows")
     if X.dtype == torch.bfloat16:
         f = Factors.weak_f32(weights, scores, total) or Factors(weights, scores, np.dtype(np.float32), total=total)
-        out = out if out is not None else torch.empty(P, dtype=torch.float32, device=dev)
-        outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
+        if out_bf16 is not None:
+            if not (out_bf16.is_cuda and out_bf16.dtype == torch.bfloat16 and out_bf16.is_contiguous()
+                    and out_bf16.numel() >= P):
+                raise ValueError(f"out_bf16 must be a contiguous CUDA bfloat16 tensor of >= {P} elements")
+            outb = out_bf16
+        else:
+            outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
+        if out is None and (outb is None or want_bf16):
+            out = torch.empty(P, dtype=torch.float32, device=dev)
         _lib.call("fa_fedavg_bf16_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div),
-                  out.data_ptr(), _ptr(outb), st)
-        return (out, outb) if want_bf16 else out
+                  _ptr(out), _ptr(outb), st)
+        if want_bf16:
+            return out, outb
+        if out_bf16 is not None:
+            return outb if out is None else (out, outb)
+        return out
     in_dt = np.dtype(_TORCH_TO_NP.get(X.dtype, np.void))
     if in_dt == np.void:
         raise InvalidParameterShapeError(f"unsupported dtype {X.dtype}")
@@ -314,35 +329,98 @@ def rounds_state(device: torch.device, stream: Optional[int] = None) -> ctypes.c
         return h
 
 
+def f32_factors(weights: Sequence, scores: Optional[Sequence] = None, total=None) -> Optional[Factors]:
+    """The float32 factors of a fold over float32 (or bf16) rows, or None when
+    numpy would promote the result (numpy-scalar weights, scores or total):
+    the weak-scalar fast path first, the type scan only when it declines."""
+    f = Factors.weak_f32(weights, scores, total)
+    if f is not None:
+        return f
+    if result_dtype(np.dtype(np.float32), list(weights), scores, total) != np.float32:
+        return None
+    return Factors(weights, scores, np.dtype(np.float32), total=total)
+
+
+class StagedFactors:
+    """Float32 factors uploaded ONCE (one H2D on the current stream) for the
+    several folds of one exchange step (fold_staged): the per-round launches
+    of ShardedAggregator read them instead of staging their own per launch."""
+
+    def __init__(self, f: Factors, device):
+        self.a, self.s = f.to(torch.device(device))
+        self.div = float(f.div)
+        self.n = len(f.a)
+
+
+def fold_staged(X: torch.Tensor, sf: StagedFactors, *, out: Optional[torch.Tensor] = None,
+                out_bf16: Optional[torch.Tensor] = None):
+    """fold_stacked with staged float32 factors: fp32 rows into out; bf16 rows
+    into out and/or out_bf16 (ABI 5).  Returns out (fp32) or out_bf16 when it
+    is the only output, else (out, out_bf16)."""
+    N, P, ldx = _check_matrix(X)
+    if N != sf.n:
+        raise InvalidParameterShapeError(f"{N} rows but {sf.n} staged factors")
+    st = stream_ptr(X.device)
+    for name, t, dt in (("out", out, torch.float32), ("out_bf16", out_bf16, torch.bfloat16)):
+        if t is not None and not (t.is_cuda and t.dtype == dt and t.is_contiguous() and t.numel() >= P):
+            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor of >= {P} elements")
+    if X.dtype == torch.bfloat16:
+        if out is None and out_bf16 is None:
+            raise ValueError("fold_staged: bf16 rows need out or out_bf16")
+        _lib.call("fa_fedavg_bf16", X.data_ptr(), N, P, ldx, sf.a.data_ptr(), _ptr(sf.s), sf.div, _ptr(out),
+                  _ptr(out_bf16), st)
+        return out_bf16 if out is None else (out if out_bf16 is None else (out, out_bf16))
+    if X.dtype != torch.float32 or out is None or out_bf16 is not None:
+        raise ValueError("fold_staged: fp32 rows fold into out (float32), no out_bf16")
+    _lib.call("fa_fedavg_f32", X.data_ptr(), N, P, ldx, sf.a.data_ptr(), _ptr(sf.s), sf.div, out.data_ptr(), st)
+    return out
+
+
 def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], offsets: Sequence[int], *,
-                out, out_bf16=None, total=None, state: Optional[ctypes.c_void_p] = None) -> ctypes.c_void_p:
+                out=None, out_bf16=None, total=None, state: Optional[ctypes.c_void_p] = None,
+                capacity: Optional[int] = None, factors: Optional[Factors] = None) -> ctypes.c_void_p:
     """Every exchange round of a step in ONE launch (fa_fedavg_*_rounds): round
     k folds the columns [offsets[k], offsets[k+1]) of X (fp32 or bf16 rows)
-    into the same columns of out (and of out_bf16, the RNE copy, for bf16 X),
-    on the current stream.  Returns the rounds state for `wait_round` (the
-    current stream's, or `state`: a peer exchange's, fa_peers_rounds): the
-    exchange of round k may start, on another stream, as soon as round k is
-    complete, while the launch goes on.  Same bits as fold_stacked on each
-    round's columns.  out / out_bf16: tensors or raw device addresses (a peer
-    exchange's send buffer)."""
+    into the same columns of out (fp32) and, for bf16 X, of out_bf16 (the RNE
+    copy), on the current stream.  fp32 X needs out; bf16 X needs out,
+    out_bf16 or both (ABI 5: a step that exchanges the bf16 copy stores no
+    fp32 result).  Returns the rounds state for `wait_round` (the current
+    stream's, or `state`: a peer exchange's, fa_peers_rounds): the exchange of
+    round k may start, on another stream, as soon as round k is complete,
+    while the launch goes on.  Same bits as fold_stacked on each round's
+    columns.  out / out_bf16: tensors (at least offsets[-1] elements) or raw
+    device addresses (a peer exchange's send buffer), which need `capacity`,
+    the elements the address holds.  factors: f32_factors(weights, scores,
+    total) when the caller has them already (one step, one rounding)."""
     N, W, ldx = _check_matrix(X)
     if len(weights) != N or (scores is not None and len(scores) != N):
         raise InvalidParameterShapeError(f"{N} rows but {len(weights)} weights")
+    end = int(offsets[-1]) if len(offsets) else 0
+    for name, t, dt in (("out", out, torch.float32), ("out_bf16", out_bf16, torch.bfloat16)):
+        if t is None:
+            continue
+        if isinstance(t, int):
+            if capacity is None or end > capacity:
+                raise ValueError(f"{name}: a raw address needs capacity >= {end} elements (got {capacity})")
+        elif not (t.is_cuda and t.dtype == dt and t.is_contiguous() and t.numel() >= end):
+            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor of >= {end} elements")
+    if out is None and (X.dtype != torch.bfloat16 or out_bf16 is None):
+        raise ValueError("fold_rounds needs out (fp32 rows) or out / out_bf16 (bf16 rows)")
     dev = X.device
-    f = Factors.weak_f32(weights, scores, total) or Factors(weights, scores, np.dtype(np.float32), total=total)
-    if result_dtype(np.dtype(np.float32), list(weights), scores, total) != np.float32:
+    f = factors if factors is not None else f32_factors(weights, scores, total)
+    if f is None:
         raise InvalidParameterShapeError("the rounds fold takes float32 factors (Python-number weights)")
-    a, s = f.to(dev)
     rounds = len(offsets) - 1
     offs = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
     st = stream_ptr(dev)
     r = state if state is not None else rounds_state(dev, st)
     addr = (lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr()))
+    # the factors from host memory: the library stages them (one C call, _hostf)
     if X.dtype == torch.bfloat16:
-        _lib.call("fa_fedavg_bf16_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
+        _lib.call("fa_fedavg_bf16_rounds_hostf", r, X.data_ptr(), N, ldx, *f.host(), float(f.div),
                   addr(out), addr(out_bf16), rounds, offs, st)
     elif X.dtype == torch.float32:
-        _lib.call("fa_fedavg_f32_rounds", r, X.data_ptr(), N, ldx, a.data_ptr(), _ptr(s), float(f.div),
+        _lib.call("fa_fedavg_f32_rounds_hostf", r, X.data_ptr(), N, ldx, *f.host(), float(f.div),
                   addr(out), rounds, offs, st)
     else:
         raise InvalidParameterShapeError(f"the rounds fold takes float32 or bfloat16 rows, got {X.dtype}")

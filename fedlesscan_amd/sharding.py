@@ -14,6 +14,7 @@ count, so 1/2/4/8 GPUs use the same code.
 from __future__ import annotations
 
 import math
+import socket
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -211,6 +212,17 @@ def gather_into(full: torch.Tensor, piece: torch.Tensor, group, async_op: bool):
     return dist.all_gather_into_tensor(full, piece, group=group, async_op=async_op)
 
 
+def _timing_pair(stream, folds):
+    """Two timing events around one fold launch on `stream`, the first recorded
+    now and both appended to `folds`; None when folds is None (not timed)."""
+    if folds is None:
+        return None
+    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    e[0].record(stream)
+    folds.append(e)
+    return e
+
+
 def device_ident(device) -> str:
     """The identity a step-form decision is keyed by: gfx arch and CU count of
     `device` ("gfx950:256"), as the tuner's cache file keys kernel forms."""
@@ -231,24 +243,24 @@ def step_key(ident: str, bf16: bool, n_clients: int, layout: "SlotLayout", excha
 
 class PeerExchange:
     """The kernel-free exchange of one rank (fa_peers, csrc/peer_exchange.hpp)
-    for one slot layout and dtype: this rank's send buffer (the step's fold
-    writes its slots there), its IPC handles all-gathered once over the group,
-    and per step a fence, the one-launch fold on the exchange's own rounds
-    state, and copy-engine pulls of every rank's round-k slot as soon as that
-    rank has completed round k.  Creating one is a collective."""
+    for one slot layout and dtype: this rank's two send buffers (step e's fold
+    writes its slots into buffer e % 2), its IPC handles all-gathered once over
+    the group, and per step the one-launch fold on the exchange's own rounds
+    state and copy pulls of every rank's round-k slot as soon as that rank has
+    completed round k.  Creating one is a collective."""
 
     def __init__(self, group, device, layout: "SlotLayout", bf16: bool):
         import ctypes
 
         from . import _lib
-        L = _lib.load()
+        L = self.L = _lib.load()
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.device = torch.device(device)
         self.layout, self.bf16 = layout, bf16
         eb = 2 if bf16 else 4
-        send_bytes = -(-layout.local_width * eb // 16) * 16
+        send_bytes = self.send_bytes = -(-layout.local_width * eb // 16) * 16
         h = ctypes.c_void_p()
         _lib.call("fa_peers_create", ctypes.byref(h), self.device.index, self.world, self.rank, send_bytes)
         self.h = h
@@ -263,29 +275,38 @@ class PeerExchange:
         joined = b"".join(every)
         _lib.call("fa_peers_open", h, ctypes.create_string_buffer(joined, len(joined)))
         self.state = ctypes.c_void_p(L.fa_peers_rounds(h))
-        self.send = int(L.fa_peers_send(h))
         R = layout.rounds
         self.offsets = [layout.offset(k) for k in range(R + 1)]
         self.src = (ctypes.c_int64 * (R + 1))(*[o * eb for o in self.offsets])
         self.dst = (ctypes.c_int64 * (R * self.world))(
             *[(layout.round_range(k)[0] + q * layout.width(k)) * eb for k in range(R) for q in range(self.world)])
 
-    def step(self, X_local, weights, scores, full, total, fold_stream_, other_stream):
-        """Fence, fold (every round in one launch) on fold_stream_, exchange on
-        other_stream into `full`; returns (event after the waits, state)."""
+    def step(self, X_local, weights, scores, full, total, fold_stream_, other_stream, factors=None,
+             fold_end: Optional[torch.cuda.Event] = None):
+        """The fold (every round in one launch) on fold_stream_ into this
+        step's send buffer, the exchange on other_stream into `full`, then
+        fold_stream_ waits for the exchange; returns (event after the waits,
+        state).  A bf16 step stores only the RNE-bf16 result it exchanges
+        (ABI 5).  No fence: the library orders the state's next fold after
+        this exchange, and the two send buffers alternate (fa_peers_send).
+        fold_end: an event recorded on fold_stream_ right after the fold."""
         from . import _lib, engine
-        _lib.call("fa_peers_fence", self.h, fold_stream_.cuda_stream)
-        if self.bf16:
-            local = torch.empty(self.layout.local_width, dtype=torch.float32, device=self.device)
-            engine.fold_rounds(X_local, weights, scores, self.offsets, out=local, out_bf16=self.send, total=total,
-                               state=self.state)
-            local.record_stream(fold_stream_)
-        else:
-            engine.fold_rounds(X_local, weights, scores, self.offsets, out=self.send, total=total, state=self.state)
+        send = int(self.L.fa_peers_send(self.h))  # this step's buffer
+        cap = self.send_bytes // (2 if self.bf16 else 4)
+        with torch.cuda.stream(fold_stream_):
+            if self.bf16:
+                engine.fold_rounds(X_local, weights, scores, self.offsets, out_bf16=send, total=total,
+                                   state=self.state, capacity=cap, factors=factors)
+            else:
+                engine.fold_rounds(X_local, weights, scores, self.offsets, out=send, total=total, state=self.state,
+                                   capacity=cap, factors=factors)
+            if fold_end is not None:
+                fold_end.record(fold_stream_)
         _lib.call("fa_peers_exchange", self.h, self.layout.rounds, self.src, full.data_ptr(), self.dst,
                   other_stream.cuda_stream)
         done = torch.cuda.Event()
         done.record(other_stream)
+        fold_stream_.wait_stream(other_stream)
         return done, self.state
 
     def close(self) -> None:
@@ -303,12 +324,12 @@ class PeerExchange:
 class ShardedAggregator:
     """Fold this rank's parameter bucket, then all-gather the global model.
 
-    `fold` maps (X_local [N, P_r], weights, scores, out=, total=, want_bf16=)
-    -> [P_r] (or (f32, bf16) with want_bf16 on bf16 input), the contract of
-    engine.fold_stacked, which is the default.  Tests on CPU (gloo) pass the
-    oracle instead.  `total` is the divisor sum over EVERY weight (the
-    reference divides by sum(weights) even where zip() truncated the rows,
-    fed_avg_aggregator.py:31-35).
+    `fold` maps (X_local [N, P_r], weights, scores, out=, total=, want_bf16=,
+    out_bf16=) -> [P_r], the contract of engine.fold_stacked, which is the
+    default (bf16 input: want_bf16 -> (f32, bf16); out_bf16 alone -> the bf16
+    result only).  Tests on CPU (gloo) pass the oracle instead.  `total` is
+    the divisor sum over EVERY weight (the reference divides by sum(weights)
+    even where zip() truncated the rows, fed_avg_aggregator.py:31-35).
 
     one_launch -- how aggregate_slots runs an exchange step's folds:
       True      one launch for every round (engine.fold_rounds), each round's
@@ -317,14 +338,23 @@ class ShardedAggregator:
       "auto"    the form recorded for this machine and shape (the tuner's
                 cache file, fa_step_lookup: a decision a probe made in an
                 earlier process or another rank's, imported), per-round
-                launches when none is recorded -- never a timing run, a
-                synchronisation or a collective of its own, so a one-call
-                process (one FaaS invocation, aggregation.py:71-75) runs the
-                recorded form from its first call;
+                launches when none is recorded -- never a timing run or a
+                synchronisation of its own, so a one-call process (one FaaS
+                invocation, aggregation.py:71-75) runs the recorded form from
+                its first call.  At world > 1 the group runs RANK 0's record:
+                the first call of a shape in a process broadcasts it (one small
+                collective per shape and process), so ranks whose cache files
+                differ (another node, a concurrent writer) still take one form
+                and issue the same collectives;
       "probe"   as "auto", but a shape with no recorded form is timed: its
                 first 2 x PROBE_CALLS calls alternate the two forms on the
                 device (max over the group's ranks), then the faster is kept
                 and recorded (fa_step_record) for later processes.
+    Every rank of a group takes the same form: the choice depends only on
+    what the ranks share (the constructor's arguments, the layout, the client
+    count, rank 0's record), and a rank whose rows cannot take the one launch
+    as they are (not 16-B aligned, a row pitch off the octet / quad grid)
+    folds an aligned copy of them instead of leaving the form.
     check -- what a one-launch step does about a round wait that timed out (a
       waiter gives up after 30 s, and the exchange behind it then reads an
       unfinished round):
@@ -343,10 +373,17 @@ class ShardedAggregator:
       "peer_copy"  each rank pulls its peers' finished slots with copy-engine
                    copies through IPC-opened buffers (PeerExchange, fa_peers):
                    no kernel beside the fold but one wave per round that polls
-                   the ranks' flags.  Needs the one-launch step on every rank
-                   (checked once per layout with a collective; otherwise
-                   "rccl"); one_launch=False keeps per-round launches with RCCL.
+                   the ranks' flags.  Needs every rank on one host (checked
+                   once per layout with a collective; otherwise "rccl");
+                   one_launch=False keeps per-round launches with RCCL.
                    close() releases the buffers (a collective).
+    trace -- None (default), or a list to which every CUDA exchange step
+      appends (fold events, end event): timing events around each fold launch
+      on the fold stream, and one on the caller's stream after the step
+      (bench.py splits a step into fold and exposed exchange with them).
+
+    A bf16 step folds in fp32 and stores only the RNE-bf16 result it exchanges
+    (ABI 5: no fp32 result is written, 2 B/param out instead of 6).
     """
 
     # calls per step form the "probe" mode times before it keeps the faster
@@ -374,8 +411,12 @@ class ShardedAggregator:
         self.one_launch = one_launch
         self.check = check
         self.ident = device_ident
+        self.trace: Optional[list] = None
         self._probe: dict = {}  # step key -> {"one": [ms], "per": [ms]} while probing
+        self.probed: dict = {}  # step key -> the same, for the probes that have decided
         self._steps: dict = {}  # step key -> True (one launch) / False (per round): decided or restored
+        self._agreed: set = set()  # step keys whose decision the group has agreed on (world > 1)
+        self._nodecision: set = set()  # agreed keys with no decision on rank 0: this rank's file is not read
         self._pending: list = []  # "deferred": (event after the waits, rounds state) per unchecked step
 
     def step_key(self, X_local: torch.Tensor, layout: "SlotLayout") -> Optional[str]:
@@ -404,12 +445,13 @@ class ShardedAggregator:
         from . import _lib
         _lib.call("fa_step_record", key.encode(), 1 if one_launch else 0)
         self._steps[key] = bool(one_launch)
+        self._nodecision.discard(key)
 
     def _lookup(self, key: Optional[str]) -> Optional[bool]:
         if key is None:
             return None
         got = self._steps.get(key)
-        if got is None:
+        if got is None and key not in self._nodecision:
             from . import _lib
             v = _lib.load().fa_step_lookup(key.encode())
             if v == -2:
@@ -417,6 +459,45 @@ class ShardedAggregator:
             if v >= 0:
                 got = self._steps[key] = bool(v)
         return got
+
+    def _backend_device(self, device) -> torch.device:
+        return torch.device(device) if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+
+    def _agree(self, key: Optional[str], device) -> None:
+        """world > 1: every rank takes rank 0's decision for `key` (one
+        broadcast, the first time this process sees the key)."""
+        if self.world == 1 or key is None or key in self._agreed:
+            return
+        got = self._lookup(key)
+        t = torch.tensor([-1 if got is None else int(got)], dtype=torch.int32, device=self._backend_device(device))
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        dist.broadcast(t, src=src, group=self.group)
+        v = int(t.item())
+        self._agreed.add(key)
+        if v < 0:
+            self._steps.pop(key, None)
+            self._nodecision.add(key)
+        else:
+            self._steps[key] = bool(v)
+            self._nodecision.discard(key)
+
+    def _form(self, X_local: torch.Tensor, layout: "SlotLayout"):
+        """(one launch?, probing) for a multi-round CUDA step: the same on
+        every rank of the group."""
+        if self.one_launch in (True, False) or not 1 < layout.rounds <= 8:
+            return self.one_launch is True, None
+        key = self.step_key(X_local, layout)
+        self._agree(key, X_local.device)
+        got = self._lookup(key)
+        if got is None and self.one_launch == "probe" and self.default_fold:
+            if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
+                self._probe.pop(next(iter(self._probe)))
+            t = self._probe.setdefault(key, {"one": [], "per": []})
+            # the form with fewer timed calls, one launch first: the schedule
+            # depends only on what every rank shares, so all time in step
+            probing = (key, "one" if len(t["one"]) <= len(t["per"]) else "per")
+            return probing[1] == "one", probing
+        return bool(got), None
 
     def bounds(self, P: int) -> Tuple[int, int]:
         return bucket_bounds(P, self.world)[self.rank]
@@ -471,74 +552,70 @@ class ShardedAggregator:
         float32 for fp32 updates; for bf16 updates the RNE bf16 model (the fold
         still accumulates in fp32), so the exchange moves 2 bytes per parameter,
         half the xGMI bytes of the fp32 result.  `fold` must accept out= (and
-        want_bf16= for bf16 input), as engine.fold_stacked does.  Raises
+        out_bf16= for bf16 input), as engine.fold_stacked does.  Raises
         AggregationError (every rank) when a one-launch step's round wait timed
         out (check="sync"; "deferred": at check_timeouts())."""
         if X_local.shape[1] != layout.local_width:
             raise ValueError(f"X_local has {X_local.shape[1]} columns, layout needs {layout.local_width}")
-        multi = 1 < layout.rounds <= 8
-        # which step form: fixed, or the recorded decision (a lookup only: no
-        # timing, synchronisation or collective unless "probe" has to measure)
-        if self.one_launch in (True, False) or not multi:
-            one, probing = self.one_launch is True, None
-        else:
-            key = self.step_key(X_local, layout)
-            got = self._lookup(key)
-            one, probing = bool(got), None
-            if got is None and self.one_launch == "probe" and X_local.is_cuda and self.default_fold:
-                if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
-                    self._probe.pop(next(iter(self._probe)))
-                t = self._probe.setdefault(key, {"one": [], "per": []})
-                # the form with fewer timed calls, one launch first; the schedule
-                # depends only on what every rank shares (layout, client count),
-                # so a rank whose buffers cannot take the one launch still times
-                # its per-round calls in step with the others
-                probing = (key, "one" if len(t["one"]) <= len(t["per"]) else "per")
-                one = probing[1] == "one"
-        if not X_local.is_cuda or layout.rounds == 1:
+        if not X_local.is_cuda or torch.cuda.is_current_stream_capturing():
+            # CPU ranks, or a HIP graph capture (the one launch refuses
+            # capture: its epochs would replay): per-round launches, nothing
+            # timed or checked
             return self._aggregate_slots(X_local, weights, scores, layout, out, total)
-        if torch.cuda.is_current_stream_capturing():
-            # a HIP graph capture: the per-round launches (the one launch
-            # refuses capture: its epochs would replay), nothing timed
-            return self._aggregate_slots(X_local, weights, scores, layout, out, total)
-        one = one and self._one_launch_ok(X_local, weights, scores, layout, total)
+        # the factors, rounded once for the whole step (numpy's weak-scalar
+        # rule, engine.f32_factors): the default fold's slots are float32 /
+        # bf16 buffers, so promoted factors (numpy-scalar weights) are refused
+        f = None
+        if self.default_fold:
+            from .aggregator.exceptions import InvalidParameterShapeError
+            from .engine import f32_factors
+            if X_local.dtype not in (torch.float32, torch.bfloat16):
+                raise InvalidParameterShapeError(f"sharded slots take float32 or bfloat16 rows, not {X_local.dtype}")
+            f = f32_factors(weights, scores, total)
+            if f is None:
+                raise InvalidParameterShapeError("weights/scores promote the float32 fold (numpy scalar types)")
+        one, probing = self._form(X_local, layout)
+        one = one and self._one_launch_ok(X_local, layout)
         # the rounds' folds on a high-priority stream of their own (fold_stream), ordered after
         # the caller's work and before the caller's later work
-        caller = torch.cuda.current_stream(X_local.device)
-        fs = fold_stream(X_local.device)
+        dev = X_local.device
+        caller = torch.cuda.current_stream(dev)
+        fs = fold_stream(dev)
         fs.wait_stream(caller)
+        folds = [] if (probing or self.trace is not None) else None  # (start, end) timing events per fold launch
         waited = None
         with torch.cuda.stream(fs):
-            if probing:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record(fs)
-            px = self._peer_exchange(X_local, weights, scores, layout, total) if (
-                one and self.exchange == "peer_copy") else None
+            if one:
+                X_local = self._aligned(X_local)
+            px = self._peer_exchange(X_local, layout) if (one and self.exchange == "peer_copy") else None
             if px is not None:
                 odt = torch.bfloat16 if px.bf16 else torch.float32
-                full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
+                full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
                 if full.dtype != odt or full.numel() < layout.padded_total or not full.is_contiguous():
                     raise ValueError(f"out needs {layout.padded_total} contiguous {odt} elements")
-                gs = gather_stream(X_local.device)
-                waited = px.step(X_local, weights, scores, full, total, fs, gs)
-                fs.wait_stream(gs)
+                e = _timing_pair(fs, folds)
+                waited = px.step(X_local, weights, scores, full, total, fs, gather_stream(dev), factors=f,
+                                 fold_end=None if e is None else e[1])
                 full = full[: layout.P]
             elif one:
-                full, waited = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total)
+                full, waited = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total, folds, f)
             else:
-                full = self._aggregate_slots(X_local, weights, scores, layout, out, total)
-            if probing:
-                ev[1].record(fs)
+                full = self._aggregate_slots(X_local, weights, scores, layout, out, total, folds, f)
         caller.wait_stream(fs)
         full.record_stream(caller)
+        if folds is not None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(caller)
+            if self.trace is not None:
+                self.trace.append((folds, end))
         if waited is not None:
             if self.check == "sync":
                 waited[0].synchronize()
-                self._raise_on_timeouts(self._timed_out([waited[1]]))
+                self._raise_on_timeouts(self._timed_out([waited[1]]), dev)
             else:
                 self._pending.append(waited)
         if probing:
-            self._record_probe(probing, ev, X_local, layout)
+            self._record_probe(probing, folds[0][0], end, X_local, layout)
         return full
 
     def _timed_out(self, states) -> int:
@@ -552,13 +629,13 @@ class ShardedAggregator:
             n += v
         return n
 
-    def _raise_on_timeouts(self, n: int) -> None:
+    def _raise_on_timeouts(self, n: int, device=None) -> None:
         """Every rank learns whether any rank's round wait timed out (MAX over
         the group) and, if one did, raises: an exchange behind that wait read
         an unfinished round, so no rank may use the gathered model."""
         if self.world > 1:
-            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
-            t = torch.tensor([n], dtype=torch.int32, device=dev)
+            dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+            t = torch.tensor([n], dtype=torch.int32, device=self._backend_device(dev))
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             n = int(t.item())
         if n:
@@ -584,60 +661,77 @@ class ShardedAggregator:
                 px.close()
         self._peers.clear()
 
-    def _peer_exchange(self, X_local, weights, scores, layout, total):
+    def _peer_exchange(self, X_local, layout):
         """This layout's PeerExchange, created on first use (a collective: the
-        ranks' handles are all-gathered, and every rank must be able to run the
-        one-launch step, else None: the RCCL exchange)."""
+        ranks' hosts are compared and their handles all-gathered), or None --
+        the RCCL exchange -- when the ranks are not all on one host (IPC
+        handles open only on the host that made them)."""
         bf16 = X_local.dtype == torch.bfloat16
         key = (tuple(layout.widths), layout.P, layout.world, bf16, X_local.device)
         if key not in self._peers:
-            ok = self._one_launch_ok(X_local, weights, scores, layout, total)
+            ok = True
             if self.world > 1:
-                t = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                                 device=X_local.device if dist.get_backend(self.group) == "nccl" else "cpu")
-                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-                ok = bool(t.item())
+                hosts = [None] * self.world
+                dist.all_gather_object(hosts, socket.gethostname(), group=self.group)
+                ok = len(set(hosts)) == 1
             self._peers[key] = PeerExchange(self.group, X_local.device, layout, bf16) if ok else None
         return self._peers[key]
 
-    def _record_probe(self, probing, ev, X_local, layout) -> None:
+    def _record_probe(self, probing, start, end, X_local, layout) -> None:
         """One timed call of the "probe" mode: its device time (max over the
         group's ranks, so every rank keeps the same form); after PROBE_CALLS
         calls of each form the faster one (best call) is recorded for the
         shape (record_step_form: this process and the cache file)."""
         key, form = probing
-        ev[1].synchronize()
-        t = torch.tensor([ev[0].elapsed_time(ev[1])], dtype=torch.float64, device=X_local.device)
+        end.synchronize()
+        t = torch.tensor([start.elapsed_time(end)], dtype=torch.float64, device=X_local.device)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         got = self._probe[key]
         got[form].append(float(t.item()))
         if len(got["one"]) >= self.PROBE_CALLS and len(got["per"]) >= self.PROBE_CALLS:
             del self._probe[key]
+            self.probed[key] = got  # what the decision saw (ms per call, max over ranks)
+            while len(self.probed) > 64:
+                self.probed.pop(next(iter(self.probed)))
             self.record_step_form(X_local, layout, min(got["one"]) <= min(got["per"]))
 
-    def _one_launch_ok(self, X_local, weights, scores, layout, total) -> bool:
-        import numpy as np
-
-        from .engine import result_dtype
+    def _one_launch_ok(self, X_local, layout) -> bool:
+        """Can the step run as one launch?  Only what every rank shares (the
+        fold, dtype, layout, client count; the factors were checked float32 by
+        the caller): a rank's own row alignment is fixed by _aligned, so the
+        ranks never split on it."""
         if not (self.default_fold and X_local.is_cuda) or not 1 < layout.rounds <= 8:
             return False
-        if X_local.dtype not in (torch.float32, torch.bfloat16) or X_local.stride(1) != 1:
+        if X_local.dtype not in (torch.float32, torch.bfloat16):
             return False
         if X_local.shape[0] < 1 or min(layout.widths) < 1:
             return False
         align = 8 if X_local.dtype == torch.bfloat16 else 4
-        if any(layout.offset(k) % align for k in range(layout.rounds)) or X_local.stride(0) % align:
-            return False
-        if X_local.data_ptr() % 16:
-            return False
-        return result_dtype(np.dtype(np.float32), list(weights), scores, total) == np.float32
+        return not any(layout.offset(k) % align for k in range(layout.rounds))
 
-    def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total):
+    @staticmethod
+    def _aligned(X_local: torch.Tensor) -> torch.Tensor:
+        """X_local, or an aligned copy of it when its rows are not 16-B aligned
+        or its pitch is off the octet (bf16) / quad (fp32) grid: the one
+        launch's 16-byte loads need both.  The copy runs on the current stream
+        (the fold stream), in order before the fold that reads it."""
+        align = 8 if X_local.dtype == torch.bfloat16 else 4
+        if (X_local.data_ptr() % 16 == 0 and X_local.stride(1) == 1
+                and (X_local.shape[0] == 1 or X_local.stride(0) % align == 0)):
+            return X_local
+        Y = torch.empty(X_local.shape, dtype=X_local.dtype, device=X_local.device)
+        Y.copy_(X_local)
+        return Y
+
+    def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total, folds=None, factors=None):
         """Every round's fold in ONE launch on the current (fold) stream; round
         k's exchange issued on the gather stream behind a wait for round k, so
-        it runs while the launch folds the later rounds.  Returns the model and
-        (an event after the last wait, the rounds state) for the timeout check."""
+        it runs while the launch folds the later rounds -- except the last
+        round's, issued on the fold stream itself right after the launch (stream
+        order is its wait: one wait kernel and one cross-stream hop fewer at the
+        end of the step).  Returns the model and (an event after the waits, the
+        rounds state) for the timeout check."""
         from . import engine
         dev = X_local.device
         bf16 = X_local.dtype == torch.bfloat16
@@ -645,23 +739,32 @@ class ShardedAggregator:
         full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
         if full.dtype != odt or full.numel() < layout.padded_total:
             raise ValueError(f"out needs {layout.padded_total} {odt} elements")
-        local = torch.empty(layout.local_width, dtype=torch.float32, device=dev)
-        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=dev) if bf16 else None
+        # what the exchange moves, and all the fold stores: the fp32 result, or
+        # for bf16 rows only its RNE-bf16 copy (no fp32 result, ABI 5)
+        send_all = torch.empty(layout.local_width, dtype=odt, device=dev)
         offs = [layout.offset(k) for k in range(layout.rounds + 1)]
-        r = engine.fold_rounds(X_local, weights, scores, offs, out=local, out_bf16=local_b, total=total)
         fs = torch.cuda.current_stream(dev)
+        e = _timing_pair(fs, folds)
+        if bf16:
+            r = engine.fold_rounds(X_local, weights, scores, offs, out_bf16=send_all, total=total, factors=factors)
+        else:
+            r = engine.fold_rounds(X_local, weights, scores, offs, out=send_all, total=total, factors=factors)
+        if e is not None:
+            e[1].record(fs)
         gs = gather_stream(dev)
-        send_all = local_b if bf16 else local
         send_all.record_stream(gs)
         works = []
         waits_done = torch.cuda.Event()
+        last = layout.rounds - 1
         for k in range(layout.rounds):
-            engine.wait_round(r, k, gs)
-            if k == layout.rounds - 1:
-                waits_done.record(gs)  # every round's wait has run (the timeout check)
             lo, hi = layout.round_range(k)
             send = send_all[layout.offset(k):layout.offset(k + 1)]
-            with torch.cuda.stream(gs):
+            if k < last:
+                engine.wait_round(r, k, gs)
+                if k == last - 1:
+                    waits_done.record(gs)  # every round's wait has run (the timeout check)
+            st = gs if k < last else fs
+            with torch.cuda.stream(st):
                 if self.world == 1:
                     full[lo:hi].copy_(send)
                     continue
@@ -673,30 +776,41 @@ class ShardedAggregator:
         fs.wait_stream(gs)
         return full[: layout.P], (waits_done, r)
 
-    def _aggregate_slots(self, X_local, weights, scores, layout, out, total):
+    def _aggregate_slots(self, X_local, weights, scores, layout, out, total, folds=None, factors=None):
         bf16 = X_local.dtype == torch.bfloat16
         odt = torch.bfloat16 if bf16 else torch.float32
         full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
         if full.dtype != odt or full.numel() < layout.padded_total:
             raise ValueError(f"out needs {layout.padded_total} {odt} elements")
-        local = torch.empty(layout.local_width, dtype=torch.float32, device=X_local.device)
-        local_b = torch.empty(layout.local_width, dtype=torch.bfloat16, device=X_local.device) if bf16 else None
+        # each round's fold writes straight into the slice the exchange sends:
+        # fp32 rows the fp32 result, bf16 rows only its RNE-bf16 copy
+        local = torch.empty(layout.local_width, dtype=odt, device=X_local.device)
+        cur = torch.cuda.current_stream(X_local.device) if X_local.is_cuda else None
+        staged = None
+        if factors is not None and X_local.is_cuda and not torch.cuda.is_current_stream_capturing():
+            # the step's factors uploaded once, for every round's launch
+            from .engine import StagedFactors
+            staged = StagedFactors(factors, X_local.device)
         works = []
         for k in range(layout.rounds):
             a, b = layout.offset(k), layout.offset(k) + layout.width(k)
             piece = local[a:b]
             if b > a:
-                if bf16:
-                    _, pb = self.fold(X_local[:, a:b], weights, scores, out=piece, total=total, want_bf16=True)
-                    local_b[a:b].copy_(pb)
+                e = _timing_pair(cur, folds) if cur is not None else None
+                if staged is not None:
+                    from .engine import fold_staged
+                    fold_staged(X_local[:, a:b], staged, **({"out_bf16": piece} if bf16 else {"out": piece}))
+                elif bf16:
+                    self.fold(X_local[:, a:b], weights, scores, out_bf16=piece, total=total)
                 else:
                     self.fold(X_local[:, a:b], weights, scores, out=piece, total=total)
-            send = local_b[a:b] if bf16 else piece
+                if e is not None:
+                    e[1].record(cur)
             lo, hi = layout.round_range(k)
             if self.world == 1:
-                full[lo:hi].copy_(send)
+                full[lo:hi].copy_(piece)
                 continue
-            w = gather_into(full[lo:hi], send, self.group, async_op=True)
+            w = gather_into(full[lo:hi], piece, self.group, async_op=True)
             if w is not None:
                 works.append(w)
         for w in works:

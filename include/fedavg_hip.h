@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 4
+#define FA_ABI_VERSION 5
 
 enum fa_status {
     FA_OK = 0,
@@ -106,7 +106,10 @@ int fa_accumulate_f32(float* acc, const float* x, float a, float s, int first, i
 int fa_finalize_f32(const float* acc, float divisor, float* out, int64_t P, void* stream);
 
 /* bf16 updates (BASELINE config 4; no reference path: defined as exact upcast
- * to f32 + the f32 fold).  out_f32 [P] required; out_bf16 [P] optional (RNE). */
+ * to f32 + the f32 fold).  out_f32 [P] (the fp32 result) and out_bf16 [P] (its
+ * RNE bf16 copy) are each optional, at least one given (ABI 5: a multi-GPU
+ * step exchanges only the bf16 copy, so it stores no fp32 result; both NULL ->
+ * FA_ERR_ARG).  The bf16 bits are the same whether out_f32 is given or not. */
 int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                    const float* a, const float* s, float divisor,
                    float* out_f32, uint16_t* out_bf16, void* stream);
@@ -146,6 +149,8 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  *     and its result must not be used (fedlesscan_amd/sharding.py raises
  *     AggregationError on every rank).
  *   fa_rounds_timeouts: (synchronous) every timed-out wait since creation.
+ *   fa_fedavg_bf16_rounds: out_f32 / out_bf16 as fa_fedavg_bf16 (ABI 5: either
+ *     may be NULL, not both).
  *   One object per launching stream (engine.py keeps one per stream object). */
 typedef struct fa_rounds fa_rounds;
 int fa_rounds_create(fa_rounds** r, int device);
@@ -163,35 +168,38 @@ int fa_rounds_timeouts(fa_rounds* r);
 /* [host] the kernel form fa_fedavg_bf16_rounds (bf16 != 0) / _f32_rounds runs */
 const char* fa_rounds_form(int bf16);
 
-/* ---- kernel-free peer exchange of a step (ABI 4) ------------------------------
+/* ---- kernel-free peer exchange of a step (ABI 4; ABI 5: no fence) ----------
  * The reference saves ONE global model per round (aggregation.py:125-138 ->
  * ParameterDao.save, client_daos.py:351-378); at N > 1 every rank folds its
  * slots and needs every other rank's.  An RCCL all-gather runs copy kernels on
  * a few CUs beside the next round's fold; here each rank PULLS its peers'
- * finished slots with hipMemcpyAsync on copy streams (the copy engines: no
- * CU) from their send buffers, opened once through IPC handles.  One object
- * per rank and layout; every call below that names a step is made by every
- * rank of the group, in the same order.
- *   fa_peers_create:  this rank's send buffer (send_bytes, 16-B multiple), its
- *                     ack words and its own rounds state (device memory)
+ * finished slots with hipMemcpyAsync on two copy streams from their send
+ * buffers, opened once through IPC handles.  One object per rank and layout;
+ * every call below that names a step is made by every rank of the group, in
+ * the same order.
+ *   fa_peers_create:  this rank's two send buffers (send_bytes each, a 16-B
+ *                     multiple; step e's fold writes buffer e % 2) and its own
+ *                     rounds state (device memory)
  *   fa_peers_handle_bytes / fa_peers_handle: [host] this rank's IPC handles
  *   fa_peers_open:    [host] every rank's handles, world x handle_bytes in rank
  *                     order (all-gathered by the caller); opens the peers'
- *   fa_peers_send:    [host] the send buffer: the step's fold writes this
- *                     rank's slots there (out_bf16 for bf16 rows, out for fp32)
+ *   fa_peers_send:    [host] the send buffer of the NEXT fold launch with
+ *                     fa_peers_rounds (ask before every step): the fold writes
+ *                     this rank's slots there (out_bf16 for bf16 rows, out for fp32)
  *   fa_peers_rounds:  [host] the rounds state (owned by the fa_peers) to pass
- *                     to fa_fedavg_*_rounds: its launches publish every round
- *                     at system scope
- *   fa_peers_fence:   enqueue on the fold stream, before the fold launch: wait
- *                     until every peer has pulled the previous step out of this
- *                     rank's send buffer
+ *                     to fa_fedavg_*_rounds: its launches store their tiles
+ *                     system-coherent and publish every round at system scope,
+ *                     and each waits for the state's previous exchange
  *   fa_peers_exchange: enqueue, after the launch, on another stream: per round
  *                     k, a wait until every rank has completed round k, then
  *                     rank q's bytes [src_offsets[k], src_offsets[k+1]) of its
- *                     send buffer are copied to dst + dst_offsets[k * world + q]
- *                     (this rank's own slot included); then this rank tells
- *                     every peer it is done reading their buffers.  A wait that
- *                     gives up is reported by fa_rounds_check(fa_peers_rounds).
+ *                     send buffer of this step are copied to dst +
+ *                     dst_offsets[k * world + q] (this rank's own slot
+ *                     included, last).  A wait that gives up is reported by
+ *                     fa_rounds_check(fa_peers_rounds).  The next fold launch
+ *                     with the state waits for this exchange; with the two
+ *                     buffers that is what keeps a buffer from being rewritten
+ *                     before every peer has pulled it (no fence, no ack)
  *   fa_peers_destroy: after every rank's last exchange (a barrier) */
 typedef struct fa_peers fa_peers;
 int fa_peers_create(fa_peers** x, int device, int world, int rank, int64_t send_bytes);
@@ -201,7 +209,6 @@ int fa_peers_handle(fa_peers* x, void* out);
 int fa_peers_open(fa_peers* x, const void* all_handles);
 void* fa_peers_send(fa_peers* x);
 fa_rounds* fa_peers_rounds(fa_peers* x);
-int fa_peers_fence(fa_peers* x, void* stream);
 int fa_peers_exchange(fa_peers* x, int rounds, const int64_t* src_offsets, void* dst, const int64_t* dst_offsets,
                       void* stream);
 
@@ -222,6 +229,15 @@ int fa_fedavg_f32_ptrs_hostf(const float* const* xi, int64_t N, int64_t P,
 int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                          const float* a, const float* s, float divisor,
                          float* out_f32, uint16_t* out_bf16, void* stream);
+/* The one-launch step with host factors (ABI 5): as fa_fedavg_*_rounds, the
+ * factors staged by the library like the folds above (one C call per step). */
+int fa_fedavg_f32_rounds_hostf(fa_rounds* r, const float* X, int64_t N, int64_t ldx,
+                               const float* a, const float* s, float divisor, float* out,
+                               int rounds, const int64_t* offsets, void* stream);
+int fa_fedavg_bf16_rounds_hostf(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx,
+                                const float* a, const float* s, float divisor,
+                                float* out_f32, uint16_t* out_bf16,
+                                int rounds, const int64_t* offsets, void* stream);
 
 /* Measured form choice.  Every kernel form of the fp32, bf16 and row-table
  * folds computes the same bits; which is fastest depends on how a shape's

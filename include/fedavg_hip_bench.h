@@ -88,7 +88,8 @@ const char* fa_ptrs_variant_name(int variant);
 /* One launch per exchange step with a chosen step form (fa_step_form_name;
  * the product's fa_fedavg_*_rounds runs the policy's form): a bench-library
  * launch state, the launch and its waiter.  X/out_bf16 are bf16 for the
- * bf16_* forms (out_bf16 may be NULL), fp32 otherwise (out_bf16 ignored). */
+ * bf16_* forms (out or out_bf16 may be NULL, not both), fp32 otherwise
+ * (out_bf16 ignored). */
 int fa_num_step_forms(void);
 const char* fa_step_form_name(int form);
 int fa_bench_rounds_create(void** r, int device);
@@ -97,6 +98,12 @@ int fa_fedavg_rounds_form(void* r, int form, const void* X, int64_t N, int64_t l
                           float divisor, float* out, uint16_t* out_bf16, int rounds, const int64_t* offsets,
                           void* stream);
 int fa_bench_rounds_wait(void* r, int round, void* stream);
+/* How the state's launches publish their rounds: 0 agent scope (the default,
+ * sc1 tile stores); 1 system scope as a peer exchange's state (fa_peers_rounds:
+ * sc0 sc1 tile stores, the policy forms only); 2 system scope as round 5 did
+ * (sc1 tile stores and a system release fence per block and round): the A/B of
+ * what the system-scope publication costs the fold (tools/peer_step_decomp.py). */
+int fa_bench_rounds_set_sys(void* r, int sys);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round 6 ad-hoc GPU steps (scripts/gpu_steps.sh): the product step against
+# bench.py's loop, and the world-1 peer-copy decomposition.
+C4R="--config c4 --params 12500000 --rounds 4 --steps 30 --warmup 5 --no-cpu-baseline"
+C3R="--config c3 --rounds 4 --steps 20 --warmup 5 --no-cpu-baseline"
+T="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread"
+case "${1:-lines}" in
+  tests)
+    scripts/gpu_steps.sh "t_shared:400:$T tests/test_gpu_shared_fold.py" "t_sharding:500:$T tests/test_gpu_sharding.py" \
+        "t_rccl:500:$T tests/test_gpu_rccl.py" ;;
+  decomp)
+    scripts/gpu_steps.sh "decomp_c4:300:python3 tools/peer_step_decomp.py --config c4" \
+        "decomp_c3:300:python3 tools/peer_step_decomp.py --config c3 --steps 5" ;;
+  lines)
+    scripts/gpu_steps.sh \
+     "c4r_prod_one_sync:300:python3 bench.py --rccl-world1 $C4R --step-mode one" \
+     "c4r_prod_one_def:300:python3 bench.py --rccl-world1 $C4R --step-mode one --check deferred" \
+     "c4r_loop_one:300:python3 bench.py --rccl-world1 $C4R --step-mode one --step-impl loop" \
+     "c4r_prod_per:300:python3 bench.py --rccl-world1 $C4R --step-mode per-round" \
+     "c4r_loop_per:300:python3 bench.py --rccl-world1 $C4R --step-mode per-round --step-impl loop" \
+     "c4r_prod_peer:300:python3 bench.py --rccl-world1 $C4R --step-mode one --exchange peer_copy" \
+     "c4r_prod_auto:300:python3 bench.py --rccl-world1 $C4R" \
+     "c3r_prod_one_sync:300:python3 bench.py --rccl-world1 $C3R --step-mode one" \
+     "c3r_prod_one_def:300:python3 bench.py --rccl-world1 $C3R --step-mode one --check deferred" \
+     "c3r_loop_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one --step-impl loop" \
+     "c3r_prod_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round" \
+     "c3r_loop_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round --step-impl loop" ;;
+  trace)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/tr_peer" \
+        -o peer --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/peer_step_decomp.py" \
+        --only fold_sys,peer_step,product_peer,product_rccl --reps 2 --steps 5 ;;
+esac

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Counter evidence for one 8-GPU C4 rank's step on one GPU:
 # 256 clients x the rank's four bf16 slots (sharding.overlap_layout(100M, 8,
-# "bf16"), 12.5M columns) through tools/exchange_interference.py with no copy:
+# "bf16"), 12.5M columns; the RNE-bf16 result only, ABI 5: 6.425 GB per step)
+# through tools/exchange_interference.py with no copy:
 # the product's one-launch step (k_fedavg_bf16_step) and the per-round policy
 # launches (k_fedavg_bf16_gs band forms), tuner off.  A kernel trace + stats,
 # an SQ pass, FETCH_SIZE and WRITE_SIZE passes (each its own rocprofv3 run),
@@ -30,12 +31,12 @@ eval timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o c4 --outp
 cd "$ROOT"
 # the one-launch step: one dispatch per step (3 warm-up + STEPS timed per step form)
 python3 scripts/pmc_traffic.py --fetch "$OUT/fetch" --write "$OUT/write" --sq "$OUT/sq" \
-    --kernel "k_fedavg_bf16_step<8, 4, 8, 2" --bytes 6475000000 \
+    --kernel "k_fedavg_bf16_step<8, 4, 8, 2" --bytes 6425000000 \
     --provenance "rocprofv3 passes of tools/exchange_interference.py --config c4 (no copy), round $TAG, commit $COMMIT, $(date -u +%Y-%m-%dT%H:%MZ)" \
     --out "$OUT/pmc_c4_rank_step.json"
 # the per-round policy launches: 3 + 2 warm-up + STEPS timed steps, several band dispatches each
 python3 scripts/pmc_traffic.py --fetch "$OUT/fetch" --write "$OUT/write" --sq "$OUT/sq" \
-    --kernel "k_fedavg_bf16_gs" --bytes 6475000000 --calls $((5 + STEPS)) \
+    --kernel "k_fedavg_bf16_gs" --bytes 6425000000 --calls $((5 + STEPS)) \
     --provenance "rocprofv3 passes of tools/exchange_interference.py --config c4 (no copy), round $TAG, commit $COMMIT, $(date -u +%Y-%m-%dT%H:%MZ)" \
     --out "$OUT/pmc_c4_rank_perround.json"
 echo done

@@ -112,3 +112,36 @@ def test_rccl_world1_slots_and_layers_bit_exact():
     exp_layers = G.expected("f32_small", "fedavg")
     assert len(got["layers"]) == len(exp_layers)
     assert all(a.shape == b.shape and G.same_bits(a, b) for a, b in zip(got["layers"], exp_layers))
+
+
+@pytest.mark.parametrize("impl,extra", [("product", []), ("product", ["--check", "deferred"]),
+                                        ("product", ["--exchange", "peer_copy", "--step-mode", "one"]),
+                                        ("loop", [])])
+@pytest.mark.parametrize("config", ["c4", "c3"])
+def test_bench_times_the_shipped_class(config, impl, extra):
+    """bench.py under a one-rank nccl group (--rccl-world1): the default
+    --step-impl product times ShardedAggregator.aggregate_slots itself (VERDICT
+    r5 next #1), --step-impl loop bench.py's own step; both reassemble the
+    model the per-round folds give (gather_check), with no round-wait timeout,
+    and a bf16 step stores only the bf16 copy (ABI 5)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    params = "2000000" if config == "c4" else "500000"
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--rccl-world1", "--config", config, "--params", params,
+           "--clients", "64", "--steps", "3", "--warmup", "5", "--no-cpu-baseline", "--step-impl", impl, *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["gather_check"] is True and line["round_wait_timeouts"] == 0
+    cfg = line["config"]
+    assert cfg["step_impl"].startswith("product: ShardedAggregator") == (impl == "product")
+    if impl == "product":
+        assert ("check='deferred'" in cfg["step_impl"]) == ("deferred" in extra)
+    if config == "c4":
+        assert cfg["outputs"].startswith("RNE bf16 only")
+        assert line["roofline"]["bytes_per_launch"] == 64 * line["config"]["params_per_gpu"] * 2 + \
+            line["config"]["params_per_gpu"] * 2
+    if "peer_copy" in extra:
+        assert cfg["exchange"] == "peer_copy"

@@ -183,15 +183,27 @@ def test_round_wait_timeout_raises_on_every_path(monkeypatch):
     sc = _scores(seed, N)
     monkeypatch.setattr(engine, "_rounds_states", {})  # fresh states read the limit
     monkeypatch.setenv("FEDAVG_ROUND_WAIT_US", "1")
+    busy = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+
+    def hold_the_fold():
+        # ~5 ms of work ahead of the step on the caller's stream: the fold (and
+        # the waiters' clocks, which start with it) begins only after the host
+        # has enqueued the whole step, so every wait sees an unfinished round
+        # however slowly this process issues its first calls
+        for _ in range(24):
+            busy.fill_(1.0)
+    hold_the_fold()
     with pytest.raises(AggregationError, match="timed out"):
         ShardedAggregator(one_launch=True).aggregate_slots(X, w, sc, lay)
     deferred = ShardedAggregator(one_launch=True, check="deferred")
+    hold_the_fold()
     out = deferred.aggregate_slots(X, w, sc, lay)
     assert out.dtype == torch.bfloat16
     with pytest.raises(AggregationError, match="timed out"):
         deferred.check_timeouts()
     deferred.check_timeouts()  # nothing left unchecked
     torch.cuda.synchronize()
+    del busy
     monkeypatch.setattr(engine, "_rounds_states", {})
     monkeypatch.delenv("FEDAVG_ROUND_WAIT_US")
     agg = ShardedAggregator(one_launch=True)
@@ -287,7 +299,19 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl"):
+def _misaligned(X):
+    """The same values in a view that is NOT 16-B aligned and whose row pitch
+    is off the quad / octet grid (one element of padding per row, one of
+    offset): the one launch cannot read it as it is."""
+    N, W = X.shape
+    base = torch.empty(N * (W + 1) + 1, dtype=X.dtype, device=X.device)
+    V = base[1:].view(N, W + 1)[:, :W]
+    V.copy_(X)
+    assert V.data_ptr() % 16 != 0 and V.stride(0) % 4 != 0
+    return V
+
+
+def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl", misalign=False):
     import torch as T
     import torch.distributed as dist
     from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
@@ -310,7 +334,18 @@ def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl"):
         sc = _scores(seed, N)
         Xin = X.view(T.bfloat16) if bf16 else X
         outs = []
-        if exchange == "rccl":
+        if misalign:
+            # rank 1 hands over rows the one launch cannot
+            # read as they are; the group still takes one form (rank 1 folds
+            # an aligned copy), so every rank issues the same collectives --
+            # the sync check's all-reduce included -- and nobody hangs
+            if rank == 1:
+                Xin = _misaligned(Xin)
+            agg = ShardedAggregator(one_launch=True, exchange=exchange)
+            fulls = [agg.aggregate_slots(Xin, w, sc, lay) for _ in range(3)]
+            outs = [f.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes() for f in fulls]
+            agg.close()
+        elif exchange == "rccl":
             agg = ShardedAggregator(one_launch="probe")  # the probe's all-reduce runs over the group
             for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
                 full = agg.aggregate_slots(Xin, w, sc, lay)
@@ -336,19 +371,21 @@ def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl"):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("misalign", [False, True])
 @pytest.mark.parametrize("exchange", ["rccl", "peer_copy"])
 @pytest.mark.parametrize("bf16", [False, True])
-def test_two_ranks_on_one_gpu(bf16, exchange):
+def test_two_ranks_on_one_gpu(bf16, exchange, misalign):
     """Two ranks share the GPU over gloo: the slot exchange through the group
     ("rccl": gloo host-staged here), or the kernel-free peer copy (IPC handles
-    of the same device, cross-process flags and acks), bit-exact."""
+    of the same device, cross-process flags and acks), bit-exact; misalign:
+    rank 1's rows are a 16-B-misaligned view."""
     import torch.multiprocessing as mp
     from oracle import fedavg_oracle as O
     N, P, rounds, seed, world = 17, 20011, 3, 8, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, N, P, rounds, seed, bf16, q, exchange))
+    procs = [ctx.Process(target=_rank, args=(r, world, port, N, P, rounds, seed, bf16, q, exchange, misalign))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -64,6 +64,24 @@ def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
                                            None if ob is None else ob.data_ptr(), lay.rounds, offs, st.cuda_stream),
                    "step form", bench=True)
         res[name] = (o.cpu().numpy(), None if ob is None else ob.cpu().numpy().view(np.uint16))
+        if bf16:  # ABI 5: the bf16 result alone, no fp32 output
+            ob2 = torch.zeros((W,), dtype=torch.int16, device=dev)
+            _lib.check(B.fa_fedavg_rounds_form(rb, f, X.data_ptr(), N, W, a.data_ptr(), sp, div, None, ob2.data_ptr(),
+                                               lay.rounds, offs, st.cuda_stream), "step form, bf16 only", bench=True)
+            res[name + " bf16 only"] = (None, ob2.cpu().numpy().view(np.uint16))
+    # the policy form publishing at system scope: sc0 sc1 tile stores (a peer
+    # exchange's launches, sys 1) and round 5's per-block fence (sys 2)
+    pol = L.fa_rounds_form(1 if bf16 else 0).decode()
+    fpol = next(f for f in range(B.fa_num_step_forms()) if B.fa_step_form_name(f).decode() == pol)
+    for sysm in (1, 2):
+        _lib.check(B.fa_bench_rounds_set_sys(rb, sysm), "sys", bench=True)
+        o = torch.full((W,), float("nan"), dtype=torch.float32, device=dev)
+        ob = torch.zeros((W,), dtype=torch.int16, device=dev) if bf16 else None
+        _lib.check(B.fa_fedavg_rounds_form(rb, fpol, X.data_ptr(), N, W, a.data_ptr(), sp, div,
+                                           None if bf16 else o.data_ptr(), None if ob is None else ob.data_ptr(),
+                                           lay.rounds, offs, st.cuda_stream), f"policy form sys {sysm}", bench=True)
+        res[f"{pol} sys {sysm}"] = (None if bf16 else o.cpu().numpy(),
+                                    None if ob is None else ob.cpu().numpy().view(np.uint16))
     _lib.check(B.fa_bench_rounds_destroy(rb), "destroy", bench=True)
     r = ctypes.c_void_p()
     _lib.check(L.fa_rounds_create(ctypes.byref(r), dev.index), "fa_rounds_create")
@@ -74,9 +92,10 @@ def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
         if ob is not None:
             ob.fill_(-1)
         got = torch.full((W,), -1, dtype=torch.int16 if bf16 else torch.int32, device=dev)
-        if bf16:
-            rc = L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, W, a.data_ptr(), sp, div, o.data_ptr(), ob.data_ptr(),
-                                         lay.rounds, offs, st.cuda_stream)
+        if bf16:  # reps 2-3 store the bf16 result alone (ABI 5: out_f32 NULL)
+            rc = L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, W, a.data_ptr(), sp, div,
+                                         o.data_ptr() if rep < 2 else None, ob.data_ptr(), lay.rounds, offs,
+                                         st.cuda_stream)
         else:
             rc = L.fa_fedavg_f32_rounds(r, X.data_ptr(), N, W, a.data_ptr(), sp, div, o.data_ptr(), lay.rounds, offs,
                                         st.cuda_stream)
@@ -88,7 +107,11 @@ def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
                 a0, a1 = lay.offset(k), lay.offset(k + 1)
                 got[a0:a1].copy_(src[a0:a1])
         torch.cuda.synchronize()
-        res[f"product rounds rep {rep}"] = (o.cpu().numpy(), ob.cpu().numpy().view(np.uint16) if bf16 else None)
+        if bf16 and rep >= 2:
+            assert np.isnan(o.cpu().numpy()).all()  # no fp32 store at all
+            res[f"product rounds rep {rep}"] = (None, ob.cpu().numpy().view(np.uint16))
+        else:
+            res[f"product rounds rep {rep}"] = (o.cpu().numpy(), ob.cpu().numpy().view(np.uint16) if bf16 else None)
         g = got.cpu().numpy()
         res[f"copied behind the waits rep {rep}"] = ((None, g.view(np.uint16)) if bf16 else (g.view(np.float32), None))
     assert L.fa_rounds_timeouts(r) == 0 and L.fa_rounds_check(r) == 0
@@ -279,3 +302,45 @@ def test_rounds_entry_errors(dev, libs):
     assert rc == _lib.FA_ERR_ARG
     assert L.fa_rounds_timeouts(r) == 0 and L.fa_rounds_check(r) == 0
     _lib.check(L.fa_rounds_destroy(r), "destroy")
+
+
+@pytest.mark.parametrize("P", [8 * 3000 + 5, 1_000_003, 12_500_000])
+def test_bf16_result_alone(dev, libs, P):
+    """ABI 5: a bf16 fold stores the fp32 result, the RNE-bf16 copy or both,
+    and the bf16 bits are the same either way (engine.fold_stacked(out_bf16=)
+    is the per-round exchange step's call; the rounds entry: above).  Neither
+    output is an argument error, not a launch."""
+    from fedlesscan_amd import engine
+    _lib, L, B = libs
+    N, seed = 64, 71
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ldx = (P + 63) // 64 * 64
+    X = torch.empty((N, ldx), dtype=torch.bfloat16, device=dev)
+    _lib.check(B.fa_synth_bf16(X.data_ptr(), N, ldx, ldx, seed, 0, 0, st), "synth", bench=True)
+    w = synth.cardinalities(seed, N)
+    sc = [(r + 1) / 11 for r in synth.round_ids(seed, N, 10, 2)]
+    both_f, both_b = engine.fold_stacked(X[:, :P], w, sc, want_bf16=True)
+    alone = torch.full((P,), -1, dtype=torch.int16, device=dev).view(torch.bfloat16)
+    got = engine.fold_stacked(X[:, :P], w, sc, out_bf16=alone)
+    assert got is alone
+    f_only = engine.fold_stacked(X[:, :P], w, sc)
+    torch.cuda.synchronize()
+    c = min(P, 1 << 20)
+    ef, eb = OL.fedavg_bf16(OL.synth_bf16(seed, N, c), np.array(w, np.float32), np.float32(sum(w)),
+                            s=np.array(sc, np.float32))
+    bits = alone.view(torch.int16).cpu().numpy().view(np.uint16)
+    assert np.array_equal(bits[:c], eb)
+    assert np.array_equal(bits, both_b.view(torch.int16).cpu().numpy().view(np.uint16))
+    assert _same(both_f.cpu().numpy()[:c], ef) and _same(f_only.cpu().numpy(), both_f.cpu().numpy())
+    a = torch.tensor(np.array(w, np.float32), device=dev)
+    rc = L.fa_fedavg_bf16(X.data_ptr(), N, P, ldx, a.data_ptr(), None, float(sum(w)), None, None, st)
+    assert rc == _lib.FA_ERR_ARG
+    import ctypes
+    r = ctypes.c_void_p()
+    _lib.check(L.fa_rounds_create(ctypes.byref(r), dev.index), "create")
+    offs = (ctypes.c_int64 * 2)(0, P // 8 * 8)
+    assert L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, ldx, a.data_ptr(), None, 1.0, None, None, 1, offs,
+                                   st) == _lib.FA_ERR_ARG
+    _lib.check(L.fa_rounds_destroy(r), "destroy")
+    with pytest.raises(ValueError):
+        engine.fold_rounds(X, w, sc, [0, P // 8 * 8])  # neither output

@@ -118,16 +118,20 @@ def test_library_argument_errors_need_no_gpu():
 
 
 def test_exchange_entry_argument_errors_need_no_gpu():
-    """ABI 4's multi-GPU entries validate before any HIP call: bad peer-group
-    shapes, null handles, malformed step-form keys."""
+    """The multi-GPU entries validate before any HIP call: bad peer-group
+    shapes, null handles, malformed step-form keys (ABI 5: no peer fence; the
+    rounds entries with host factors)."""
     L = _lib.load()
     h = ctypes.c_void_p()
     for world, rank, nbytes in ((0, 0, 64), (17, 0, 64), (2, 2, 64), (2, -1, 64), (2, 0, 8), (2, 0, 100)):
         assert L.fa_peers_create(ctypes.byref(h), 0, world, rank, nbytes) == _lib.FA_ERR_ARG, (world, rank, nbytes)
         assert h.value is None
     assert L.fa_peers_create(None, 0, 2, 0, 64) == _lib.FA_ERR_ARG
-    assert L.fa_peers_handle_bytes() == 3 * 64  # three hipIpcMemHandle_t
-    assert L.fa_peers_fence(None, None) == _lib.FA_ERR_ARG
+    assert L.fa_peers_handle_bytes() == 2 * 64  # two hipIpcMemHandle_t: the send buffers, the signal words
+    assert "fa_peers_fence" not in _lib.header_functions()  # ABI 5: the double-buffered exchange needs none
+    assert L.fa_fedavg_f32_rounds_hostf(None, None, 1, 4, None, None, 1.0, None, 1, None, None) == _lib.FA_ERR_ARG
+    assert L.fa_fedavg_bf16_rounds_hostf(None, None, 1, 8, None, None, 1.0, None, None, 1, None, None) == \
+        _lib.FA_ERR_ARG
     assert L.fa_peers_exchange(None, 1, None, None, None, None) == _lib.FA_ERR_ARG
     assert L.fa_peers_send(None) is None and L.fa_peers_rounds(None) is None
     assert L.fa_peers_destroy(None) == _lib.FA_OK

@@ -119,7 +119,7 @@ def _free_port():
     return p
 
 
-def _oracle_fold(X, w, s=None, out=None, total=None, want_bf16=False):
+def _oracle_fold(X, w, s=None, out=None, total=None, want_bf16=False, out_bf16=None):
     """engine.fold_stacked's contract, computed by the oracle (CPU ranks)."""
     from oracle import fedavg_oracle as O
     if X.dtype == torch.bfloat16:
@@ -132,6 +132,9 @@ def _oracle_fold(X, w, s=None, out=None, total=None, want_bf16=False):
     if out is not None:
         out.copy_(res)
         res = out
+    if out_bf16 is not None:
+        out_bf16.copy_(resb)
+        return out_bf16 if out is None else (res, out_bf16)
     return (res, resb) if want_bf16 else res
 
 
@@ -295,6 +298,50 @@ def test_step_form_restored_in_a_new_process_without_probing(tmp_path):
         form, used, out = got[r]
         assert form == "one launch" and used == [], (r, form, used)
         assert np.array_equal(np.frombuffer(out, dtype=np.uint32), exp.view(np.uint32)), r
+
+
+def _agree_worker(rank, world, port, cache, case, q):
+    """Ranks with DIFFERENT cache files (another node, a concurrent writer):
+    the first step of a shape takes rank 0's record on every rank."""
+    os.environ["FEDAVG_TUNE_CACHE"] = cache
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lay = SlotLayout(40_000, world, 4)
+        X = torch.zeros((9, lay.local_width))
+        mine = {"both": [True, False, False][rank], "rank0_none": [None, True, False][rank]}[case]
+        agg = ShardedAggregator(fold=_oracle_fold, device_ident="cputest:1")
+        if mine is not None:
+            agg.record_step_form(X, lay, one_launch=mine)
+        fresh = ShardedAggregator(fold=_oracle_fold, device_ident="cputest:1")  # a later call's aggregator
+        first = fresh._form(X, lay)
+        again = fresh._form(X, lay)  # agreed once: no second collective (the group would hang if ranks differed)
+        q.put((rank, (first, again, fresh.step_form(X, lay))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["both", "rank0_none"])
+def test_step_form_is_rank0s_on_every_rank(tmp_path, case):
+    """the step form is a group decision.  Rank 0 records
+    one launch and ranks 1-2 per round (or rank 0 nothing): every rank runs
+    rank 0's form, so none issues a collective the others do not."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, str(tmp_path / f"t{r}.txt"), case, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = (True, None) if case == "both" else (False, None)
+    form = "one launch" if case == "both" else None
+    for r in range(world):
+        assert got[r] == (want, want, form), (r, got[r])
 
 
 def test_step_keys_and_modes():

@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--copy", default="kernel", choices=["kernel", "sdma"],
                     help="kernel: fa_bench_copy_f32 on --blocks blocks; sdma: hipMemcpyAsync from page-locked "
                          "host memory on the copy stream (copy engines, no CUs)")
+    ap.add_argument("--with-f32", action="store_true",
+                    help="bf16: also store the fp32 result (round 5's steps); by default a bf16 step stores only the "
+                         "RNE-bf16 copy it exchanges, as ShardedAggregator does (ABI 5)")
     args = ap.parse_args()
     if args.copy == "sdma":
         args.host_src = True
@@ -84,6 +87,10 @@ def main():
     div = float(np.float32(sum(w)))
     out = torch.empty(W, dtype=torch.float32, device=dev)
     outb = torch.empty(W, dtype=torch.bfloat16, device=dev) if dt == "bf16" else None
+    f32_out = dt == "f32" or args.with_f32  # bf16 exchange steps store only the bf16 copy (ABI 5)
+
+    def optr(off=0):
+        return out.data_ptr() + off * 4 if f32_out else None
     recv = max(lay.widths) * (args.world - 1) * out_esz // 4 * 4  # floats moved per round, at most
     src = (torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, pin_memory=True) if args.host_src else
            torch.empty(recv // 4 * 4 + 4, dtype=torch.float32, device=dev))
@@ -136,14 +143,14 @@ def main():
             _lib.check(rc, "form", bench=True)
             return
         if forced:
-            rc = B.fa_fedavg_bf16_form(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+            rc = B.fa_fedavg_bf16_form(x, N, width, W, a.data_ptr(), None, div, optr(off),
                                        outb.data_ptr() + off * 2, fs.cuda_stream, form[0])
             _lib.check(rc, "form", bench=True)
             return
         if dt == "f32":
             rc = L.fa_fedavg_f32(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4, fs.cuda_stream)
         else:
-            rc = L.fa_fedavg_bf16(x, N, width, W, a.data_ptr(), None, div, out.data_ptr() + off * 4,
+            rc = L.fa_fedavg_bf16(x, N, width, W, a.data_ptr(), None, div, optr(off),
                                   outb.data_ptr() + off * 2, fs.cuda_stream)
         _lib.check(rc, "fold")
 
@@ -175,12 +182,12 @@ def main():
                 rc = L.fa_fedavg_f32_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, out.data_ptr(),
                                             lay.rounds, offs, fs.cuda_stream)
             else:
-                rc = L.fa_fedavg_bf16_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, out.data_ptr(),
+                rc = L.fa_fedavg_bf16_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, optr(),
                                              outb.data_ptr(), lay.rounds, offs, fs.cuda_stream)
             _lib.check(rc, "rounds fold")
         else:
             rc = B.fa_fedavg_rounds_form(rs_bench, step_names[sform], X.data_ptr(), N, W, a.data_ptr(), None, div,
-                                         out.data_ptr(), None if outb is None else outb.data_ptr(), lay.rounds, offs,
+                                         optr(), None if outb is None else outb.data_ptr(), lay.rounds, offs,
                                          fs.cuda_stream)
             _lib.check(rc, "rounds form", bench=True)
         ev[0][1].record(fs)
