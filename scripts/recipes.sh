@@ -41,7 +41,9 @@ case "$recipe" in
   rehearse_w8)
     steps=("rehearse_c3_w8:400:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c3 --clients 16 --steps 2 --warmup 1 --no-cpu-baseline"
            "rehearse_c4_w8:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline"
-           "rehearse_c4_w8_perround:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline --per-round-launches") ;;
+           "rehearse_c4_w8_perround:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline --per-round-launches"
+           "rehearse_peer_w8:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 3 --warmup 1 --no-cpu-baseline --exchange peer_copy --step-mode one"
+           "rehearse_c4_w8_loop:600:FEDAVG_BENCH_BACKEND=gloo python3 bench.py --gpus 8 --config c4 --steps 2 --warmup 1 --no-cpu-baseline --step-impl loop") ;;
   c4_rank)
     steps=("c4_rank_one:300:python3 bench.py --rccl-world1 $C4R --step-mode one"
            "c4_rank_perround:300:python3 bench.py --rccl-world1 $C4R --per-round-launches"
