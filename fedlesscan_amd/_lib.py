@@ -54,10 +54,10 @@ _PROTOS = {
     "fa_fedavg_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
     "fa_rounds_create": (_int, [_vp, _int]),
     "fa_rounds_destroy": (_int, [_vp]),
-    "fa_fedavg_f32_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
-    "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
-    "fa_fedavg_f32_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp]),
-    "fa_fedavg_bf16_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp]),
+    "fa_fedavg_f32_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp, _vp]),
+    "fa_fedavg_bf16_rounds": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp, _vp]),
+    "fa_fedavg_f32_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _int, _vp, _vp, _vp]),
+    "fa_fedavg_bf16_rounds_hostf": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _int, _vp, _vp, _vp]),
     "fa_rounds_wait": (_int, [_vp, _int, _vp]),
     "fa_rounds_check": (_int, [_vp]),
     "fa_rounds_timeouts": (_int, [_vp]),

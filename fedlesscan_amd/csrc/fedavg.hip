@@ -17,23 +17,29 @@ namespace {
 // ---- per-client factors handed over in HOST memory (the *_hostf entries) ----
 // The reference's weights are Python numbers; its caller has them on the host.
 // A ring of slots per device, each a page-locked buffer, a device buffer and
-// an event: the factors are copied into the slot's pinned buffer, travel in
-// one async H2D on the caller's stream, the fold reads the device copy, and
-// an event recorded after the fold guards the slot, which is reused only
-// after that fold has completed.  One C call instead of an allocation, a
-// copy and an event from the host language per fold.
+// two events: the factors are copied into the slot's pinned buffer and travel
+// in one async H2D on the ring's own staging stream, so the copy (a small
+// blit kernel) runs beside whatever the caller's stream is still doing, and
+// the caller's stream waits for it (an event: no dispatch of its own in front
+// of the fold -- on the fold's stream it cost a kernel and ~15 us of dispatch
+// gaps per step, profiles/r06_peer/); the fold reads the device copy, and an
+// event recorded after the fold guards the slot, which is reused only after
+// that fold has completed.  One C call instead of an allocation, a copy and an
+// event from the host language per fold.
 constexpr int kFactorSlots = 8;
 struct FactorSlot {
     float* host = nullptr;
     float* dev = nullptr;
     size_t cap = 0;  // floats
-    hipEvent_t done = nullptr;
+    hipEvent_t ready = nullptr;  // the slot's H2D has completed (staging stream)
+    hipEvent_t done = nullptr;   // the fold that read the slot has completed (caller's stream)
     bool pending = false;
 };
 struct FactorRing {
     std::mutex mu;
     FactorSlot slot[kFactorSlots];
     int next = 0;
+    hipStream_t stage = nullptr;  // the H2D copies' stream (created on first use, per device)
 };
 FactorRing g_factor_rings[16];
 
@@ -117,11 +123,19 @@ int with_host_factors(const float* a, const float* s, int64_t N, void* stream, L
     }
     if (!S.done) {
         hipError_t e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.ready, hipEventDisableTiming);
         if (e != hipSuccess) return fail(FA_ERR_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+    }
+    if (!R.stage) {
+        hipError_t e = hipStreamCreateWithFlags(&R.stage, hipStreamNonBlocking);
+        if (e != hipSuccess) return fail(FA_ERR_HIP, "factor staging stream: %s", hipGetErrorString(e));
     }
     memcpy(S.host, a, (size_t)N * sizeof(float));
     if (s) memcpy(S.host + N, s, (size_t)N * sizeof(float));
-    hipError_t e = hipMemcpyAsync(S.dev, S.host, need * sizeof(float), hipMemcpyHostToDevice, st);
+    // the device buffer is free: the fold that last read it has completed (S.done, above)
+    hipError_t e = hipMemcpyAsync(S.dev, S.host, need * sizeof(float), hipMemcpyHostToDevice, R.stage);
+    if (e == hipSuccess) e = hipEventRecord(S.ready, R.stage);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, S.ready, 0);
     if (e != hipSuccess) return fail(FA_ERR_HIP, "factor H2D: %s", hipGetErrorString(e));
     const int rc = launch((const float*)S.dev, s ? (const float*)(S.dev + N) : (const float*)nullptr);
     e = hipEventRecord(S.done, st);
@@ -283,19 +297,20 @@ int fa_rounds_destroy(fa_rounds* r) {
 
 int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx, const float* a, const float* s,
                           float divisor, float* out_f32, uint16_t* out_bf16, int rounds, const int64_t* offsets,
-                          void* stream) {
+                          const int64_t* out_offsets, void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
     StreamDevice on_stream_device(stream);
     return launch_step(*r, pick_step(true), (hipStream_t)stream, X, N, ldx, a, s, divisor, out_f32, out_bf16,
-                       rounds, offsets);
+                       rounds, offsets, out_offsets);
 }
 
 int fa_fedavg_f32_rounds(fa_rounds* r, const float* X, int64_t N, int64_t ldx, const float* a, const float* s,
-                         float divisor, float* out, int rounds, const int64_t* offsets, void* stream) {
+                         float divisor, float* out, int rounds, const int64_t* offsets, const int64_t* out_offsets,
+                         void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
     StreamDevice on_stream_device(stream);
     return launch_step(*r, pick_step(false), (hipStream_t)stream, X, N, ldx, a, s, divisor, out, nullptr, rounds,
-                       offsets);
+                       offsets, out_offsets);
 }
 
 const char* fa_rounds_form(int bf16) { return step_form_name(pick_step(bf16 != 0)); }
@@ -504,19 +519,21 @@ int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx, c
 }
 
 int fa_fedavg_f32_rounds_hostf(fa_rounds* r, const float* X, int64_t N, int64_t ldx, const float* a, const float* s,
-                               float divisor, float* out, int rounds, const int64_t* offsets, void* stream) {
+                               float divisor, float* out, int rounds, const int64_t* offsets,
+                               const int64_t* out_offsets, void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
     return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
-        return fa_fedavg_f32_rounds(r, X, N, ldx, ad, sd, divisor, out, rounds, offsets, stream);
+        return fa_fedavg_f32_rounds(r, X, N, ldx, ad, sd, divisor, out, rounds, offsets, out_offsets, stream);
     });
 }
 
 int fa_fedavg_bf16_rounds_hostf(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx, const float* a,
                                 const float* s, float divisor, float* out_f32, uint16_t* out_bf16, int rounds,
-                                const int64_t* offsets, void* stream) {
+                                const int64_t* offsets, const int64_t* out_offsets, void* stream) {
     if (!r) return fail(FA_ERR_ARG, "null fa_rounds");
     return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {
-        return fa_fedavg_bf16_rounds(r, X, N, ldx, ad, sd, divisor, out_f32, out_bf16, rounds, offsets, stream);
+        return fa_fedavg_bf16_rounds(r, X, N, ldx, ad, sd, divisor, out_f32, out_bf16, rounds, offsets, out_offsets,
+                                     stream);
     });
 }
 

@@ -1565,6 +1565,8 @@ constexpr int kMaxRounds = 8, kMaxSegs = 3 * kMaxRounds;
 struct StepTable {
     int64_t seg_end[kMaxSegs];
     int64_t col0[kMaxSegs];
+    int64_t ocol0[kMaxSegs];  // the output column of segment g's first column: col0[g], or where the caller
+                              // maps its round (out_offsets: a rank's slots straight into the gathered model)
     int64_t width[kMaxSegs];
     int32_t round[kMaxSegs];
     int32_t small[kMaxSegs];
@@ -1759,14 +1761,14 @@ __global__ __launch_bounds__(B) void k_fedavg_bf16_step(
     const float* __restrict__ s, float divisor, float* __restrict__ out, uint16_t* __restrict__ outb, StepTable T,
     unsigned int* sig, unsigned int epoch) {
     auto wide = [&](int g, int64_t bid) {
-        const int64_t c0 = T.col0[g];
-        bf16_tile<UB, CB, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + c0 : nullptr,
-                                          outb ? outb + c0 : nullptr);
+        const int64_t c0 = T.col0[g], o0 = T.ocol0[g];
+        bf16_tile<UB, CB, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + o0 : nullptr,
+                                          outb ? outb + o0 : nullptr);
     };
     auto narrow = [&](int g, int64_t bid) {
-        const int64_t c0 = T.col0[g];
-        bf16_tile<US, CS, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + c0 : nullptr,
-                                          outb ? outb + c0 : nullptr);
+        const int64_t c0 = T.col0[g], o0 = T.ocol0[g];
+        bf16_tile<US, CS, SCORED, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, divisor, out ? out + o0 : nullptr,
+                                          outb ? outb + o0 : nullptr);
     };
     if constexpr (BAL) {
         step_tiles_bal(T, sig, epoch, wide, narrow);
@@ -1785,12 +1787,12 @@ __global__ __launch_bounds__(B) void k_fold_f32_step(
     auto wide = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
         fold_tile<UB, CB, true, SCORED, false, true, true, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                                   divisor, out + c0);
+                                                                   divisor, out + T.ocol0[g]);
     };
     auto narrow = [&](int g, int64_t bid) {
         const int64_t c0 = T.col0[g];
         fold_tile<US, CS, true, SCORED, false, true, true, B, WTM>(bid, X + c0, N, T.width[g], ldx, a, s, nullptr,
-                                                                   divisor, out + c0);
+                                                                   divisor, out + T.ocol0[g]);
     };
     if constexpr (BAL) {
         step_tiles_bal(T, sig, epoch, wide, narrow);
@@ -2423,8 +2425,8 @@ struct RoundsState {
 // [offsets[k], offsets[k+1]): every round's columns in wide tiles, except the
 // last pool columns of the step (cut at wide-tile boundaries, walking back
 // from the last round) in narrow tiles.  FA status.
-inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offsets, int64_t ldx, int64_t grid,
-                            StepTable& T) {
+inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offsets, const int64_t* out_offsets,
+                            int64_t ldx, int64_t grid, StepTable& T) {
     const int64_t ucols = sp.bf16 ? 8 : 4;  // columns per octet / quad
     const int64_t wide_cols = (int64_t)kBlock * sp.cb * ucols;
     T = StepTable{};
@@ -2437,6 +2439,9 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
         if (c0 < 0 || w < 1 || c0 % ucols || offsets[k + 1] > ldx)
             return fail(FA_ERR_ARG, "round %d: columns [%lld, %lld) (every round non-empty, %lld-aligned, within ldx)",
                         k, (long long)c0, (long long)offsets[k + 1], (long long)ucols);
+        if (out_offsets && (out_offsets[k] < 0 || out_offsets[k] % ucols))
+            return fail(FA_ERR_ARG, "round %d: output column %lld (non-negative, %lld-aligned)", k,
+                        (long long)out_offsets[k], (long long)ucols);
         if (pool <= 0) { split[k] = w; continue; }
         if (pool >= w) { split[k] = 0; pool -= w; continue; }
         split[k] = ((w - pool) / wide_cols) * wide_cols;  // the static part ends on a wide-tile boundary
@@ -2453,6 +2458,7 @@ inline int build_step_table(const StepSpec& sp, int rounds, const int64_t* offse
         total += (units(hi - lo) + per - 1) / per;
         T.seg_end[g] = total;
         T.col0[g] = c0 + lo;
+        T.ocol0[g] = (out_offsets ? out_offsets[k] : c0) + lo;
         T.width[g] = hi - lo;
         T.round[g] = k;
         T.small[g] = small ? 1 : 0;
@@ -2572,7 +2578,7 @@ inline int rounds_check(RoundsState& o) {
 // [offsets[k], offsets[k+1]).
 inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int64_t N, int64_t ldx,
                        const float* a, const float* s, float divisor, float* out, uint16_t* outb, int rounds,
-                       const int64_t* offsets) {
+                       const int64_t* offsets, const int64_t* out_offsets = nullptr) {
     R.launched = false;
     if (f < 0 || f >= kNumStepForms) return fail(FA_ERR_ARG, "unknown step form %d", f);
     if (rounds < 1 || rounds > kMaxRounds || !offsets) return fail(FA_ERR_ARG, "rounds must be 1..%d", kMaxRounds);
@@ -2591,7 +2597,7 @@ inline int launch_step(RoundsState& R, int f, hipStream_t st, const void* X, int
     }
     int64_t grid = cu_count();
     StepTable T;
-    int rc = build_step_table(sp, rounds, offsets, ldx, grid, T);
+    int rc = build_step_table(sp, rounds, offsets, out_offsets, ldx, grid, T);
     if (rc) return rc;
     T.sys = R.sys ? 1 : 0;
     T.sysfence = R.sys == 2 ? 1 : 0;

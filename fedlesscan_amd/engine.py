@@ -378,7 +378,8 @@ def fold_staged(X: torch.Tensor, sf: StagedFactors, *, out: Optional[torch.Tenso
 
 def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], offsets: Sequence[int], *,
                 out=None, out_bf16=None, total=None, state: Optional[ctypes.c_void_p] = None,
-                capacity: Optional[int] = None, factors: Optional[Factors] = None) -> ctypes.c_void_p:
+                capacity: Optional[int] = None, factors: Optional[Factors] = None,
+                out_offsets: Optional[Sequence[int]] = None) -> ctypes.c_void_p:
     """Every exchange round of a step in ONE launch (fa_fedavg_*_rounds): round
     k folds the columns [offsets[k], offsets[k+1]) of X (fp32 or bf16 rows)
     into the same columns of out (fp32) and, for bf16 X, of out_bf16 (the RNE
@@ -391,11 +392,20 @@ def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], 
     columns.  out / out_bf16: tensors (at least offsets[-1] elements) or raw
     device addresses (a peer exchange's send buffer), which need `capacity`,
     the elements the address holds.  factors: f32_factors(weights, scores,
-    total) when the caller has them already (one step, one rounding)."""
+    total) when the caller has them already (one step, one rounding).
+    out_offsets: round k's results go to output columns [out_offsets[k],
+    out_offsets[k] + width k) instead (a rank's slots straight into its chunk
+    of the gathered model: the all-gather then runs in place)."""
     N, W, ldx = _check_matrix(X)
     if len(weights) != N or (scores is not None and len(scores) != N):
         raise InvalidParameterShapeError(f"{N} rows but {len(weights)} weights")
-    end = int(offsets[-1]) if len(offsets) else 0
+    rounds = len(offsets) - 1
+    if out_offsets is not None:
+        if len(out_offsets) < rounds:
+            raise ValueError(f"{len(out_offsets)} output offsets for {rounds} rounds")
+        end = max((int(out_offsets[k]) + int(offsets[k + 1]) - int(offsets[k]) for k in range(rounds)), default=0)
+    else:
+        end = int(offsets[-1]) if len(offsets) else 0
     for name, t, dt in (("out", out, torch.float32), ("out_bf16", out_bf16, torch.bfloat16)):
         if t is None:
             continue
@@ -410,18 +420,18 @@ def fold_rounds(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence], 
     f = factors if factors is not None else f32_factors(weights, scores, total)
     if f is None:
         raise InvalidParameterShapeError("the rounds fold takes float32 factors (Python-number weights)")
-    rounds = len(offsets) - 1
     offs = (ctypes.c_int64 * len(offsets))(*[int(o) for o in offsets])
+    oo = None if out_offsets is None else (ctypes.c_int64 * rounds)(*[int(o) for o in out_offsets[:rounds]])
     st = stream_ptr(dev)
     r = state if state is not None else rounds_state(dev, st)
     addr = (lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr()))
     # the factors from host memory: the library stages them (one C call, _hostf)
     if X.dtype == torch.bfloat16:
         _lib.call("fa_fedavg_bf16_rounds_hostf", r, X.data_ptr(), N, ldx, *f.host(), float(f.div),
-                  addr(out), addr(out_bf16), rounds, offs, st)
+                  addr(out), addr(out_bf16), rounds, offs, oo, st)
     elif X.dtype == torch.float32:
         _lib.call("fa_fedavg_f32_rounds_hostf", r, X.data_ptr(), N, ldx, *f.host(), float(f.div),
-                  addr(out), rounds, offs, st)
+                  addr(out), rounds, offs, oo, st)
     else:
         raise InvalidParameterShapeError(f"the rounds fold takes float32 or bfloat16 rows, got {X.dtype}")
     return r

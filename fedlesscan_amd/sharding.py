@@ -724,51 +724,56 @@ class ShardedAggregator:
         Y.copy_(X_local)
         return Y
 
+    def _own(self, layout: "SlotLayout", k: int) -> Tuple[int, int]:
+        """[lo, hi) of this rank's chunk of round k in the gathered model (its
+        slot k, padding included): where the fold writes it, so each round's
+        all-gather runs in place."""
+        lo = layout.round_range(k)[0] + self.rank * layout.width(k)
+        return lo, lo + layout.width(k)
+
     def _aggregate_slots_one_launch(self, X_local, weights, scores, layout, out, total, folds=None, factors=None):
-        """Every round's fold in ONE launch on the current (fold) stream; round
-        k's exchange issued on the gather stream behind a wait for round k, so
-        it runs while the launch folds the later rounds -- except the last
-        round's, issued on the fold stream itself right after the launch (stream
-        order is its wait: one wait kernel and one cross-stream hop fewer at the
-        end of the step).  Returns the model and (an event after the waits, the
-        rounds state) for the timeout check."""
+        """Every round's fold in ONE launch on the current (fold) stream, each
+        round's slot written straight into this rank's chunk of the model
+        (out_offsets); round k's in-place all-gather issued on the gather
+        stream behind a wait for round k, so it runs while the launch folds the
+        later rounds -- except the last round's, issued on the fold stream
+        itself right after the launch (stream order is its wait).  At world 1
+        there is nothing to exchange: the launch alone writes the model.
+        Returns the model and (an event after the waits, the rounds state) for
+        the timeout check, or None when no wait ran."""
         from . import engine
         dev = X_local.device
         bf16 = X_local.dtype == torch.bfloat16
         odt = torch.bfloat16 if bf16 else torch.float32
         full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=dev)
-        if full.dtype != odt or full.numel() < layout.padded_total:
-            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
-        # what the exchange moves, and all the fold stores: the fp32 result, or
-        # for bf16 rows only its RNE-bf16 copy (no fp32 result, ABI 5)
-        send_all = torch.empty(layout.local_width, dtype=odt, device=dev)
+        if full.dtype != odt or full.numel() < layout.padded_total or not full.is_contiguous():
+            raise ValueError(f"out needs {layout.padded_total} contiguous {odt} elements")
         offs = [layout.offset(k) for k in range(layout.rounds + 1)]
+        own = [self._own(layout, k) for k in range(layout.rounds)]
         fs = torch.cuda.current_stream(dev)
         e = _timing_pair(fs, folds)
-        if bf16:
-            r = engine.fold_rounds(X_local, weights, scores, offs, out_bf16=send_all, total=total, factors=factors)
-        else:
-            r = engine.fold_rounds(X_local, weights, scores, offs, out=send_all, total=total, factors=factors)
+        # all the fold stores: the fp32 result, or for bf16 rows only its
+        # RNE-bf16 copy (no fp32 result, ABI 5) -- the form the exchange moves
+        kw = {"out_bf16": full} if bf16 else {"out": full}
+        r = engine.fold_rounds(X_local, weights, scores, offs, total=total, factors=factors,
+                               out_offsets=[lo for lo, _ in own], **kw)
         if e is not None:
             e[1].record(fs)
+        if self.world == 1:
+            return full[: layout.P], None
         gs = gather_stream(dev)
-        send_all.record_stream(gs)
+        full.record_stream(gs)
         works = []
         waits_done = torch.cuda.Event()
         last = layout.rounds - 1
         for k in range(layout.rounds):
             lo, hi = layout.round_range(k)
-            send = send_all[layout.offset(k):layout.offset(k + 1)]
             if k < last:
                 engine.wait_round(r, k, gs)
                 if k == last - 1:
                     waits_done.record(gs)  # every round's wait has run (the timeout check)
-            st = gs if k < last else fs
-            with torch.cuda.stream(st):
-                if self.world == 1:
-                    full[lo:hi].copy_(send)
-                    continue
-                w = gather_into(full[lo:hi], send, self.group, async_op=True)
+            with torch.cuda.stream(gs if k < last else fs):
+                w = gather_into(full[lo:hi], full[own[k][0]:own[k][1]], self.group, async_op=True)
             if w is not None:
                 works.append(w)
         for w in works:
@@ -780,11 +785,11 @@ class ShardedAggregator:
         bf16 = X_local.dtype == torch.bfloat16
         odt = torch.bfloat16 if bf16 else torch.float32
         full = out if out is not None else torch.empty(layout.padded_total, dtype=odt, device=X_local.device)
-        if full.dtype != odt or full.numel() < layout.padded_total:
-            raise ValueError(f"out needs {layout.padded_total} {odt} elements")
-        # each round's fold writes straight into the slice the exchange sends:
-        # fp32 rows the fp32 result, bf16 rows only its RNE-bf16 copy
-        local = torch.empty(layout.local_width, dtype=odt, device=X_local.device)
+        if full.dtype != odt or full.numel() < layout.padded_total or not full.is_contiguous():
+            raise ValueError(f"out needs {layout.padded_total} contiguous {odt} elements")
+        # each round's fold writes straight into this rank's chunk of the model
+        # (fp32 rows the fp32 result, bf16 rows only its RNE-bf16 copy), and the
+        # round's all-gather runs in place: at world 1 nothing is copied
         cur = torch.cuda.current_stream(X_local.device) if X_local.is_cuda else None
         staged = None
         if factors is not None and X_local.is_cuda and not torch.cuda.is_current_stream_capturing():
@@ -794,7 +799,8 @@ class ShardedAggregator:
         works = []
         for k in range(layout.rounds):
             a, b = layout.offset(k), layout.offset(k) + layout.width(k)
-            piece = local[a:b]
+            olo, ohi = self._own(layout, k)
+            piece = full[olo:ohi]
             if b > a:
                 e = _timing_pair(cur, folds) if cur is not None else None
                 if staged is not None:
@@ -806,10 +812,9 @@ class ShardedAggregator:
                     self.fold(X_local[:, a:b], weights, scores, out=piece, total=total)
                 if e is not None:
                     e[1].record(cur)
-            lo, hi = layout.round_range(k)
             if self.world == 1:
-                full[lo:hi].copy_(piece)
                 continue
+            lo, hi = layout.round_range(k)
             w = gather_into(full[lo:hi], piece, self.group, async_op=True)
             if w is not None:
                 works.append(w)

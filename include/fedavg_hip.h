@@ -151,17 +151,22 @@ int fa_fedavg_bf16(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  *   fa_rounds_timeouts: (synchronous) every timed-out wait since creation.
  *   fa_fedavg_bf16_rounds: out_f32 / out_bf16 as fa_fedavg_bf16 (ABI 5: either
  *     may be NULL, not both).
+ *   out_offsets (ABI 5) [host] rounds output columns, or NULL: round k's
+ *     results go to columns [out_offsets[k], out_offsets[k] + width k) of the
+ *     outputs instead of [offsets[k], offsets[k+1]) (each 4-aligned, bf16
+ *     8-aligned) -- a rank writes its slot of round k straight into its own
+ *     chunk of the gathered model, and the all-gather runs in place. 
  *   One object per launching stream (engine.py keeps one per stream object). */
 typedef struct fa_rounds fa_rounds;
 int fa_rounds_create(fa_rounds** r, int device);
 int fa_rounds_destroy(fa_rounds* r);
 int fa_fedavg_f32_rounds(fa_rounds* r, const float* X, int64_t N, int64_t ldx,
                          const float* a, const float* s, float divisor, float* out,
-                         int rounds, const int64_t* offsets, void* stream);
+                         int rounds, const int64_t* offsets, const int64_t* out_offsets, void* stream);
 int fa_fedavg_bf16_rounds(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx,
                           const float* a, const float* s, float divisor,
                           float* out_f32, uint16_t* out_bf16,
-                          int rounds, const int64_t* offsets, void* stream);
+                          int rounds, const int64_t* offsets, const int64_t* out_offsets, void* stream);
 int fa_rounds_wait(fa_rounds* r, int round, void* stream);
 int fa_rounds_check(fa_rounds* r);
 int fa_rounds_timeouts(fa_rounds* r);
@@ -215,9 +220,10 @@ int fa_peers_exchange(fa_peers* x, int rounds, const int64_t* src_offsets, void*
 /* The same folds with the per-client factors a[0..N), s[0..N) (s may be
  * NULL) in HOST memory, as the reference's caller holds them (Python numbers,
  * fed_avg_aggregator.py:32-41).  The library copies them into a page-locked
- * slot of its own, sends them in one async H2D on `stream` ahead of the fold
- * and reuses the slot only after that fold has completed, so a and s may be
- * freed or rewritten as soon as the call returns.  X, xi, out stay device
+ * slot of its own, sends them in one async H2D on a staging stream of its own
+ * that `stream` waits for (an event) ahead of the fold, and reuses the slot
+ * only after that fold has completed, so a and s may be freed or rewritten as
+ * soon as the call returns.  X, xi, out stay device
  * pointers.  _ptrs: rows_aligned != 0 takes fa_fedavg_f32_ptrs_aligned's
  * kernels (every row 16-B aligned, out 16-B aligned), 0 fa_fedavg_f32_ptrs. */
 int fa_fedavg_f32_hostf(const float* X, int64_t N, int64_t P, int64_t ldx,
@@ -233,11 +239,11 @@ int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
  * factors staged by the library like the folds above (one C call per step). */
 int fa_fedavg_f32_rounds_hostf(fa_rounds* r, const float* X, int64_t N, int64_t ldx,
                                const float* a, const float* s, float divisor, float* out,
-                               int rounds, const int64_t* offsets, void* stream);
+                               int rounds, const int64_t* offsets, const int64_t* out_offsets, void* stream);
 int fa_fedavg_bf16_rounds_hostf(fa_rounds* r, const uint16_t* X, int64_t N, int64_t ldx,
                                 const float* a, const float* s, float divisor,
                                 float* out_f32, uint16_t* out_bf16,
-                                int rounds, const int64_t* offsets, void* stream);
+                                int rounds, const int64_t* offsets, const int64_t* out_offsets, void* stream);
 
 /* Measured form choice.  Every kernel form of the fp32, bf16 and row-table
  * folds computes the same bits; which is fastest depends on how a shape's

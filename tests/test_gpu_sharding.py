@@ -162,53 +162,72 @@ def test_step_form_restored_from_the_cache_file(bf16, recorded, monkeypatch):
     assert agg.step_form(Xin, lay) == {"one": "one launch", "per": "per round", None: None}[recorded]
 
 
+def _c4_rank_input(dev, N=256, seed=52):
+    """A C4 rank's share as 4 rounds (~1 ms of fold) at world 1, in HBM."""
+    from fedlesscan_amd.sharding import overlap_layout
+    B = __import__("fedlesscan_amd._lib", fromlist=["x"]).load_bench()
+    lay = overlap_layout(100_000_000 // 8, 1, "bf16")
+    W = lay.local_width
+    X = torch.empty((N, W), dtype=torch.bfloat16, device=dev)
+    assert B.fa_synth_bf16(X.data_ptr(), N, W, W, seed, 0, 0, torch.cuda.current_stream(dev).cuda_stream) == 0
+    return lay, X, synth.cardinalities(seed, N), _scores(seed, N)
+
+
+def _hold_the_fold(busy):
+    """~5 ms of work ahead of the step on the caller's stream: the fold (and the
+    waiters' clocks, which start with it) begins only after the host has
+    enqueued the whole step, so every wait sees an unfinished round however
+    slowly this process issues its first calls."""
+    for _ in range(24):
+        busy.fill_(1.0)
+
+
 def test_round_wait_timeout_raises_on_every_path(monkeypatch):
     """A round wait that gives up (a tick limit far below one C4-slot fold,
     FEDAVG_ROUND_WAIT_US) lets the exchange behind it read an unfinished
     round: aggregate_slots raises AggregationError instead of returning the
-    model (check="sync"), or check_timeouts() does (check="deferred").  At the
-    default limit the same step is bit-exact against the oracle, every column."""
-    from fedlesscan_amd import engine
+    model (check="sync"), or check_timeouts() does (check="deferred").  At
+    world 1 the waits are the peer exchange's (the RCCL step folds its slots
+    straight into the model and has nothing to wait for there; its waits at
+    world 2: test_round_wait_timeout_two_ranks).  At the default limit the
+    same steps are bit-exact against the oracle, every column."""
     from fedlesscan_amd.aggregator.exceptions import AggregationError
-    from fedlesscan_amd.sharding import ShardedAggregator, overlap_layout
+    from fedlesscan_amd.sharding import ShardedAggregator
     from oracle import oracle_lib as OL
     dev = torch.device("cuda", 0)
-    B = __import__("fedlesscan_amd._lib", fromlist=["x"]).load_bench()
     N, seed = 256, 52
-    lay = overlap_layout(100_000_000 // 8, 1, "bf16")  # a C4 rank's share as 4 rounds: ~1 ms of fold
-    W = lay.local_width
-    X = torch.empty((N, W), dtype=torch.bfloat16, device=dev)
-    assert B.fa_synth_bf16(X.data_ptr(), N, W, W, seed, 0, 0, torch.cuda.current_stream(dev).cuda_stream) == 0
-    w = synth.cardinalities(seed, N)
-    sc = _scores(seed, N)
-    monkeypatch.setattr(engine, "_rounds_states", {})  # fresh states read the limit
-    monkeypatch.setenv("FEDAVG_ROUND_WAIT_US", "1")
+    lay, X, w, sc = _c4_rank_input(dev, N, seed)
+    monkeypatch.setenv("FEDAVG_ROUND_WAIT_US", "1")  # read when the peer exchange's state is created
     busy = torch.empty(1 << 28, dtype=torch.float32, device=dev)
-
-    def hold_the_fold():
-        # ~5 ms of work ahead of the step on the caller's stream: the fold (and
-        # the waiters' clocks, which start with it) begins only after the host
-        # has enqueued the whole step, so every wait sees an unfinished round
-        # however slowly this process issues its first calls
-        for _ in range(24):
-            busy.fill_(1.0)
-    hold_the_fold()
+    sync = ShardedAggregator(one_launch=True, exchange="peer_copy")
+    deferred = ShardedAggregator(one_launch=True, exchange="peer_copy", check="deferred")
+    for agg in (sync, deferred):
+        # a first call creates the peer exchange (which synchronises the device):
+        # timed out or not, it is not the call under test
+        try:
+            agg.aggregate_slots(X, w, sc, lay)
+            agg.check_timeouts()
+        except AggregationError:
+            pass
+    _hold_the_fold(busy)
     with pytest.raises(AggregationError, match="timed out"):
-        ShardedAggregator(one_launch=True).aggregate_slots(X, w, sc, lay)
-    deferred = ShardedAggregator(one_launch=True, check="deferred")
-    hold_the_fold()
+        sync.aggregate_slots(X, w, sc, lay)
+    _hold_the_fold(busy)
     out = deferred.aggregate_slots(X, w, sc, lay)
     assert out.dtype == torch.bfloat16
     with pytest.raises(AggregationError, match="timed out"):
         deferred.check_timeouts()
     deferred.check_timeouts()  # nothing left unchecked
     torch.cuda.synchronize()
-    del busy
-    monkeypatch.setattr(engine, "_rounds_states", {})
+    sync.close()
+    deferred.close()
+    del busy, out
     monkeypatch.delenv("FEDAVG_ROUND_WAIT_US")
-    agg = ShardedAggregator(one_launch=True)
-    got = _bits(agg.aggregate_slots(X, w, sc, lay), True)
-    del X, out
+    peer = ShardedAggregator(one_launch=True, exchange="peer_copy")
+    got_peer = _bits(peer.aggregate_slots(X, w, sc, lay), True)
+    got_one = _bits(ShardedAggregator(one_launch=True).aggregate_slots(X, w, sc, lay), True)
+    peer.close()
+    del X
     torch.cuda.empty_cache()
     an, sn = np.array(w, np.float32), np.array(sc, np.float32)
     P = lay.P  # world 1: global column p is local column p
@@ -216,7 +235,65 @@ def test_round_wait_timeout_raises_on_every_path(monkeypatch):
     for c0 in range(0, P, 1 << 21):
         nc = min(1 << 21, P - c0)
         _, expb[c0:c0 + nc] = OL.fedavg_bf16(OL.synth_bf16(seed, N, nc, col0=c0), an, np.float32(sum(w)), s=sn)
-    assert np.array_equal(got, expb)
+    assert np.array_equal(got_peer, expb) and np.array_equal(got_one, expb)
+
+
+def _timeout_rank(rank, world, port, q):
+    """One of two ranks sharing the GPU: the RCCL-form one-launch step with a
+    1 us round-wait limit must raise on BOTH ranks (the MAX over the group)."""
+    import torch as T
+    import torch.distributed as dist
+    from fedlesscan_amd.aggregator.exceptions import AggregationError
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FEDAVG_ROUND_WAIT_US="1")
+    T.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = T.device("cuda", 0)
+        N, P = 256, 4_000_000
+        lay = SlotLayout(P, world, 4)
+        B = __import__("fedlesscan_amd._lib", fromlist=["x"]).load_bench()
+        W = lay.local_width
+        X = T.empty((N, W), dtype=T.bfloat16, device=dev)
+        assert B.fa_synth_bf16(X.data_ptr(), N, W, W, 5, 0, 0, T.cuda.current_stream(dev).cuda_stream) == 0
+        w = synth.cardinalities(5, N)
+        busy = T.empty(1 << 28, dtype=T.float32, device=dev)
+        res = []
+        for check in ("sync", "deferred"):
+            agg = ShardedAggregator(one_launch=True, check=check)
+            try:  # a first call creates the rounds state (a device synchronisation): not the call under test
+                agg.aggregate_slots(X, w, None, lay)
+                agg.check_timeouts()
+            except AggregationError:
+                pass
+            _hold_the_fold(busy)
+            try:
+                agg.aggregate_slots(X, w, None, lay)
+                if check == "deferred":
+                    agg.check_timeouts()
+                res.append("returned")
+            except AggregationError as e:
+                res.append("raised" if "timed out" in str(e) else repr(e))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_round_wait_timeout_two_ranks():
+    """The RCCL exchange's round waits at world 2 (two gloo ranks sharing the
+    GPU): with a 1 us limit every rank raises, in both check modes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == {0: ["raised", "raised"], 1: ["raised", "raised"]}, got
 
 
 @pytest.mark.parametrize("one_launch", ["auto", True])

@@ -94,11 +94,11 @@ def _one_launch_steps(dev, libs, X, N, W, lay, a, s, div, bf16):
         got = torch.full((W,), -1, dtype=torch.int16 if bf16 else torch.int32, device=dev)
         if bf16:  # reps 2-3 store the bf16 result alone (ABI 5: out_f32 NULL)
             rc = L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, W, a.data_ptr(), sp, div,
-                                         o.data_ptr() if rep < 2 else None, ob.data_ptr(), lay.rounds, offs,
+                                         o.data_ptr() if rep < 2 else None, ob.data_ptr(), lay.rounds, offs, None,
                                          st.cuda_stream)
         else:
             rc = L.fa_fedavg_f32_rounds(r, X.data_ptr(), N, W, a.data_ptr(), sp, div, o.data_ptr(), lay.rounds, offs,
-                                        st.cuda_stream)
+                                        None, st.cuda_stream)
         _lib.check(rc, "rounds fold")
         src = ob if bf16 else o.view(torch.int32)
         for k in range(lay.rounds):
@@ -279,7 +279,7 @@ def test_rounds_entry_errors(dev, libs):
     def launch(offsets, rounds=None):
         offs = (ctypes.c_int64 * len(offsets))(*offsets)
         return L.fa_fedavg_f32_rounds(r, X.data_ptr(), 4, 1024, a.data_ptr(), None, 4.0, o.data_ptr(),
-                                      len(offsets) - 1 if rounds is None else rounds, offs, st)
+                                      len(offsets) - 1 if rounds is None else rounds, offs, None, st)
     with pytest.raises(ValueError):
         _lib.check(L.fa_rounds_wait(r, 0, st), "wait before launch")
     for bad in ([0, 0, 512], [0, 2, 1024], [0, 512, 1028], [0] + list(range(64, 640, 64))):
@@ -298,7 +298,7 @@ def test_rounds_entry_errors(dev, libs):
         with torch.cuda.graph(g, stream=side):
             offs = (ctypes.c_int64 * 3)(0, 512, 1024)
             rc = L.fa_fedavg_f32_rounds(r, X.data_ptr(), 4, 1024, a.data_ptr(), None, 4.0, o.data_ptr(), 2, offs,
-                                        side.cuda_stream)
+                                        None, side.cuda_stream)
     assert rc == _lib.FA_ERR_ARG
     assert L.fa_rounds_timeouts(r) == 0 and L.fa_rounds_check(r) == 0
     _lib.check(L.fa_rounds_destroy(r), "destroy")
@@ -339,7 +339,7 @@ def test_bf16_result_alone(dev, libs, P):
     r = ctypes.c_void_p()
     _lib.check(L.fa_rounds_create(ctypes.byref(r), dev.index), "create")
     offs = (ctypes.c_int64 * 2)(0, P // 8 * 8)
-    assert L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, ldx, a.data_ptr(), None, 1.0, None, None, 1, offs,
+    assert L.fa_fedavg_bf16_rounds(r, X.data_ptr(), N, ldx, a.data_ptr(), None, 1.0, None, None, 1, offs, None,
                                    st) == _lib.FA_ERR_ARG
     _lib.check(L.fa_rounds_destroy(r), "destroy")
     with pytest.raises(ValueError):

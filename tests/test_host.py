@@ -129,8 +129,9 @@ def test_exchange_entry_argument_errors_need_no_gpu():
     assert L.fa_peers_create(None, 0, 2, 0, 64) == _lib.FA_ERR_ARG
     assert L.fa_peers_handle_bytes() == 2 * 64  # two hipIpcMemHandle_t: the send buffers, the signal words
     assert "fa_peers_fence" not in _lib.header_functions()  # ABI 5: the double-buffered exchange needs none
-    assert L.fa_fedavg_f32_rounds_hostf(None, None, 1, 4, None, None, 1.0, None, 1, None, None) == _lib.FA_ERR_ARG
-    assert L.fa_fedavg_bf16_rounds_hostf(None, None, 1, 8, None, None, 1.0, None, None, 1, None, None) == \
+    assert L.fa_fedavg_f32_rounds_hostf(None, None, 1, 4, None, None, 1.0, None, 1, None, None, None) == \
+        _lib.FA_ERR_ARG
+    assert L.fa_fedavg_bf16_rounds_hostf(None, None, 1, 8, None, None, 1.0, None, None, 1, None, None, None) == \
         _lib.FA_ERR_ARG
     assert L.fa_peers_exchange(None, 1, None, None, None, None) == _lib.FA_ERR_ARG
     assert L.fa_peers_send(None) is None and L.fa_peers_rounds(None) is None

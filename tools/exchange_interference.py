@@ -180,10 +180,10 @@ def main():
         if sform == "product":
             if dt == "f32":
                 rc = L.fa_fedavg_f32_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, out.data_ptr(),
-                                            lay.rounds, offs, fs.cuda_stream)
+                                            lay.rounds, offs, None, fs.cuda_stream)
             else:
                 rc = L.fa_fedavg_bf16_rounds(rs_prod, X.data_ptr(), N, W, a.data_ptr(), None, div, optr(),
-                                             outb.data_ptr(), lay.rounds, offs, fs.cuda_stream)
+                                             outb.data_ptr(), lay.rounds, offs, None, fs.cuda_stream)
             _lib.check(rc, "rounds fold")
         else:
             rc = B.fa_fedavg_rounds_form(rs_bench, step_names[sform], X.data_ptr(), N, W, a.data_ptr(), None, div,
