@@ -581,7 +581,8 @@ class ShardedAggregator:
         dev = X_local.device
         caller = torch.cuda.current_stream(dev)
         fs = fold_stream(dev)
-        fs.wait_stream(caller)
+        if caller != fs:  # a caller already on the fold stream needs no hop
+            fs.wait_stream(caller)
         folds = [] if (probing or self.trace is not None) else None  # (start, end) timing events per fold launch
         waited = None
         with torch.cuda.stream(fs):
@@ -601,8 +602,9 @@ class ShardedAggregator:
                 full, waited = self._aggregate_slots_one_launch(X_local, weights, scores, layout, out, total, folds, f)
             else:
                 full = self._aggregate_slots(X_local, weights, scores, layout, out, total, folds, f)
-        caller.wait_stream(fs)
-        full.record_stream(caller)
+        if caller != fs:
+            caller.wait_stream(fs)
+            full.record_stream(caller)
         if folds is not None:
             end = torch.cuda.Event(enable_timing=True)
             end.record(caller)
