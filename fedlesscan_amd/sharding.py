@@ -742,7 +742,8 @@ class ShardedAggregator:
         itself right after the launch (stream order is its wait).  At world 1
         there is nothing to exchange: the launch alone writes the model.
         Returns the model and (an event after the waits, the rounds state) for
-        the timeout check, or None when no wait ran."""
+        the timeout check, or None when no wait ran or check="sync" already
+        checked them (before the last round's gather)."""
         from . import engine
         dev = X_local.device
         bf16 = X_local.dtype == torch.bfloat16
@@ -768,12 +769,26 @@ class ShardedAggregator:
         works = []
         waits_done = torch.cuda.Event()
         last = layout.rounds - 1
+        waited = (waits_done, r)
         for k in range(layout.rounds):
             lo, hi = layout.round_range(k)
             if k < last:
                 engine.wait_round(r, k, gs)
                 if k == last - 1:
                     waits_done.record(gs)  # every round's wait has run (the timeout check)
+            elif self.check == "sync":
+                # check="sync" here, before the last round's gather: the waits
+                # (rounds 0..R-2; the last round is ordered by the stream) are
+                # done while the launch still folds the last round, and the
+                # check's MAX all-reduce goes on the gather stream, ahead of
+                # the last gather -- so the host's wait and the collective
+                # overlap the fold's tail instead of following the step.  A
+                # timeout raises on every rank here, before any rank issues the
+                # last gather (the MAX agrees)
+                waits_done.synchronize()
+                with torch.cuda.stream(gs):
+                    self._raise_on_timeouts(self._timed_out([r]), dev)
+                waited = None
             with torch.cuda.stream(gs if k < last else fs):
                 w = gather_into(full[lo:hi], full[own[k][0]:own[k][1]], self.group, async_op=True)
             if w is not None:
@@ -781,7 +796,7 @@ class ShardedAggregator:
         for w in works:
             w.wait()  # the fold stream waits for the collectives
         fs.wait_stream(gs)
-        return full[: layout.P], (waits_done, r)
+        return full[: layout.P], waited
 
     def _aggregate_slots(self, X_local, weights, scores, layout, out, total, folds=None, factors=None):
         bf16 = X_local.dtype == torch.bfloat16
