@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 import socket
+import warnings
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -722,6 +723,9 @@ class ShardedAggregator:
         if (X_local.data_ptr() % 16 == 0 and X_local.stride(1) == 1
                 and (X_local.shape[0] == 1 or X_local.stride(0) % align == 0)):
             return X_local
+        warnings.warn(f"aggregate_slots: rows at {X_local.data_ptr():#x} with pitch {X_local.stride(0)} cannot take "
+                      "the one-launch step as they are; folding an aligned copy (allocate X_local 16-B aligned with "
+                      f"a pitch that is a multiple of {align} elements to avoid it)", RuntimeWarning, stacklevel=3)
         Y = torch.empty(X_local.shape, dtype=X_local.dtype, device=X_local.device)
         Y.copy_(X_local)
         return Y
