@@ -674,10 +674,10 @@ def main():
         for _ in range(warm_extra):
             step()
     if product and agg.one_launch == "probe" and rounds > 1:
-        # the class's probe alternates the forms over its first 2 x PROBE_CALLS
+        # the class's probe alternates the forms over its first PROBE_STEPS
         # calls of the shape; the timed steps run the form it keeps (the same
         # count of calls on every rank: its decision is max-over-ranks timing)
-        for _ in range(2 * agg.PROBE_CALLS):
+        for _ in range(agg.PROBE_STEPS):
             if agg.step_form(wl.X, lay) is not None:
                 break
             step()
@@ -687,8 +687,9 @@ def main():
         mode_probe = ({"chosen": agg.step_form(wl.X, lay), "recorded": pkey,
                        "one_launch_ms": [round(x, 4) for x in got["one"]],
                        "per_round_ms": [round(x, 4) for x in got["per"]],
-                       "how": "ShardedAggregator(one_launch='probe'): its first 2 x PROBE_CALLS calls alternate "
-                              "the forms (device time per call, max over ranks), the best call of each compared"}
+                       "how": "ShardedAggregator(one_launch='probe'): its first PROBE_STEPS calls alternate "
+                              "the forms, PROBE_WARM untimed calls of each, then PROBE_CALLS timed back to back "
+                              "(device time per call, max over ranks); the best call of each compared"}
                       if got else {"chosen": agg.step_form(wl.X, lay), "restored": pkey,
                                    "how": "recorded in the tuner's cache file (fa_step_lookup), rank 0's record "
                                           "broadcast: no timing run"})

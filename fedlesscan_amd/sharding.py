@@ -348,9 +348,16 @@ class ShardedAggregator:
                 differ (another node, a concurrent writer) still take one form
                 and issue the same collectives;
       "probe"   as "auto", but a shape with no recorded form is timed: its
-                first 2 x PROBE_CALLS calls alternate the two forms on the
-                device (max over the group's ranks), then the faster is kept
-                and recorded (fa_step_record) for later processes.
+                first PROBE_STEPS calls alternate the two forms, PROBE_WARM
+                untimed calls of each first (first-use costs: the rounds
+                state, buffers, the tuner), then PROBE_CALLS timed calls of
+                each, back to back as the steps run (no synchronisation per
+                call: a call's device time, from its fold stream's start to its
+                end on the caller's stream, hides the host's enqueue as steady
+                steps do); the call that completes the schedule reads the
+                times, takes their MAX over the group's ranks (one
+                all-reduce), keeps the form with the faster best call and
+                records it (fa_step_record) for later processes.
     Every rank of a group takes the same form: the choice depends only on
     what the ranks share (the constructor's arguments, the layout, the client
     count, rank 0's record), and a rank whose rows cannot take the one launch
@@ -387,8 +394,11 @@ class ShardedAggregator:
     (ABI 5: no fp32 result is written, 2 B/param out instead of 6).
     """
 
-    # calls per step form the "probe" mode times before it keeps the faster
+    # the "probe" mode, per step form: untimed calls first, then timed calls;
+    # PROBE_STEPS calls of a shape in all before it keeps the faster form
+    PROBE_WARM = 1
     PROBE_CALLS = 2
+    PROBE_STEPS = 2 * (PROBE_WARM + PROBE_CALLS)
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, fold: Optional[Callable] = None,
                  one_launch="auto", check: str = "sync", device_ident: Optional[str] = None,
@@ -413,7 +423,7 @@ class ShardedAggregator:
         self.check = check
         self.ident = device_ident
         self.trace: Optional[list] = None
-        self._probe: dict = {}  # step key -> {"one": [ms], "per": [ms]} while probing
+        self._probe: dict = {}  # step key -> {"calls": {form: n}, "timed": [(form, start, end)]} while probing
         self.probed: dict = {}  # step key -> the same, for the probes that have decided
         self._steps: dict = {}  # step key -> True (one launch) / False (per round): decided or restored
         self._agreed: set = set()  # step keys whose decision the group has agreed on (world > 1)
@@ -493,11 +503,14 @@ class ShardedAggregator:
         if got is None and self.one_launch == "probe" and self.default_fold:
             if key not in self._probe and len(self._probe) >= 64:  # bounded: forget the oldest shape
                 self._probe.pop(next(iter(self._probe)))
-            t = self._probe.setdefault(key, {"one": [], "per": []})
-            # the form with fewer timed calls, one launch first: the schedule
-            # depends only on what every rank shares, so all time in step
-            probing = (key, "one" if len(t["one"]) <= len(t["per"]) else "per")
-            return probing[1] == "one", probing
+            t = self._probe.setdefault(key, {"calls": {"one": 0, "per": 0}, "timed": []})
+            # the form with fewer calls, one launch first; a form's first
+            # PROBE_WARM calls untimed: the schedule depends only on what every
+            # rank shares, so all ranks time the same calls
+            n = t["calls"]
+            form = "one" if n["one"] <= n["per"] else "per"
+            probing = (key, form, n[form] >= self.PROBE_WARM)
+            return form == "one", probing
         return bool(got), None
 
     def bounds(self, P: int) -> Tuple[int, int]:
@@ -584,7 +597,8 @@ class ShardedAggregator:
         fs = fold_stream(dev)
         if caller != fs:  # a caller already on the fold stream needs no hop
             fs.wait_stream(caller)
-        folds = [] if (probing or self.trace is not None) else None  # (start, end) timing events per fold launch
+        timed = probing is not None and probing[2]
+        folds = [] if (timed or self.trace is not None) else None  # (start, end) timing events per fold launch
         waited = None
         with torch.cuda.stream(fs):
             if one:
@@ -618,7 +632,7 @@ class ShardedAggregator:
             else:
                 self._pending.append(waited)
         if probing:
-            self._record_probe(probing, folds[0][0], end, X_local, layout)
+            self._record_probe(probing, folds[0][0] if timed else None, end if timed else None, X_local, layout)
         return full
 
     def _timed_out(self, states) -> int:
@@ -681,23 +695,32 @@ class ShardedAggregator:
         return self._peers[key]
 
     def _record_probe(self, probing, start, end, X_local, layout) -> None:
-        """One timed call of the "probe" mode: its device time (max over the
-        group's ranks, so every rank keeps the same form); after PROBE_CALLS
-        calls of each form the faster one (best call) is recorded for the
-        shape (record_step_form: this process and the cache file)."""
-        key, form = probing
-        end.synchronize()
-        t = torch.tensor([start.elapsed_time(end)], dtype=torch.float64, device=X_local.device)
+        """One call of the "probe" mode: counted, and its (start, end) events
+        kept when timed.  The call that completes the schedule reads every
+        timed call's device time (waiting for its own end only), takes the MAX
+        over the group's ranks (one all-reduce, so every rank keeps the same
+        form) and records the form with the faster best call
+        (record_step_form: this process and the cache file)."""
+        key, form, timed = probing
+        got = self._probe[key]
+        got["calls"][form] += 1
+        if timed:
+            got["timed"].append((form, start, end))
+        if min(got["calls"].values()) < self.PROBE_WARM + self.PROBE_CALLS:
+            return
+        del self._probe[key]
+        end = got["timed"][-1][2]
+        end.synchronize()  # the calls' events complete in stream order
+        t = torch.tensor([s.elapsed_time(e) for _, s, e in got["timed"]], dtype=torch.float64,
+                         device=self._backend_device(X_local.device) if self.world > 1 else "cpu")
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        got = self._probe[key]
-        got[form].append(float(t.item()))
-        if len(got["one"]) >= self.PROBE_CALLS and len(got["per"]) >= self.PROBE_CALLS:
-            del self._probe[key]
-            self.probed[key] = got  # what the decision saw (ms per call, max over ranks)
-            while len(self.probed) > 64:
-                self.probed.pop(next(iter(self.probed)))
-            self.record_step_form(X_local, layout, min(got["one"]) <= min(got["per"]))
+        ms = [float(x) for x in t.tolist()]
+        res = {f: [m for (g, _, _), m in zip(got["timed"], ms) if g == f] for f in ("one", "per")}
+        self.probed[key] = res  # what the decision saw (ms per timed call, max over ranks)
+        while len(self.probed) > 64:
+            self.probed.pop(next(iter(self.probed)))
+        self.record_step_form(X_local, layout, min(res["one"]) <= min(res["per"]))
 
     def _one_launch_ok(self, X_local, layout) -> bool:
         """Can the step run as one launch?  Only what every rank shares (the

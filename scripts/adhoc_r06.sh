@@ -25,6 +25,19 @@ case "${1:-lines}" in
      "c3r_loop_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one --step-impl loop" \
      "c3r_prod_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round" \
      "c3r_loop_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round --step-impl loop" ;;
+  probe)  # the warmed, pipelined step-form probe: what it chooses against both forms' lines
+    scripts/gpu_steps.sh "t_sharding:500:$T tests/test_gpu_sharding.py" "t_rccl:500:$T tests/test_gpu_rccl.py" \
+     "c4r_prod_auto:300:python3 bench.py --rccl-world1 $C4R" \
+     "c3r_prod_auto:300:python3 bench.py --rccl-world1 $C3R" \
+     "c4r_prod_one:300:python3 bench.py --rccl-world1 $C4R --step-mode one" \
+     "c4r_prod_per:300:python3 bench.py --rccl-world1 $C4R --step-mode per-round" \
+     "c3r_prod_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one" \
+     "c3r_prod_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round" ;;
+  c3one)  # the C3 rank's one launch: product vs loop vs the decomposition tool, one box
+    scripts/gpu_steps.sh "c3r_prod_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one" \
+     "c3r_loop_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one --step-impl loop" \
+     "c3r_prod_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round" \
+     "decomp_c3:300:python3 tools/peer_step_decomp.py --config c3 --steps 5 --only fold_agent,product_rccl,product_sync" ;;
   trace)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/tr_peer" \

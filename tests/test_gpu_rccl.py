@@ -67,7 +67,7 @@ def _rccl_worker(port, q):
                 # "probe": both forms timed over the first calls, then the faster kept and recorded
                 agg = ShardedAggregator(one_launch="probe")
                 runs = set()
-                for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
+                for _ in range(ShardedAggregator.PROBE_STEPS + 1):
                     full = agg.aggregate_slots(X.view(T.bfloat16) if bf16 else X, w, sc if scored else None, lay)
                     runs.add(full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes())
                 assert len(runs) == 1 and agg.step_form(X.view(T.bfloat16) if bf16 else X, lay) is not None

@@ -95,8 +95,9 @@ def _bits(full, bf16):
 
 @pytest.mark.parametrize("bf16", [False, True])
 def test_probe_step_form_settles_records_and_stays_exact(bf16, monkeypatch):
-    """one_launch="probe": the first 2 x PROBE_CALLS calls of a shape alternate
-    the one launch and per-round launches (each timed), later calls keep the
+    """one_launch="probe": the first PROBE_STEPS calls of a shape alternate
+    the one launch and per-round launches (PROBE_WARM untimed calls of each,
+    then PROBE_CALLS timed ones), later calls keep the
     faster, and the choice is recorded: a fresh "auto" aggregator (a later
     process's) runs it without probing.  Every call bit-exact; a new shape
     probes anew."""
@@ -111,9 +112,9 @@ def test_probe_step_form_settles_records_and_stays_exact(bf16, monkeypatch):
         N, seed = 33, 9
         lay = SlotLayout(P, 1, rounds)
         Xin, w, sc, exp = _slots_input(bf16, N, P, seed, lay, dev)
-        for call in range(2 * ShardedAggregator.PROBE_CALLS + 2):
+        for call in range(ShardedAggregator.PROBE_STEPS + 2):
             settled = agg.step_form(Xin, lay)
-            assert (settled is None) == (call < 2 * ShardedAggregator.PROBE_CALLS), (call, settled)
+            assert (settled is None) == (call < ShardedAggregator.PROBE_STEPS), (call, settled)
             assert np.array_equal(_bits(agg.aggregate_slots(Xin, w, sc, lay), bf16), exp), (P, call)
         form = agg.step_form(Xin, lay)
         assert form in ("one launch", "per round")
@@ -424,7 +425,7 @@ def _rank(rank, world, port, N, P, rounds, seed, bf16, q, exchange="rccl", misal
             agg.close()
         elif exchange == "rccl":
             agg = ShardedAggregator(one_launch="probe")  # the probe's all-reduce runs over the group
-            for _ in range(2 * ShardedAggregator.PROBE_CALLS + 1):
+            for _ in range(ShardedAggregator.PROBE_STEPS + 1):
                 full = agg.aggregate_slots(Xin, w, sc, lay)
                 outs.append(full.view(T.int16 if bf16 else T.int32).cpu().numpy().tobytes())
             assert agg.step_form(Xin, lay) in ("one launch", "per round")

@@ -344,6 +344,46 @@ def test_step_form_is_rank0s_on_every_rank(tmp_path, case):
         assert got[r] == (want, want, form), (r, got[r])
 
 
+def test_probe_schedule_warms_times_then_decides(monkeypatch):
+    """one_launch="probe" schedule (host logic, no GPU): the forms alternate,
+    one launch first; each form's first PROBE_WARM calls are untimed (so a
+    cold first call -- state, buffers, tuner -- cannot decide); the call that
+    completes PROBE_STEPS compares the best timed call of each form, records
+    the faster, and later calls run it without probing."""
+    lay = SlotLayout(1000, 1, 4)
+    agg = ShardedAggregator(one_launch="probe", device_ident="test:probe")
+    monkeypatch.setattr(ShardedAggregator, "_lookup", lambda self, key: self._steps.get(key))
+    rec = []
+    monkeypatch.setattr(ShardedAggregator, "record_step_form",
+                        lambda self, X, L, one: rec.append(one) or self._steps.__setitem__(self.step_key(X, L), one))
+
+    class Ev:  # a timing event whose elapsed_time is the difference of fixed stamps
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+        def synchronize(self):
+            pass
+
+    X = torch.zeros(3, lay.local_width)
+    # the one launch's warm call is slow (first use), its timed calls faster than per-round's
+    times = {"one": [9.0, 1.0, 1.2], "per": [0.5, 1.1, 1.3]}
+    seen = []
+    for _ in range(ShardedAggregator.PROBE_STEPS):
+        one, probing = agg._form(X, lay)
+        form = "one" if one else "per"
+        seen.append((form, probing[2]))
+        t = times[form].pop(0)
+        agg._record_probe(probing, *((Ev(0.0), Ev(t)) if probing[2] else (None, None)), X, lay)
+    W, C = ShardedAggregator.PROBE_WARM, ShardedAggregator.PROBE_CALLS
+    assert seen == [("one", False), ("per", False)] * W + [("one", True), ("per", True)] * C
+    assert rec == [True]
+    assert agg.probed[agg.step_key(X, lay)] == {"one": [1.0, 1.2], "per": [1.1, 1.3]}
+    assert agg._form(X, lay) == (True, None)
+
+
 def test_step_keys_and_modes():
     """The decision key names what the choice depends on; bad modes raise."""
     agg = ShardedAggregator(fold=_oracle_fold, device_ident="gfx950:256")
