@@ -38,6 +38,9 @@ case "${1:-lines}" in
      "c3r_loop_one:300:python3 bench.py --rccl-world1 $C3R --step-mode one --step-impl loop" \
      "c3r_prod_per:300:python3 bench.py --rccl-world1 $C3R --step-mode per-round" \
      "decomp_c3:300:python3 tools/peer_step_decomp.py --config c3 --steps 5 --only fold_agent,product_rccl,product_sync" ;;
+  hops)  # what the bench's per-fold events and the caller-stream hops add to the product step
+    scripts/gpu_steps.sh "hops_c4:300:python3 tools/peer_step_decomp.py --config c4 --only fold_agent,product_rccl,product_per,product_rccl_traced,product_per_traced,product_rccl_dflt,product_per_dflt" \
+     "hops_c3:300:python3 tools/peer_step_decomp.py --config c3 --steps 5 --only fold_agent,product_rccl,product_per,product_rccl_traced,product_per_traced,product_rccl_dflt,product_per_dflt" ;;
   trace)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/tr_peer" \

@@ -21,6 +21,11 @@ median of --reps interleaved repetitions.
   product_rccl     ShardedAggregator(one_launch=True) at world 1 (the rounds'
                    self-copies behind their waits), check="deferred"
   product_sync     product_rccl with check="sync" (a host wait per call)
+  product_per      ShardedAggregator(one_launch=False): per-round launches
+  *_traced         product_rccl / product_per with .trace on (bench.py's timing
+                   events around every fold launch, the cost they add)
+  *_dflt           product_rccl / product_per called from the default stream
+                   (the class hops onto the fold stream and back: the hops' cost)
 
 The same command under `rocprofv3 --kernel-trace --memory-copy-trace` names
 the engine that moves each copy (a blit kernel in the kernel trace, or an
@@ -93,7 +98,13 @@ def main():
     full = torch.empty(lay.padded_total, dtype=odt, device=dev)
     aggs = {"product_peer": ShardedAggregator(one_launch=True, exchange="peer_copy", check="deferred"),
             "product_rccl": ShardedAggregator(one_launch=True, check="deferred"),
-            "product_sync": ShardedAggregator(one_launch=True, check="sync")}
+            "product_sync": ShardedAggregator(one_launch=True, check="sync"),
+            "product_per": ShardedAggregator(one_launch=False, check="deferred")}
+    for n in ("product_rccl", "product_per"):
+        for sfx in ("_traced", "_dflt"):
+            aggs[n + sfx] = ShardedAggregator(one_launch=n == "product_rccl", check="deferred")
+            if sfx == "_traced":
+                aggs[n + sfx].trace = []
 
     def run(name):
         if name in ("fold_agent", "fold_sys", "fold_sys_fence"):
@@ -104,12 +115,15 @@ def main():
         elif name == "peer_step":
             px.step(X, w, None, full, None, fs, gs)
             fs.wait_stream(gs)
+        elif name.endswith("_dflt"):
+            aggs[name].aggregate_slots(X, w, None, lay, out=full)
         else:
             with torch.cuda.stream(fs):
                 aggs[name].aggregate_slots(X, w, None, lay, out=full)
 
     names = ["fold_agent", "fold_sys", "fold_sys_fence", "self_copy", "peer_step", "product_peer", "product_rccl",
-             "product_sync"]
+             "product_sync", "product_per", "product_rccl_traced", "product_per_traced", "product_rccl_dflt",
+             "product_per_dflt"]
     if args.only:
         names = [n for n in names if n in args.only.split(",")]
     for n in names:  # warm-up (first launches, the tuner's per-round shapes, buffers)
@@ -133,6 +147,8 @@ def main():
             e1.record(fs)
             e1.synchronize()
             res[n].append(e0.elapsed_time(e1) / args.steps)
+            if n.endswith("_traced"):
+                aggs[n].trace.clear()
     # every product / peer model equals the agent-scope fold's output, bit for bit
     fold(0)
     torch.cuda.synchronize()
