@@ -27,7 +27,7 @@ BENCH_LIB_PATH = os.path.join(PKG, "_native", "libfedavg_hip_bench.so")
 HOSTFAST_PATH = os.path.join(PKG, "_native", "_hostfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HEADER = os.path.join(REPO, "include", "fedavg_hip.h")
 BENCH_HEADER = os.path.join(REPO, "include", "fedavg_hip_bench.h")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FA_OK, FA_ERR_ARG, FA_ERR_NO_CLIENTS, FA_ERR_SHAPE, FA_ERR_HIP = range(5)
 
@@ -47,6 +47,7 @@ _PROTOS = {
     "fa_fedavg_f32_hostf": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fedavg_f32_ptrs_hostf": (_int, [_vp, _i64, _i64, _vp, _vp, _f32, _int, _vp, _vp]),
     "fa_fedavg_bf16_hostf": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
+    "fa_factors_fill": (_int, [_vp, _vp, _vp, _i64, _vp]),
     "fa_fedavg_f32_splitn": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _f32, _vp, _vp]),
     "fa_fold_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _f32, _int, _vp, _vp]),
     "fa_accumulate_f32": (_int, [_vp, _vp, _f32, _f32, _int, _i64, _vp]),

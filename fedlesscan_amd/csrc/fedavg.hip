@@ -45,38 +45,19 @@ FactorRing g_factor_rings[16];
 
 // Under a HIP graph capture the ring cannot be used (waiting for a slot's
 // event is not allowed while a stream captures, and a captured copy would read
-// the slot again at every replay, after later calls rewrote it): the factors
-// become kernel arguments of fill kernels -- captured by value -- that write a
-// stream-ordered allocation of the graph, freed after the fold.
-constexpr int kFillFloats = 480;
+// the slot again at every replay, after later calls rewrote it), and the
+// library owns no memory that lives as long as a graph: the *_hostf entries
+// refuse capture, and a capturing caller stages the factors with
+// fa_factors_fill -- fill kernels whose arguments carry the values, captured by
+// value -- into memory the graph owns, then calls the device-factor entry.
+// (Round 6 staged them here in a stream-ordered allocation of the graph; a
+// replay inside the full GPU suite read part of it as zeros.)
+constexpr int kFillFloats = 256;
 struct FillArgs {
     float v[kFillFloats];
 };
 __global__ __launch_bounds__(64) void k_fill_factors(float* dst, FillArgs f, int n) {
     for (int i = threadIdx.x; i < n; i += 64) dst[i] = f.v[i];
-}
-
-template <class Launch>
-int with_captured_factors(const float* a, const float* s, int64_t N, hipStream_t st, Launch launch) {
-    const int64_t need = N * (s ? 2 : 1);
-    float* d = nullptr;
-    hipError_t e = hipMallocAsync((void**)&d, (size_t)need * sizeof(float), st);
-    if (e != hipSuccess) return fail(FA_ERR_HIP, "captured factors: hipMallocAsync: %s", hipGetErrorString(e));
-    for (int64_t off = 0; off < need; off += kFillFloats) {
-        FillArgs f;
-        const int n = (int)(need - off < kFillFloats ? need - off : kFillFloats);
-        for (int i = 0; i < n; ++i) {
-            const int64_t j = off + i;
-            f.v[i] = j < N ? a[j] : s[j - N];
-        }
-        hipLaunchKernelGGL(k_fill_factors, dim3(1), dim3(64), 0, st, d + off, f, n);
-        const int rc = check_launch("captured factors");
-        if (rc) return rc;
-    }
-    const int rc = launch((const float*)d, s ? (const float*)(d + N) : (const float*)nullptr);
-    e = hipFreeAsync(d, st);
-    if (e != hipSuccess && !rc) return fail(FA_ERR_HIP, "captured factors: hipFreeAsync: %s", hipGetErrorString(e));
-    return rc;
 }
 
 // Stage a[0..N) (and s[0..N) when s != NULL) and run launch(a_dev, s_dev) on
@@ -88,10 +69,9 @@ int with_host_factors(const float* a, const float* s, int64_t N, void* stream, L
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) (void)hipGetLastError();
-        else if (cs != hipStreamCaptureStatusNone) {
-            StreamDevice on_stream_device(stream);
-            return with_captured_factors(a, s, N, (hipStream_t)stream, launch);
-        }
+        else if (cs != hipStreamCaptureStatusNone)
+            return fail(FA_ERR_ARG, "host factors under graph capture: stage them with fa_factors_fill into memory "
+                                    "the graph owns and call the device-factor entry");
     }
     // the slot (and its device buffer) of the GPU that owns the stream, not of
     // the calling thread's current device
@@ -496,6 +476,24 @@ int fa_fedavg_i64(const int64_t* X, int64_t N, int64_t P, int64_t ldx, const int
 }
 
 // ---- the same folds with the per-client factors in host memory ---------------
+int fa_factors_fill(float* dst, const float* a, const float* s, int64_t N, void* stream) {
+    if (N < 0 || (N > 0 && (!dst || !a))) return fail(FA_ERR_ARG, "fa_factors_fill: N %lld, null pointer", (long long)N);
+    StreamDevice on_stream_device(stream);
+    const int64_t need = N * (s ? 2 : 1);
+    for (int64_t off = 0; off < need; off += kFillFloats) {
+        FillArgs f;
+        const int n = (int)(need - off < kFillFloats ? need - off : kFillFloats);
+        for (int i = 0; i < n; ++i) {
+            const int64_t j = off + i;
+            f.v[i] = j < N ? a[j] : s[j - N];
+        }
+        hipLaunchKernelGGL(k_fill_factors, dim3(1), dim3(64), 0, (hipStream_t)stream, dst + off, f, n);
+        const int rc = check_launch("fa_factors_fill");
+        if (rc) return rc;
+    }
+    return FA_OK;
+}
+
 int fa_fedavg_f32_hostf(const float* X, int64_t N, int64_t P, int64_t ldx, const float* a, const float* s,
                         float divisor, float* out, void* stream) {
     return with_host_factors(a, s, N, stream, [&](const float* ad, const float* sd) {

@@ -216,6 +216,17 @@ class Factors:
         return staged[0], (staged[1] if self.s is not None else None)
 
 
+def _captured_factors(f: Factors, dev) -> tuple:
+    """Under a HIP graph capture: the float32 factors (a, s or None) in a
+    tensor allocated inside the capture -- memory the graph owns -- written by
+    fill kernels that carry the values in their arguments (fa_factors_fill),
+    for the device-factor entries; the _hostf entries refuse capture."""
+    n = len(f.a)
+    buf = torch.empty(n * (1 if f.s is None else 2), dtype=torch.float32, device=dev)
+    _lib.call("fa_factors_fill", buf.data_ptr(), *f.host(), n, stream_ptr(dev))
+    return buf[:n], (None if f.s is None else buf[n:])
+
+
 def _check_matrix(X: torch.Tensor) -> tuple[int, int, int]:
     if not X.is_cuda:
         raise ValueError("X must be a CUDA (HIP) tensor")
@@ -260,8 +271,13 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
             outb = torch.empty(P, dtype=torch.bfloat16, device=dev) if want_bf16 else None
         if out is None and (outb is None or want_bf16):
             out = torch.empty(P, dtype=torch.float32, device=dev)
-        _lib.call("fa_fedavg_bf16_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div),
-                  _ptr(out), _ptr(outb), st)
+        if torch.cuda.is_current_stream_capturing():
+            a, s = _captured_factors(f, dev)
+            _lib.call("fa_fedavg_bf16", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                      _ptr(out), _ptr(outb), st)
+        else:
+            _lib.call("fa_fedavg_bf16_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div),
+                      _ptr(out), _ptr(outb), st)
         if want_bf16:
             return out, outb
         if out_bf16 is not None:
@@ -296,6 +312,10 @@ def fold_stacked(X: torch.Tensor, weights: Sequence, scores: Optional[Sequence] 
         if split:
             a, s = f.to(dev)
             _lib.call("fa_fedavg_f32_splitn", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
+                      out.data_ptr(), st)
+        elif torch.cuda.is_current_stream_capturing():
+            a, s = _captured_factors(f, dev)
+            _lib.call("fa_fedavg_f32", X.data_ptr(), N, P, ldx, a.data_ptr(), _ptr(s), float(f.div),
                       out.data_ptr(), st)
         else:  # factors from host memory: the library stages them (one C call)
             _lib.call("fa_fedavg_f32_hostf", X.data_ptr(), N, P, ldx, *f.host(), float(f.div), out.data_ptr(), st)
@@ -555,8 +575,13 @@ def fold_rows(rows, weights: Sequence, scores: Optional[Sequence] = None, *,
         out = None
     out = out if out is not None else torch.empty(rs.P, dtype=torch.float32, device=dev)
     aligned = rs.aligned and out.data_ptr() % 16 == 0
-    _lib.call("fa_fedavg_f32_ptrs_hostf", rs.ptrs.data_ptr(), rs.N, rs.P, *f.host(), float(f.div), int(aligned),
-              out.data_ptr(), stream_ptr(dev))
+    if torch.cuda.is_current_stream_capturing():
+        a, s = _captured_factors(f, dev)
+        _lib.call("fa_fedavg_f32_ptrs_aligned" if aligned else "fa_fedavg_f32_ptrs", rs.ptrs.data_ptr(), rs.N, rs.P,
+                  a.data_ptr(), _ptr(s), float(f.div), out.data_ptr(), stream_ptr(dev))
+    else:
+        _lib.call("fa_fedavg_f32_ptrs_hostf", rs.ptrs.data_ptr(), rs.N, rs.P, *f.host(), float(f.div),
+                  int(aligned), out.data_ptr(), stream_ptr(dev))
     if dst is not None and dst is not out:
         dst.copy_(out)
         return dst

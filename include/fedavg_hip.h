@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 5
+#define FA_ABI_VERSION 6
 
 enum fa_status {
     FA_OK = 0,
@@ -235,6 +235,13 @@ int fa_fedavg_f32_ptrs_hostf(const float* const* xi, int64_t N, int64_t P,
 int fa_fedavg_bf16_hostf(const uint16_t* X, int64_t N, int64_t P, int64_t ldx,
                          const float* a, const float* s, float divisor,
                          float* out_f32, uint16_t* out_bf16, void* stream);
+/* The _hostf entries refuse a capturing stream (FA_ERR_ARG, ABI 6): a graph
+ * would have to own the staged copy.  Under capture, write the factors into
+ * memory the graph owns (PyTorch: a tensor allocated inside the capture) with
+ * fa_factors_fill -- dst[0..N) = a, then dst[N..2N) = s when s != NULL, by
+ * kernels whose arguments carry the values, so replays need no host memory --
+ * and call the device-factor entry (fa_fedavg_f32, fa_fedavg_bf16, ...). */
+int fa_factors_fill(float* dst, const float* a, const float* s, int64_t N, void* stream);
 /* The one-launch step with host factors (ABI 5): as fa_fedavg_*_rounds, the
  * factors staged by the library like the folds above (one C call per step). */
 int fa_fedavg_f32_rounds_hostf(fa_rounds* r, const float* X, int64_t N, int64_t ldx,

@@ -41,6 +41,8 @@ case "${1:-lines}" in
   hops)  # what the bench's per-fold events and the caller-stream hops add to the product step
     scripts/gpu_steps.sh "hops_c4:300:python3 tools/peer_step_decomp.py --config c4 --only fold_agent,product_rccl,product_per,product_rccl_traced,product_per_traced,product_rccl_dflt,product_per_dflt" \
      "hops_c3:300:python3 tools/peer_step_decomp.py --config c3 --steps 5 --only fold_agent,product_rccl,product_per,product_rccl_traced,product_per_traced,product_rccl_dflt,product_per_dflt" ;;
+  capture)  # captured graphs replayed over fresh rows
+    scripts/gpu_steps.sh "t_capture:300:$T tests/test_gpu_sharding.py -k 'captured_graph or captures_into'" ;;
   trace)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/tr_peer" \

@@ -1046,6 +1046,46 @@ def test_fold_captures_into_hip_graph(dev, lib, N, P):
         assert _bits_equal(out.cpu().numpy(), exp)
 
 
+def test_host_factor_entries_refuse_capture_fill_is_captured_by_value(dev, lib):
+    """ABI 6: a _hostf entry on a capturing stream is an argument error (a
+    graph would have to own the staged copy), not a launch; fa_factors_fill
+    writes a, then s, into memory the graph owns by kernels that carry the
+    values, so the replays fold with the captured factors after the caller's
+    host arrays changed (the stall-aware fold, bit-exact)."""
+    L = lib.load()
+    N, P = 300, 4099
+    X = torch.from_numpy(synth.clients_f32(81, N, 0, P)).to(dev)
+    w = np.array(synth.cardinalities(81, N), np.float32)
+    sc = np.linspace(0.25, 1.0, N, dtype=np.float32)
+    w0, sc0 = w.copy(), sc.copy()
+    div = float(np.float32(w.sum(dtype=np.float64)))
+    out = _sentinel(P, dev)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rc_h = L.fa_fedavg_f32_hostf(X.data_ptr(), N, P, P, w.ctypes.data, None, div, out.data_ptr(), s.cuda_stream)
+        msg = lib.last_error()
+        buf = torch.empty(2 * N, dtype=torch.float32, device=dev)
+        rc_f = L.fa_factors_fill(buf.data_ptr(), w.ctypes.data, sc.ctypes.data, N, s.cuda_stream)
+        rc_k = L.fa_fedavg_f32(X.data_ptr(), N, P, P, buf.data_ptr(), buf.data_ptr() + 4 * N, div, out.data_ptr(),
+                               s.cuda_stream)
+    assert rc_h == lib.FA_ERR_ARG and "capture" in msg, msg
+    assert rc_f == 0 and rc_k == 0, lib.last_error()
+    w[:] = 0
+    sc[:] = 0
+    exp = OL.fedavg_f32(X.cpu().numpy(), w0, np.float32(div), sc0)
+    for _ in range(3):
+        out.fill_(float("nan"))
+        buf.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), np.concatenate([w0, sc0]))
+        assert _bits_equal(out.cpu().numpy(), exp)
+    assert L.fa_factors_fill(None, w.ctypes.data, None, 4, s.cuda_stream) == lib.FA_ERR_ARG
+    assert L.fa_factors_fill(None, None, None, 0, s.cuda_stream) == 0
+
+
 def test_openfaas_entry_point_on_gpu(dev):
     """The FaaS entry point end to end on the HIP fold: request JSON in,
     response JSON out, the saved round+1 model bit-exact vs the oracle."""

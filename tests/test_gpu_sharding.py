@@ -329,6 +329,49 @@ def test_aggregate_slots_captures_into_hip_graph(one_launch, bf16):
         assert np.array_equal(got, exp), seed
 
 
+@pytest.mark.parametrize("what", ["step", "fold"])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_captured_graph_replays_stay_exact(what, bf16):
+    """A captured step (aggregate_slots: per-round launches) or a captured
+    fold_stacked, replayed 40 times over fresh client rows, equals the eager
+    call on the same rows every time (the captured factors live in memory the
+    graph owns)."""
+    from fedlesscan_amd import engine
+    from fedlesscan_amd.sharding import ShardedAggregator, SlotLayout
+    dev = torch.device("cuda", 0)
+    N, P = 24, 100_003
+    lay = SlotLayout(P, 1, 4)
+    Xin, w, sc, _ = _slots_input(bf16, N, P, 61, lay, dev)
+    if what == "fold":
+        Xin = Xin[:, :25_001]
+    agg, eager = ShardedAggregator(one_launch=True), ShardedAggregator(one_launch=False)
+
+    def run(a):
+        if what == "step":
+            return a.aggregate_slots(Xin, w, sc, lay)
+        return engine.fold_stacked(Xin, w, sc, out_bf16=torch.empty(Xin.shape[1], dtype=torch.bfloat16, device=dev)) \
+            if bf16 else engine.fold_stacked(Xin, w, sc)
+
+    run(agg)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        full = run(agg)
+    iv = torch.int16 if bf16 else torch.int32
+    gen = torch.Generator(device=dev)
+    bad = []
+    for i in range(40):
+        gen.manual_seed(100 + i)
+        Xin.copy_(torch.randn(Xin.shape, generator=gen, device=dev, dtype=torch.float32).to(Xin.dtype))
+        g.replay()
+        exp = run(eager)
+        torch.cuda.synchronize()
+        diff = (full.view(iv) != exp.view(iv)).nonzero()
+        if diff.numel():
+            bad.append((i, int(diff.numel()), int(diff[0]), int(diff[-1]), int((full.view(iv)[diff] == 0).sum())))
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("one_launch", [True, False])
 @pytest.mark.parametrize("bf16", [False, True])
 def test_quantised_layout_world1(one_launch, bf16):
