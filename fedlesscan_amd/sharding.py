@@ -262,19 +262,24 @@ class PeerExchange:
         self.layout, self.bf16 = layout, bf16
         eb = 2 if bf16 else 4
         send_bytes = self.send_bytes = -(-layout.local_width * eb // 16) * 16
+        self.h = None
         h = ctypes.c_void_p()
         _lib.call("fa_peers_create", ctypes.byref(h), self.device.index, self.world, self.rank, send_bytes)
+        try:
+            nb = L.fa_peers_handle_bytes()
+            mine = (ctypes.c_uint8 * nb)()
+            _lib.call("fa_peers_handle", h, mine)
+            if self.world > 1:
+                every = [None] * self.world
+                dist.all_gather_object(every, bytes(mine), group=group)
+            else:
+                every = [bytes(mine)]
+            joined = b"".join(every)
+            _lib.call("fa_peers_open", h, ctypes.create_string_buffer(joined, len(joined)))
+        except BaseException:
+            L.fa_peers_destroy(h)  # what was opened is closed with it
+            raise
         self.h = h
-        nb = L.fa_peers_handle_bytes()
-        mine = (ctypes.c_uint8 * nb)()
-        _lib.call("fa_peers_handle", h, mine)
-        if self.world > 1:
-            every = [None] * self.world
-            dist.all_gather_object(every, bytes(mine), group=group)
-        else:
-            every = [bytes(mine)]
-        joined = b"".join(every)
-        _lib.call("fa_peers_open", h, ctypes.create_string_buffer(joined, len(joined)))
         self.state = ctypes.c_void_p(L.fa_peers_rounds(h))
         R = layout.rounds
         self.offsets = [layout.offset(k) for k in range(R + 1)]
